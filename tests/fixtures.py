@@ -1,0 +1,27 @@
+"""Loads the reference's example systems (tests/golden/*.npz, data only) and cuts the blocks
+exactly as the examples do: Q = K(1:n,1:n); G = diag(diag(Q)); A = K(n+1:end,1:n);
+C = -K(n+1:end,n+1:end)  (examples/cpk_exprog1.m:59-64, cpk_exprog2.m:179-184), and the
+options of the examples (cpk_exprog1.m:79-90, cpk_exprog2.m:188-208)."""
+import os
+
+import numpy as np
+import scipy.sparse as sp
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+EXPROG_OPTS = dict(print=False, atol=1.0e-6, rtol=1.0e-6, itmax=500,
+                   residual_update=True, nitref=1, force_itref=True, itref_tol=1.0e-8)
+
+
+def load(name):
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False)
+    n, m = int(z["n"]), int(z["m"])
+    K = sp.csr_matrix((z["K_data"], z["K_indices"], z["K_indptr"]), shape=(n + m, n + m))
+    Q = K[:n, :n].tocsr()
+    G = sp.diags(Q.diagonal()).tocsr()
+    A = K[n:, :n].tocsr()
+    Cm = (-K[n:, n:]).tocsr()
+    for M in (Q, G, A, Cm):
+        M.sort_indices()
+    return dict(name=name, n=n, m=m, K=K, Q=Q, G=G, B=A, C=Cm, rhs=z["rhs"].copy(),
+                x_direct=z["x_direct"].copy())
