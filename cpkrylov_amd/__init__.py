@@ -1,0 +1,11 @@
+"""cpkrylov_amd -- MI355X-native constraint-preconditioned Krylov solvers (HIP/CDNA4).
+
+Drop-in for the hot path of optimizers/cpkrylov: reg_cpkrylov + cp{cg,cglanczos,minres,
+symmlq,gmres,dqgmres} + the opLDL2 preconditioner operator.  See DESIGN.md.
+"""
+from ._lib import CpkError, IndefiniteError, LIB_PATH  # noqa: F401  (raises if libcpk.so is missing)
+from .api import (Context, Matrix, SymGivens, analyze, cpcg, cpcglanczos, cpdqgmres, cpgmres,  # noqa: F401
+                  cpminres, cpsymmlq, default_context, get_unique_id, opLDL2, reg_cpkrylov)
+
+__all__ = ["reg_cpkrylov", "cpcg", "cpcglanczos", "cpminres", "cpsymmlq", "cpgmres", "cpdqgmres", "opLDL2",
+           "SymGivens", "Context", "Matrix", "analyze", "CpkError", "IndefiniteError", "get_unique_id"]

@@ -1,0 +1,445 @@
+// capi.cpp -- the extern "C" boundary of libcpk (include/cpk.h).  Every entry point converts
+// C++ exceptions into a cpk_status code plus a thread-local message.
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <new>
+#include <string>
+
+#include "cpk.h"
+#include "dev.hpp"
+#include "solvers.hpp"
+
+using namespace cpk;
+
+struct cpk_ctx_s {
+    Ctx c;
+};
+
+struct cpk_mat_s {
+    cpk_ctx_s *ctx = nullptr;
+    uint64_t gen = 0;
+    HCsr h;
+    std::unique_ptr<DMat> d;                          // lazily uploaded
+    std::map<uint64_t, std::unique_ptr<DMat>> ac;     // blkdiag(this, C) keyed by C's generation
+    const DMat &dev() {
+        if (!ctx) throw Error(CPK_ERR_ARGS, "host-only matrix (created with ctx == NULL) used on the device");
+        if (!d) {
+            d = std::make_unique<DMat>();
+            make_dmat(h, *d);
+        }
+        return *d;
+    }
+    const DMat &blkdiag_with(cpk_mat_s *C) {
+        if (!ctx) throw Error(CPK_ERR_ARGS, "host-only matrix (created with ctx == NULL) used on the device");
+        auto it = ac.find(C->gen);
+        if (it == ac.end()) {
+            auto m = std::make_unique<DMat>();
+            make_dmat(blkdiag(h, C->h), *m);
+            it = ac.emplace(C->gen, std::move(m)).first;
+        }
+        return *it->second;
+    }
+};
+
+struct cpk_analysis_s {
+    Analysis an;
+};
+
+struct cpk_pc_s {
+    cpk_ctx_s *ctx = nullptr;
+    std::unique_ptr<Precond> p;
+};
+
+static thread_local std::string g_err;
+static uint64_t g_gen = 1;
+
+#define API_BEGIN try {
+#define API_END                                                  \
+    }                                                            \
+    catch (const Error &e) {                                     \
+        g_err = e.what();                                        \
+        return e.code;                                           \
+    }                                                            \
+    catch (const std::bad_alloc &) {                             \
+        g_err = "out of host memory";                            \
+        return CPK_ERR_NOMEM;                                    \
+    }                                                            \
+    catch (const std::exception &e) {                            \
+        g_err = e.what();                                        \
+        return CPK_ERR_ARGS;                                     \
+    }                                                            \
+    return CPK_OK;
+
+static void need(bool cond, const char *msg) {
+    if (!cond) throw Error(CPK_ERR_ARGS, msg);
+}
+
+template <class T>
+static void h2d(DBuf<T> &d, const T *h, size_t n) {
+    d.alloc(n);
+    if (n) CPK_HIP(hipMemcpy(d.p, h, n * sizeof(T), hipMemcpyHostToDevice));
+}
+
+extern "C" {
+
+const char *cpk_last_error(void) { return g_err.c_str(); }
+int cpk_abi_version(void) { return CPK_ABI_VERSION; }
+
+int cpk_get_unique_id(unsigned char id[128]) {
+    API_BEGIN
+    need(id != nullptr, "id is NULL");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) throw Error(CPK_ERR_RCCL, "ncclGetUniqueId failed");
+    std::memcpy(id, &u, 128);
+    API_END
+}
+
+int cpk_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id, cpk_ctx *out) {
+    API_BEGIN
+    need(out != nullptr, "out is NULL");
+    need(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
+    auto ctx = std::make_unique<cpk_ctx_s>();
+    Ctx &c = ctx->c;
+    if (device >= 0) CPK_HIP(hipSetDevice(device));
+    CPK_HIP(hipGetDevice(&c.device));
+    c.rank = rank, c.nranks = nranks;
+    CPK_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    CPK_HIP(hipEventCreate(&c.ev0));
+    CPK_HIP(hipEventCreate(&c.ev1));
+    c.ensure_partials(4096);
+    if (nranks > 1) {
+        need(unique_id != nullptr, "unique_id required when nranks > 1");
+        ncclUniqueId u;
+        std::memcpy(&u, unique_id, 128);
+        ncclComm_t comm;
+        if (ncclCommInitRank(&comm, nranks, u, rank) != ncclSuccess) throw Error(CPK_ERR_RCCL, "ncclCommInitRank failed");
+        c.comm = comm;
+    }
+    *out = ctx.release();
+    API_END
+}
+
+int cpk_ctx_destroy(cpk_ctx ctx) {
+    API_BEGIN
+    if (!ctx) return CPK_OK;
+    Ctx &c = ctx->c;
+    (void)hipStreamSynchronize(c.stream);
+    if (c.comm) ncclCommDestroy((ncclComm_t)c.comm);
+    c.partials.release();
+    c.counter.release();
+    (void)hipEventDestroy(c.ev0);
+    (void)hipEventDestroy(c.ev1);
+    (void)hipStreamDestroy(c.stream);
+    delete ctx;
+    API_END
+}
+
+int cpk_ctx_synchronize(cpk_ctx ctx) {
+    API_BEGIN
+    need(ctx, "ctx is NULL");
+    CPK_HIP(hipStreamSynchronize(ctx->c.stream));
+    API_END
+}
+
+int cpk_mat_create_csc(cpk_ctx ctx, int64_t nrows, int64_t ncols, const size_t *jc, const size_t *ir,
+                       const double *pr, cpk_mat *out) {
+    API_BEGIN
+    need(out != nullptr, "NULL argument");
+    auto m = std::make_unique<cpk_mat_s>();
+    m->ctx = ctx;
+    m->gen = g_gen++;
+    m->h = csr_from_csc(nrows, ncols, jc, ir, pr);
+    *out = m.release();
+    API_END
+}
+
+int cpk_mat_create_csr(cpk_ctx ctx, int64_t nrows, int64_t ncols, const int64_t *rowptr, const int32_t *colind,
+                       const double *val, cpk_mat *out) {
+    API_BEGIN
+    need(out != nullptr, "NULL argument");
+    auto m = std::make_unique<cpk_mat_s>();
+    m->ctx = ctx;
+    m->gen = g_gen++;
+    m->h = csr_from_csr(nrows, ncols, rowptr, colind, val);
+    *out = m.release();
+    API_END
+}
+
+int cpk_mat_destroy(cpk_mat A) {
+    API_BEGIN
+    delete A;
+    API_END
+}
+
+int cpk_mat_spmv(cpk_mat A, const double *x, double *y) {
+    API_BEGIN
+    need(A && (x || !A->h.ncols) && (y || !A->h.nrows), "NULL argument");
+    Ctx &c = A->ctx->c;
+    const DMat &d = A->dev();
+    DBuf<double> dx, dy;
+    h2d(dx, x, (size_t)A->h.ncols);
+    dy.alloc((size_t)A->h.nrows);
+    launch_spmv(c, d, dx.p, dy.p, nullptr);
+    if (A->h.nrows) CPK_HIP(hipMemcpyAsync(y, dy.p, A->h.nrows * sizeof(double), hipMemcpyDeviceToHost, c.stream));
+    CPK_HIP(hipStreamSynchronize(c.stream));
+    API_END
+}
+
+int cpk_pc_create(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptime, cpk_pc *out) {
+    API_BEGIN
+    need(ctx && A11 && B && C22 && out, "opLDL2: Invalid number of arguments.");
+    auto pc = std::make_unique<cpk_pc_s>();
+    pc->ctx = ctx;
+    pc->p.reset(precond_create(ctx->c, A11->h, B->h, C22->h));
+    if (ptime) *ptime = pc->p->ptime;
+    *out = pc.release();
+    API_END
+}
+
+int cpk_pc_destroy(cpk_pc M) {
+    API_BEGIN
+    delete M;
+    API_END
+}
+
+static double matlab_round(double v) { return v < 0 ? -std::floor(-v + 0.5) : std::floor(v + 0.5); }
+
+// opLDL2 setters (ops/opLDL2.m:97-115)
+static void apply_props(Precond &p, const cpk_opts *o) {
+    if (!o) return;
+    if (o->has_nitref) p.nitref = std::max(0.0, matlab_round(o->nitref));
+    if (o->has_itref_tol) p.itref_tol = o->itref_tol;  // `sef.itref_tol` typo: no clamp in effect
+    if (o->has_residual_update) p.residual_update = o->residual_update;
+    if (o->has_force_itref) p.force_itref = (o->force_itref != 0 && o->force_itref != 1) ? 0.0 : o->force_itref;
+}
+
+int cpk_pc_set(cpk_pc M, const cpk_opts *opts) {
+    API_BEGIN
+    need(M && opts, "NULL argument");
+    apply_props(*M->p, opts);
+    API_END
+}
+
+int cpk_pc_get(cpk_pc M, double *nitref, double *itref_tol, double *force_itref, double *residual_update) {
+    API_BEGIN
+    need(M, "NULL argument");
+    if (nitref) *nitref = M->p->nitref;
+    if (itref_tol) *itref_tol = M->p->itref_tol;
+    if (force_itref) *force_itref = M->p->force_itref;
+    if (residual_update) *residual_update = M->p->residual_update;
+    API_END
+}
+
+int cpk_pc_apply(cpk_pc M, const double *x, double *y) {
+    API_BEGIN
+    need(M && x && y, "NULL argument");
+    Precond &p = *M->p;
+    Ctx &c = M->ctx->c;
+    DBuf<double> dx, dy;
+    h2d(dx, x, (size_t)p.N);
+    dy.alloc((size_t)p.N);
+    p.apply(dx.p, p.N, dy.p, nullptr);
+    CPK_HIP(hipMemcpyAsync(y, dy.p, p.N * sizeof(double), hipMemcpyDeviceToHost, c.stream));
+    CPK_HIP(hipStreamSynchronize(c.stream));
+    API_END
+}
+
+int cpk_pc_apply_device(cpk_pc M, const double *d_x, double *d_y) {
+    API_BEGIN
+    need(M && d_x && d_y, "NULL argument");
+    M->p->apply(d_x, M->p->N, d_y, nullptr);
+    API_END
+}
+
+int cpk_pc_divide(cpk_pc M, const double *b, double *x) {
+    API_BEGIN
+    need(M && b && x, "NULL argument");
+    Precond &p = *M->p;
+    Ctx &c = M->ctx->c;
+    DBuf<double> db, dx;
+    h2d(db, b, (size_t)p.N);
+    dx.alloc((size_t)p.N);
+    launch_spmv(c, p.dKp, db.p, dx.p, nullptr);
+    CPK_HIP(hipMemcpyAsync(x, dx.p, p.N * sizeof(double), hipMemcpyDeviceToHost, c.stream));
+    CPK_HIP(hipStreamSynchronize(c.stream));
+    API_END
+}
+
+int cpk_pc_get_info(cpk_pc M, cpk_pc_info *info) {
+    API_BEGIN
+    need(M && info, "NULL argument");
+    const Precond &p = *M->p;
+    info->n = p.n, info->m = p.m, info->N = p.N;
+    info->nnz_kp = p.Kp.nnz();
+    info->nnz_l = (int64_t)p.F.Li.size();
+    info->nblocks = (int64_t)p.S.blk_row.size() - 1;
+    info->nrounds = (int64_t)p.S.round_ptr.size() - 1;
+    info->max_block_levels = p.S.max_levels;
+    info->depth = p.S.depth;
+    info->ordering = p.ordering;
+    API_END
+}
+
+int cpk_pc_export(cpk_pc M, int64_t *Lcolptr, int32_t *Lrowind, double *Lval, double *D, int32_t *perm) {
+    API_BEGIN
+    need(M, "NULL argument");
+    const Factor &f = M->p->F;
+    if (Lcolptr) std::memcpy(Lcolptr, f.Lp.data(), f.Lp.size() * sizeof(int64_t));
+    if (Lrowind) std::memcpy(Lrowind, f.Li.data(), f.Li.size() * sizeof(int32_t));
+    if (Lval) std::memcpy(Lval, f.Lx.data(), f.Lx.size() * sizeof(double));
+    if (D) std::memcpy(D, f.D.data(), f.D.size() * sizeof(double));
+    if (perm) std::memcpy(perm, f.perm.data(), f.perm.size() * sizeof(int32_t));
+    API_END
+}
+
+static void check_method_dims(cpk_mat A, cpk_mat C, cpk_pc M) {
+    need(A && C && M, "NULL argument");
+    if (A->h.nrows != A->h.ncols || C->h.nrows != C->h.ncols) throw Error(CPK_ERR_DIM, "A and C must be square");
+    if (A->h.nrows != M->p->n || C->h.nrows != M->p->m) throw Error(CPK_ERR_DIM, "A, C and M dimensions disagree");
+}
+
+int cpk_method_solve_device(cpk_ctx ctx, int method, const double *d_b, cpk_mat A, cpk_mat C, cpk_pc M,
+                            const cpk_opts *opts, double *d_xy, cpk_stats *stats) {
+    API_BEGIN
+    need(ctx && d_xy && (d_b || !A->h.nrows), "NULL argument");
+    check_method_dims(A, C, M);
+    const DMat &AC = A->blkdiag_with(C);
+    method_solve_device(ctx->c, method, d_b, AC, *M->p, opts, d_xy, stats);
+    API_END
+}
+
+int cpk_method_solve(cpk_ctx ctx, int method, const double *b, cpk_mat A, cpk_mat C, cpk_pc M, const cpk_opts *opts,
+                     double *x, double *y, cpk_stats *stats) {
+    API_BEGIN
+    need(ctx && b && x && (y || !C->h.nrows), "NULL argument");
+    check_method_dims(A, C, M);
+    Ctx &c = ctx->c;
+    const int64_t n = M->p->n, m = M->p->m, N = n + m;
+    const DMat &AC = A->blkdiag_with(C);
+    DBuf<double> db, dxy;
+    h2d(db, b, (size_t)n);
+    dxy.alloc((size_t)N);
+    auto t0 = std::chrono::steady_clock::now();
+    method_solve_device(c, method, db.p, AC, *M->p, opts, dxy.p, stats);
+    CPK_HIP(hipMemcpy(x, dxy.p, n * sizeof(double), hipMemcpyDeviceToHost));
+    if (m) CPK_HIP(hipMemcpy(y, dxy.p + n, m * sizeof(double), hipMemcpyDeviceToHost));
+    if (stats) stats->stime = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    API_END
+}
+
+int cpk_reg_solve_device(cpk_ctx ctx, int method, const double *d_b, cpk_mat A, cpk_mat B, cpk_mat C, cpk_pc M,
+                         const cpk_opts *opts, double *d_x, cpk_stats *stats) {
+    API_BEGIN
+    need(ctx && d_b && d_x && B, "NULL argument");
+    check_method_dims(A, C, M);
+    const DMat &AC = A->blkdiag_with(C);
+    reg_solve_device(ctx->c, method, d_b, AC, M->p->dKp, *M->p, opts, d_x, stats);
+    if (stats) stats->ptime = M->p->ptime;
+    API_END
+}
+
+int cpk_reg_solve(cpk_ctx ctx, int method, const double *b, cpk_mat A, cpk_mat B, cpk_mat C, cpk_mat G,
+                  const cpk_opts *opts, double *x, cpk_stats *stats, cpk_pc *M_out) {
+    API_BEGIN
+    // reg_cpkrylov.m:122-125
+    if (!ctx || !b || !A || !B || !C || !G || !x) throw Error(CPK_ERR_ARGS, "reg_cpkrylov: not enough inputs");
+    Ctx &c = ctx->c;
+    // M = opLDL2(G, B, -C)   (reg_cpkrylov.m:128-132)
+    HCsr negC = C->h;
+    for (auto &v : negC.val) v = -v;
+    auto pc = std::make_unique<cpk_pc_s>();
+    pc->ctx = ctx;
+    pc->p.reset(precond_create(c, G->h, B->h, negC));
+    apply_props(*pc->p, opts);  // reg_cpkrylov.m:135-148
+    check_method_dims(A, C, pc.get());
+    const int64_t N = pc->p->N;
+    const DMat &AC = A->blkdiag_with(C);
+    DBuf<double> db, dx;
+    h2d(db, b, (size_t)N);
+    dx.alloc((size_t)N);
+    reg_solve_device(c, method, db.p, AC, pc->p->dKp, *pc->p, opts, dx.p, stats);
+    CPK_HIP(hipMemcpy(x, dx.p, N * sizeof(double), hipMemcpyDeviceToHost));
+    if (stats) stats->ptime = pc->p->ptime;
+    if (M_out) *M_out = pc.release();
+    API_END
+}
+
+int cpk_analyze(cpk_mat A11, cpk_mat B, cpk_mat C22, cpk_analysis *out) {
+    API_BEGIN
+    need(A11 && B && C22 && out, "NULL argument");
+    auto a = std::make_unique<cpk_analysis_s>();
+    a->an = analyze(A11->h, B->h, C22->h);
+    *out = a.release();
+    API_END
+}
+
+int cpk_analysis_destroy(cpk_analysis an) {
+    API_BEGIN
+    delete an;
+    API_END
+}
+
+int cpk_analysis_get_info(cpk_analysis a, cpk_pc_info *info) {
+    API_BEGIN
+    need(a && info, "NULL argument");
+    const Analysis &an = a->an;
+    info->n = an.n, info->m = an.m, info->N = an.N;
+    info->nnz_kp = an.Kp.nnz();
+    info->nnz_l = (int64_t)an.F.Li.size();
+    info->nblocks = (int64_t)an.S.blk_row.size() - 1;
+    info->nrounds = (int64_t)an.S.round_ptr.size() - 1;
+    info->max_block_levels = an.S.max_levels;
+    info->depth = an.S.depth;
+    info->ordering = an.ordering;
+    API_END
+}
+
+int cpk_analysis_export(cpk_analysis a, int64_t *Lcolptr, int32_t *Lrowind, double *Lval, double *D, int32_t *perm) {
+    API_BEGIN
+    need(a, "NULL argument");
+    const Factor &f = a->an.F;
+    if (Lcolptr) std::memcpy(Lcolptr, f.Lp.data(), f.Lp.size() * sizeof(int64_t));
+    if (Lrowind) std::memcpy(Lrowind, f.Li.data(), f.Li.size() * sizeof(int32_t));
+    if (Lval) std::memcpy(Lval, f.Lx.data(), f.Lx.size() * sizeof(double));
+    if (D) std::memcpy(D, f.D.data(), f.D.size() * sizeof(double));
+    if (perm) std::memcpy(perm, f.perm.data(), f.perm.size() * sizeof(int32_t));
+    API_END
+}
+
+int cpk_analysis_schedule(cpk_analysis a, int64_t *nlevels, int64_t *round_ptr, int64_t *blk_lvl, int64_t *lvl_row) {
+    API_BEGIN
+    need(a, "NULL argument");
+    const Schedule &s = a->an.S;
+    if (nlevels) *nlevels = (int64_t)s.lvl_row.size() - 1;
+    if (round_ptr) std::memcpy(round_ptr, s.round_ptr.data(), s.round_ptr.size() * sizeof(int64_t));
+    if (blk_lvl) std::memcpy(blk_lvl, s.blk_lvl.data(), s.blk_lvl.size() * sizeof(int64_t));
+    if (lvl_row) std::memcpy(lvl_row, s.lvl_row.data(), s.lvl_row.size() * sizeof(int64_t));
+    API_END
+}
+
+int cpk_symgivens(double a, double b, double *c, double *s, double *d) {
+    API_BEGIN
+    need(c && s && d, "NULL argument");
+    auto sign = [](double v) { return (double)((v > 0) - (v < 0)); };
+    if (b == 0) {
+        *c = (a == 0) ? 1.0 : sign(a), *s = 0.0, *d = std::fabs(a);
+    } else if (a == 0) {
+        *c = 0.0, *s = sign(b), *d = std::fabs(b);
+    } else if (std::fabs(b) > std::fabs(a)) {
+        double t = a / b;
+        *s = sign(b) / std::sqrt(1 + t * t), *c = *s * t, *d = b / *s;
+    } else {
+        double t = b / a;
+        *c = sign(a) / std::sqrt(1 + t * t), *s = *c * t, *d = a / *c;
+    }
+    API_END
+}
+
+}  // extern "C"

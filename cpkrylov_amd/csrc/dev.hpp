@@ -1,0 +1,158 @@
+// dev.hpp -- device objects of libcpk (HBM-resident matrices, factor, workspaces) and the
+// kernel launchers.  Included by host C++ (compiled with g++) and by the HIP units.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "cpk.h"
+#include "host.hpp"
+
+namespace cpk {
+
+#define CPK_HIP(call)                                                                                   \
+    do {                                                                                                \
+        hipError_t e_ = (call);                                                                         \
+        if (e_ != hipSuccess)                                                                           \
+            throw ::cpk::Error(CPK_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));        \
+    } while (0)
+
+template <class T>
+struct DBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    DBuf() = default;
+    DBuf(const DBuf &) = delete;
+    DBuf &operator=(const DBuf &) = delete;
+    DBuf(DBuf &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr, o.n = 0; }
+    DBuf &operator=(DBuf &&o) noexcept {
+        if (this != &o) release(), p = o.p, n = o.n, o.p = nullptr, o.n = 0;
+        return *this;
+    }
+    ~DBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr, n = 0;
+    }
+    void alloc(size_t count) {
+        release();
+        n = count;
+        if (count) {
+            hipError_t e = hipMalloc(&p, count * sizeof(T));
+            if (e != hipSuccess) throw Error(CPK_ERR_NOMEM, "hipMalloc of " + std::to_string(count * sizeof(T)) + " bytes failed");
+        }
+    }
+    void upload(const T *h, size_t count) {
+        alloc(count);
+        if (count) CPK_HIP(hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice));
+    }
+    void upload(const std::vector<T> &h) { upload(h.data(), h.size()); }
+    void zero(hipStream_t s) {
+        if (n) CPK_HIP(hipMemsetAsync(p, 0, n * sizeof(T), s));
+    }
+    size_t bytes() const { return n * sizeof(T); }
+};
+
+// Execution context: one GPU, one stream, reduction workspace (and RCCL when nranks > 1).
+struct Ctx {
+    int device = 0, rank = 0, nranks = 1;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    DBuf<double> partials;   // per-workgroup partial sums of the grid reductions
+    DBuf<unsigned> counter;  // arrival tickets
+    void *comm = nullptr;    // ncclComm_t
+    void ensure_partials(size_t count);
+};
+
+// HBM-resident CSR with a row-block partition for the LDS-staged streaming SpMV.
+constexpr int kSpmvCap = 2048;      // entries staged in LDS per workgroup
+constexpr int kSpmvMaxRows = 1024;  // rows per workgroup
+struct DMat {
+    int64_t nrows = 0, ncols = 0, nnz = 0, nblk = 0;
+    DBuf<uint32_t> ptr;
+    DBuf<int32_t> col;
+    DBuf<double> val;
+    DBuf<int32_t> blk;  // row-block boundaries [nblk + 1]
+    bool is_diag = false;
+    size_t bytes() const { return ptr.bytes() + col.bytes() + val.bytes() + blk.bytes(); }
+};
+void make_dmat(const HCsr &a, DMat &d);
+
+// HBM-resident factor + sweep schedule (rows in schedule order).
+struct DFactor {
+    int64_t N = 0, nnz = 0, nblk = 0, nlvl = 0;
+    DBuf<uint32_t> fptr;  // forward rows of strict lower L, columns ascending
+    DBuf<int32_t> fcol;
+    DBuf<double> fval;
+    DBuf<uint32_t> bptr;  // backward rows (= columns of L), row indices descending
+    DBuf<int32_t> bcol;
+    DBuf<double> bval;
+    DBuf<double> D;
+    DBuf<int32_t> perm;     // perm[k] = original index of pivot k
+    DBuf<int32_t> blk_lvl;  // [nblk + 1]
+    DBuf<int32_t> lvl_row;  // [nlvl + 1]
+    std::vector<int64_t> round_ptr;  // host copy: blocks per round
+    size_t bytes() const {
+        return fptr.bytes() + fcol.bytes() + fval.bytes() + bptr.bytes() + bcol.bytes() + bval.bytes() + D.bytes() +
+               perm.bytes() + blk_lvl.bytes() + lvl_row.bytes();
+    }
+};
+void make_dfactor(const Factor &f, const Schedule &s, DFactor &d);
+
+// ---- launchers (kernels.hip) -------------------------------------------------------------
+// Flags: a kernel is a no-op when *run == 0 or *active == 0 (either pointer may be null).
+// neg_from: input entries with index >= neg_from are negated on load (the reference's [u; -t]).
+void launch_spmv(Ctx &c, const DMat &A, const double *x, double *y, const int *run);
+// r = xin - A*y
+void launch_spmv_resid(Ctx &c, const DMat &A, const double *xin, int64_t neg_from, const double *y, double *r,
+                       const int *run, const int *active);
+// r = xin - A*y, and *active = (||r|| >= tol*||xin||) computed on device (opLDL2.m:176-177,183)
+void launch_spmv_resid_norm(Ctx &c, const DMat &A, const double *xin, int64_t neg_from, const double *y, double *r,
+                            double tol, int *active_out, const int *run, const int *active);
+// y = A*x restricted to columns >= col_min (B'*v from the first n rows of Kp)
+void launch_spmv_colmask(Ctx &c, const DMat &A, int64_t col_min, const double *x, double *y, const int *run);
+// forward sweep w = L \ (P' * xin), backward sweep out (=|+=) P * (L' \ (D \ w))
+void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
+                       const int *active);
+void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
+                       const int *active);
+// small vector helpers
+void launch_set_concat(Ctx &c, double *dst, const double *a, int64_t na, int64_t nb);  // dst = [a; 0]
+
+// ---- preconditioner (precond.cpp) --------------------------------------------------------
+// Host analysis of opLDL2's constructor: Kp assembly, ordering, LDL', sweep schedule.
+struct Analysis {
+    int64_t n = 0, m = 0, N = 0;
+    HCsr Kp;
+    Factor F;  // relabelled to the schedule order
+    Schedule S;
+    int ordering = 0;
+    double seconds = 0;
+};
+Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22);
+
+struct Precond {
+    Ctx *ctx = nullptr;
+    int64_t n = 0, m = 0, N = 0;
+    HCsr Kp;             // host copy (divide, export)
+    Factor F;            // relabelled factor (host copy for export)
+    Schedule S;
+    int ordering = 0;
+    DMat dKp;
+    DFactor dF;
+    DBuf<double> w, r;   // permuted work vector, refinement residual
+    DBuf<int> active;    // refinement predicate
+    // public properties of opLDL2 (opLDL2.m:45-50)
+    double nitref = 3, itref_tol = 1.0e-8, force_itref = 0, residual_update = 0;
+    double ptime = 0;
+    // y = M*x  (opLDL2.multiply); all pointers on the device, enqueued on ctx->stream
+    void apply(const double *x, int64_t neg_from, double *y, const int *run);
+    // algorithmic HBM bytes of one apply
+    double apply_bytes() const;
+};
+Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22);
+Precond *precond_create(Ctx &c, Analysis &&an);
+
+}  // namespace cpk

@@ -1,0 +1,235 @@
+// factor.cpp -- static-pivot sparse LDL' of the constraint preconditioner (replaces MATLAB's
+// [L,D,P] = ldl(op.A), ops/opLDL2.m:82) and the block/round schedule for the device
+// triangular sweeps that replace op.LDL = P*inv(L')*inv(D)*inv(L)*P' (ops/opLDL2.m:86).
+#include <algorithm>
+#include <numeric>
+
+#include "cpk.h"
+#include "host.hpp"
+
+namespace cpk {
+
+// Up-looking (row-by-row) LDL': row k of L is the solution of a sparse triangular system
+// whose pattern is the reach of row k's entries in the elimination tree.
+Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int /*nthreads*/) {
+    const int64_t N = Kp.nrows;
+    Factor f;
+    f.N = N;
+    f.perm = perm;
+    std::vector<int32_t> pinv(N);
+    for (int64_t k = 0; k < N; k++) pinv[perm[k]] = (int32_t)k;
+    f.parent.assign(N, -1);
+    std::vector<int32_t> flag(N);
+    std::vector<int64_t> lnz(N, 0);
+    // symbolic: etree + column counts
+    for (int64_t k = 0; k < N; k++) {
+        flag[k] = (int32_t)k;
+        const int32_t r = perm[k];
+        for (int64_t p = Kp.ptr[r]; p < Kp.ptr[r + 1]; p++) {
+            int32_t i = pinv[Kp.ind[p]];
+            if (i >= k) continue;
+            for (; flag[i] != k; i = f.parent[i]) {
+                if (f.parent[i] == -1) f.parent[i] = (int32_t)k;
+                lnz[i]++;
+                flag[i] = (int32_t)k;
+            }
+        }
+    }
+    f.Lp.assign(N + 1, 0);
+    for (int64_t k = 0; k < N; k++) f.Lp[k + 1] = f.Lp[k] + lnz[k];
+    if (f.Lp[N] > INT32_MAX) throw Error(CPK_ERR_NOMEM, "factor too large for 32-bit entry offsets");
+    f.Li.resize(f.Lp[N]);
+    f.Lx.resize(f.Lp[N]);
+    f.D.resize(N);
+    std::vector<double> y(N, 0.0);
+    std::vector<int32_t> pattern(N);
+    std::fill(lnz.begin(), lnz.end(), 0);
+    for (int64_t k = 0; k < N; k++) {
+        int64_t top = N;
+        flag[k] = (int32_t)k;
+        const int32_t r = perm[k];
+        for (int64_t p = Kp.ptr[r]; p < Kp.ptr[r + 1]; p++) {
+            int32_t i = pinv[Kp.ind[p]];
+            if (i > k) continue;
+            y[i] += Kp.val[p];
+            int64_t len = 0;
+            for (; flag[i] != k; i = f.parent[i]) {
+                pattern[len++] = i;
+                flag[i] = (int32_t)k;
+            }
+            while (len > 0) pattern[--top] = pattern[--len];
+        }
+        double d = y[k];
+        y[k] = 0.0;
+        for (; top < N; top++) {
+            const int32_t i = pattern[top];
+            const double yi = y[i];
+            y[i] = 0.0;
+            const int64_t p2 = f.Lp[i] + lnz[i];
+            for (int64_t p = f.Lp[i]; p < p2; p++) y[f.Li[p]] -= f.Lx[p] * yi;
+            const double lki = yi / f.D[i];
+            d -= lki * yi;
+            f.Li[p2] = (int32_t)k;
+            f.Lx[p2] = lki;
+            lnz[i]++;
+        }
+        if (d == 0.0 || !(d == d))
+            throw Error(CPK_ERR_FACTOR, "ldl: zero or NaN pivot at position " + std::to_string(k) +
+                                            " (static 1x1 pivoting needs G > 0 on the nullspace and C > 0)");
+        f.D[k] = d;
+    }
+    return f;
+}
+
+Schedule build_schedule(const Factor &f, int64_t R) {
+    const int64_t N = f.N;
+    Schedule s;
+    s.N = N;
+    // children lists
+    std::vector<int64_t> cptr(N + 2, 0);
+    for (int64_t v = 0; v < N; v++)
+        if (f.parent[v] >= 0) cptr[f.parent[v] + 1]++;
+    for (int64_t v = 0; v < N; v++) cptr[v + 1] += cptr[v];
+    std::vector<int32_t> kids(cptr[N]);
+    {
+        std::vector<int64_t> nx(cptr.begin(), cptr.begin() + N);
+        for (int64_t v = 0; v < N; v++)
+            if (f.parent[v] >= 0) kids[nx[f.parent[v]]++] = (int32_t)v;
+    }
+    // tree height (for reporting)
+    std::vector<int32_t> height(N, 0);
+    for (int64_t v = 0; v < N; v++) {
+        if (f.parent[v] >= 0) height[f.parent[v]] = std::max(height[f.parent[v]], height[v] + 1);
+        s.depth = std::max<int64_t>(s.depth, height[v] + 1);
+    }
+    // bottom-up greedy subtree clustering (children always precede parents)
+    std::vector<int64_t> open_size(N, 0);
+    std::vector<int32_t> open_dep(N, -1);
+    std::vector<int32_t> closed_round(N, -1);  // >= 0 iff v roots a closed cluster
+    std::vector<int32_t> tmp;
+    for (int64_t v = 0; v < N; v++) {
+        int64_t total = 1;
+        int32_t dep = -1;
+        tmp.assign(kids.begin() + cptr[v], kids.begin() + cptr[v + 1]);
+        for (int32_t c : tmp) total += open_size[c];
+        if (total > R) {
+            std::sort(tmp.begin(), tmp.end(), [&](int32_t a, int32_t b) {
+                return open_size[a] != open_size[b] ? open_size[a] > open_size[b] : a < b;
+            });
+            for (int32_t c : tmp) {
+                if (total <= R) break;
+                closed_round[c] = open_dep[c] + 1;
+                total -= open_size[c];
+                open_size[c] = 0;
+            }
+        }
+        for (int64_t q = cptr[v]; q < cptr[v + 1]; q++) {
+            int32_t c = kids[q];
+            dep = std::max(dep, closed_round[c] >= 0 ? closed_round[c] : open_dep[c]);
+        }
+        open_size[v] = total;
+        open_dep[v] = dep;
+        if (f.parent[v] < 0) closed_round[v] = dep + 1;
+    }
+    // cluster membership (top-down)
+    std::vector<int32_t> cl(N);
+    for (int64_t v = N - 1; v >= 0; v--) cl[v] = closed_round[v] >= 0 ? (int32_t)v : cl[f.parent[v]];
+    std::vector<int64_t> csize(N, 0);
+    for (int64_t v = 0; v < N; v++) csize[cl[v]]++;
+    int32_t nrounds = 0;
+    for (int64_t v = 0; v < N; v++)
+        if (closed_round[v] >= 0) nrounds = std::max(nrounds, closed_round[v] + 1);
+    // pack clusters of one round into blocks of <= R rows (clusters taken in root order)
+    std::vector<std::vector<int32_t>> roots_by_round(nrounds);
+    for (int64_t v = 0; v < N; v++)
+        if (closed_round[v] >= 0) roots_by_round[closed_round[v]].push_back((int32_t)v);
+    std::vector<int32_t> cluster_block(N, -1);
+    std::vector<int64_t> block_round;
+    int32_t nb = 0;
+    s.round_ptr.assign(1, 0);
+    for (int32_t r = 0; r < nrounds; r++) {
+        int64_t fill = R + 1;
+        for (int32_t c : roots_by_round[r]) {
+            if (fill + csize[c] > R) {
+                nb++;
+                fill = 0;
+            }
+            cluster_block[c] = nb - 1;
+            fill += csize[c];
+        }
+        s.round_ptr.push_back(nb);
+    }
+    std::vector<int32_t> block(N);
+    for (int64_t v = 0; v < N; v++) block[v] = cluster_block[cl[v]];
+    // intra-block levels (CSC columns ascend, so level[j] is final when column j is visited)
+    std::vector<int32_t> level(N, 0);
+    for (int64_t j = 0; j < N; j++)
+        for (int64_t p = f.Lp[j]; p < f.Lp[j + 1]; p++) {
+            int32_t i = f.Li[p];
+            if (block[i] == block[j]) level[i] = std::max(level[i], level[j] + 1);
+        }
+    // new order: blocks ascending (= rounds ascending), then level, then old index
+    std::vector<int64_t> bcount(nb + 1, 0);
+    for (int64_t v = 0; v < N; v++) bcount[block[v] + 1]++;
+    for (int32_t b = 0; b < nb; b++) bcount[b + 1] += bcount[b];
+    s.blk_row = bcount;
+    s.order.resize(N);
+    {
+        std::vector<int64_t> nx(bcount.begin(), bcount.end() - 1);
+        for (int64_t v = 0; v < N; v++) s.order[nx[block[v]]++] = (int32_t)v;
+    }
+    s.blk_lvl.assign(1, 0);
+    s.lvl_row.clear();
+    for (int32_t b = 0; b < nb; b++) {
+        auto first = s.order.begin() + s.blk_row[b], last = s.order.begin() + s.blk_row[b + 1];
+        std::stable_sort(first, last, [&](int32_t a, int32_t c) { return level[a] < level[c]; });
+        int32_t prev = -1;
+        for (int64_t q = s.blk_row[b]; q < s.blk_row[b + 1]; q++) {
+            int32_t l = level[s.order[q]];
+            if (l != prev) s.lvl_row.push_back(q), prev = l;
+        }
+        s.blk_lvl.push_back((int64_t)s.lvl_row.size());
+        s.max_levels = std::max<int64_t>(s.max_levels, s.blk_lvl[b + 1] - s.blk_lvl[b]);
+    }
+    s.lvl_row.push_back(N);
+    return s;
+}
+
+Factor relabel(const Factor &f, const Schedule &s) {
+    const int64_t N = f.N;
+    std::vector<int32_t> pos(N);
+    for (int64_t q = 0; q < N; q++) pos[s.order[q]] = (int32_t)q;
+    Factor g;
+    g.N = N;
+    g.perm.resize(N);
+    g.D.resize(N);
+    g.parent.assign(N, -1);
+    for (int64_t q = 0; q < N; q++) {
+        int32_t old = s.order[q];
+        g.perm[q] = f.perm[old];
+        g.D[q] = f.D[old];
+        if (f.parent[old] >= 0) g.parent[q] = pos[f.parent[old]];
+    }
+    g.Lp.assign(N + 1, 0);
+    for (int64_t q = 0; q < N; q++) {
+        int32_t old = s.order[q];
+        g.Lp[q + 1] = g.Lp[q] + (f.Lp[old + 1] - f.Lp[old]);
+    }
+    g.Li.resize(f.Li.size());
+    g.Lx.resize(f.Lx.size());
+    std::vector<std::pair<int32_t, double>> col;
+    for (int64_t q = 0; q < N; q++) {
+        int32_t old = s.order[q];
+        col.clear();
+        for (int64_t p = f.Lp[old]; p < f.Lp[old + 1]; p++) col.emplace_back(pos[f.Li[p]], f.Lx[p]);
+        std::sort(col.begin(), col.end(), [](auto &a, auto &b) { return a.first < b.first; });
+        for (size_t t = 0; t < col.size(); t++) {
+            if (col[t].first <= q) throw Error(CPK_ERR_FACTOR, "internal: relabel is not topological");
+            g.Li[g.Lp[q] + t] = col[t].first;
+            g.Lx[g.Lp[q] + t] = col[t].second;
+        }
+    }
+    return g;
+}
+
+}  // namespace cpk

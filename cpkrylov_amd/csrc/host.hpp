@@ -1,0 +1,75 @@
+// host.hpp -- host-side sparse structures, ordering and the static-pivot LDL' factorization
+// that replaces MATLAB's ldl() inside opLDL2 (ops/opLDL2.m:81-86).
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace cpk {
+
+// Error carrying a cpk_status code across C++ layers; converted at the C ABI.
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+// Host CSR: 64-bit row pointers, 32-bit sorted column indices, no duplicates.
+struct HCsr {
+    int64_t nrows = 0, ncols = 0;
+    std::vector<int64_t> ptr;
+    std::vector<int32_t> ind;
+    std::vector<double> val;
+    int64_t nnz() const { return ptr.empty() ? 0 : ptr.back(); }
+};
+
+HCsr csr_from_csr(int64_t nr, int64_t nc, const int64_t *rp, const int32_t *ci, const double *v);
+HCsr csr_from_csc(int64_t nr, int64_t nc, const size_t *jc, const size_t *ir, const double *pr);
+HCsr transpose(const HCsr &a);
+// Kp = [A B'; B C]  (opLDL2.m:81)
+HCsr assemble_kp(const HCsr &A, const HCsr &B, const HCsr &C);
+// blkdiag(A, C): the Krylov operator's diagonal blocks, used to fuse u = A*v and t = C*q.
+HCsr blkdiag(const HCsr &A, const HCsr &C);
+bool is_diagonal(const HCsr &a);
+
+// ---- ordering --------------------------------------------------------------------------
+enum OrderKind { ORD_NATURAL = 0, ORD_GFIRST_ND = 1, ORD_GFIRST_MD = 2, ORD_ND = 3, ORD_MD = 4 };
+// Fill-reducing symmetric ordering of Kp (n = size of the (1,1) block). perm[k] = old index.
+std::vector<int32_t> order_kp(const HCsr &Kp, int64_t n, int *kind_out);
+// building blocks (exposed for tests)
+std::vector<int32_t> min_degree(const HCsr &graph);
+std::vector<int32_t> nested_dissection(const HCsr &graph, int leaf_size);
+
+// ---- factorization -----------------------------------------------------------------------
+// P'*Kp*P = L*D*L', L unit lower (strict part stored), D diagonal (1x1 static pivots).
+struct Factor {
+    int64_t N = 0;
+    std::vector<int32_t> perm;   // perm[k] = original index of pivot k
+    std::vector<int64_t> Lp;     // CSC of strict lower L
+    std::vector<int32_t> Li;
+    std::vector<double> Lx;
+    std::vector<double> D;
+    std::vector<int32_t> parent; // elimination tree
+};
+Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int nthreads);
+
+// ---- SpTRSV schedule ---------------------------------------------------------------------
+// The elimination tree is cut into blocks: sets of whole subtrees of at most R rows, solved
+// by one workgroup each.  Blocks form rounds (block-level sets): a round's blocks only
+// depend on earlier rounds, so one kernel launch per round and sweep suffices.  Inside a
+// block, rows are grouped into intra-block levels separated by workgroup barriers.
+struct Schedule {
+    int64_t N = 0;
+    std::vector<int32_t> order;        // new position -> old (factor) index: a topological relabel
+    std::vector<int64_t> round_ptr;    // blocks of round r: [round_ptr[r], round_ptr[r+1])
+    std::vector<int64_t> blk_row;      // block b rows: [blk_row[b], blk_row[b+1]) (new numbering)
+    std::vector<int64_t> blk_lvl;      // block b levels: lvl_row[blk_lvl[b] .. blk_lvl[b+1]]
+    std::vector<int64_t> lvl_row;      // level boundaries (row positions), one array for all blocks
+    int64_t max_levels = 0;
+    int64_t depth = 0;
+};
+Schedule build_schedule(const Factor &f, int64_t R);
+// Apply the schedule's relabel to the factor (values unchanged, exact data movement).
+Factor relabel(const Factor &f, const Schedule &s);
+
+}  // namespace cpk

@@ -1,0 +1,155 @@
+// hostsparse.cpp -- host CSR conversions and the Kp = [A B'; B C] assembly (ops/opLDL2.m:81).
+#include <algorithm>
+#include <numeric>
+
+#include "cpk.h"
+#include "host.hpp"
+
+namespace cpk {
+
+// Canonicalise: sort each row by column, sum duplicates (MATLAB sparse arrays never hold any).
+static void canonicalise(HCsr &a) {
+    std::vector<int64_t> ptr(a.nrows + 1, 0);
+    std::vector<int32_t> ind;
+    std::vector<double> val;
+    ind.reserve(a.ind.size());
+    val.reserve(a.val.size());
+    std::vector<std::pair<int32_t, double>> row;
+    for (int64_t i = 0; i < a.nrows; i++) {
+        row.clear();
+        for (int64_t p = a.ptr[i]; p < a.ptr[i + 1]; p++) row.emplace_back(a.ind[p], a.val[p]);
+        bool sorted = std::is_sorted(row.begin(), row.end(),
+                                     [](auto &x, auto &y) { return x.first < y.first; });
+        if (!sorted) std::stable_sort(row.begin(), row.end(), [](auto &x, auto &y) { return x.first < y.first; });
+        for (size_t q = 0; q < row.size(); q++) {
+            if (!ind.empty() && (int64_t)ind.size() > ptr[i] && ind.back() == row[q].first)
+                val.back() += row[q].second;
+            else
+                ind.push_back(row[q].first), val.push_back(row[q].second);
+        }
+        ptr[i + 1] = (int64_t)ind.size();
+    }
+    a.ptr.swap(ptr);
+    a.ind.swap(ind);
+    a.val.swap(val);
+}
+
+HCsr csr_from_csr(int64_t nr, int64_t nc, const int64_t *rp, const int32_t *ci, const double *v) {
+    if (nr < 0 || nc < 0 || nr > INT32_MAX || nc > INT32_MAX) throw Error(CPK_ERR_DIM, "matrix dimensions out of range");
+    if (nr > 0 && (!rp || (rp[nr] > 0 && (!ci || !v)))) throw Error(CPK_ERR_ARGS, "NULL CSR array");
+    HCsr a;
+    a.nrows = nr, a.ncols = nc;
+    a.ptr.assign(rp, rp + nr + 1);
+    if (a.ptr.empty()) a.ptr.push_back(0);
+    int64_t nnz = a.ptr.back() - a.ptr.front();
+    if (a.ptr.front() != 0) for (auto &p : a.ptr) p -= rp[0];
+    a.ind.assign(ci + rp[0], ci + rp[0] + nnz);
+    a.val.assign(v + rp[0], v + rp[0] + nnz);
+    for (int64_t i = 0; i < nr; i++)
+        if (a.ptr[i + 1] < a.ptr[i]) throw Error(CPK_ERR_ARGS, "CSR row pointers not monotone");
+    for (auto c : a.ind)
+        if (c < 0 || c >= nc) throw Error(CPK_ERR_ARGS, "CSR column index out of range");
+    canonicalise(a);
+    return a;
+}
+
+HCsr csr_from_csc(int64_t nr, int64_t nc, const size_t *jc, const size_t *ir, const double *pr) {
+    if (nr < 0 || nc < 0 || nr > INT32_MAX || nc > INT32_MAX) throw Error(CPK_ERR_DIM, "matrix dimensions out of range");
+    if (nc > 0 && !jc) throw Error(CPK_ERR_ARGS, "NULL CSC array");
+    size_t nnz = nc > 0 ? jc[nc] - jc[0] : 0;
+    if (nnz && (!ir || !pr)) throw Error(CPK_ERR_ARGS, "NULL CSC array");
+    HCsr a;
+    a.nrows = nr, a.ncols = nc;
+    a.ptr.assign(nr + 1, 0);
+    for (int64_t j = 0; j < nc; j++)
+        for (size_t p = jc[j]; p < jc[j + 1]; p++) {
+            if (ir[p] >= (size_t)nr) throw Error(CPK_ERR_ARGS, "CSC row index out of range");
+            a.ptr[ir[p] + 1]++;
+        }
+    for (int64_t i = 0; i < nr; i++) a.ptr[i + 1] += a.ptr[i];
+    a.ind.resize(nnz);
+    a.val.resize(nnz);
+    std::vector<int64_t> next(a.ptr.begin(), a.ptr.end() - 1);
+    for (int64_t j = 0; j < nc; j++)  // columns ascend, so every row comes out sorted
+        for (size_t p = jc[j]; p < jc[j + 1]; p++) {
+            int64_t q = next[ir[p]]++;
+            a.ind[q] = (int32_t)j;
+            a.val[q] = pr[p];
+        }
+    canonicalise(a);
+    return a;
+}
+
+HCsr transpose(const HCsr &a) {
+    HCsr t;
+    t.nrows = a.ncols, t.ncols = a.nrows;
+    t.ptr.assign(t.nrows + 1, 0);
+    for (auto c : a.ind) t.ptr[c + 1]++;
+    for (int64_t i = 0; i < t.nrows; i++) t.ptr[i + 1] += t.ptr[i];
+    t.ind.resize(a.nnz());
+    t.val.resize(a.nnz());
+    std::vector<int64_t> next(t.ptr.begin(), t.ptr.end() - 1);
+    for (int64_t i = 0; i < a.nrows; i++)
+        for (int64_t p = a.ptr[i]; p < a.ptr[i + 1]; p++) {
+            int64_t q = next[a.ind[p]]++;
+            t.ind[q] = (int32_t)i;
+            t.val[q] = a.val[p];
+        }
+    return t;
+}
+
+HCsr assemble_kp(const HCsr &A, const HCsr &B, const HCsr &C) {
+    // dimension checks of opLDL2.m:61-75 (same messages)
+    if (A.nrows != A.ncols || C.nrows != C.ncols) throw Error(CPK_ERR_DIM, "First and last arguments must be square.");
+    if (B.ncols != A.nrows || B.nrows != C.nrows) throw Error(CPK_ERR_DIM, "Incompatible dimensions.");
+    const int64_t n = A.nrows, m = C.nrows, N = n + m;
+    if (N > INT32_MAX) throw Error(CPK_ERR_DIM, "N exceeds the 32-bit index range");
+    HCsr Bt = transpose(B);
+    HCsr K;
+    K.nrows = K.ncols = N;
+    K.ptr.assign(N + 1, 0);
+    K.ind.reserve(A.nnz() + 2 * B.nnz() + C.nnz());
+    K.val.reserve(K.ind.capacity());
+    for (int64_t i = 0; i < n; i++) {
+        for (int64_t p = A.ptr[i]; p < A.ptr[i + 1]; p++) K.ind.push_back(A.ind[p]), K.val.push_back(A.val[p]);
+        for (int64_t p = Bt.ptr[i]; p < Bt.ptr[i + 1]; p++)
+            K.ind.push_back((int32_t)(n + Bt.ind[p])), K.val.push_back(Bt.val[p]);
+        K.ptr[i + 1] = (int64_t)K.ind.size();
+    }
+    for (int64_t i = 0; i < m; i++) {
+        for (int64_t p = B.ptr[i]; p < B.ptr[i + 1]; p++) K.ind.push_back(B.ind[p]), K.val.push_back(B.val[p]);
+        for (int64_t p = C.ptr[i]; p < C.ptr[i + 1]; p++)
+            K.ind.push_back((int32_t)(n + C.ind[p])), K.val.push_back(C.val[p]);
+        K.ptr[n + i + 1] = (int64_t)K.ind.size();
+    }
+    return K;
+}
+
+HCsr blkdiag(const HCsr &A, const HCsr &C) {
+    const int64_t n = A.nrows, m = C.nrows;
+    HCsr K;
+    K.nrows = n + m;
+    K.ncols = A.ncols + C.ncols;
+    K.ptr.assign(n + m + 1, 0);
+    K.ind.reserve(A.nnz() + C.nnz());
+    K.val.reserve(A.nnz() + C.nnz());
+    for (int64_t i = 0; i < n; i++) {
+        for (int64_t p = A.ptr[i]; p < A.ptr[i + 1]; p++) K.ind.push_back(A.ind[p]), K.val.push_back(A.val[p]);
+        K.ptr[i + 1] = (int64_t)K.ind.size();
+    }
+    for (int64_t i = 0; i < m; i++) {
+        for (int64_t p = C.ptr[i]; p < C.ptr[i + 1]; p++)
+            K.ind.push_back((int32_t)(A.ncols + C.ind[p])), K.val.push_back(C.val[p]);
+        K.ptr[n + i + 1] = (int64_t)K.ind.size();
+    }
+    return K;
+}
+
+bool is_diagonal(const HCsr &a) {
+    for (int64_t i = 0; i < a.nrows; i++)
+        for (int64_t p = a.ptr[i]; p < a.ptr[i + 1]; p++)
+            if (a.ind[p] != i) return false;
+    return true;
+}
+
+}  // namespace cpk

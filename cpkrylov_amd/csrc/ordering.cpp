@@ -1,0 +1,259 @@
+// ordering.cpp -- fill-reducing symmetric orderings for the constraint preconditioner Kp.
+//
+// MATLAB's ldl() (ops/opLDL2.m:82) picks its own (MA57) ordering and 2x2 pivots; neither can
+// be reproduced, and only the exact solve with Kp matters for the Krylov iterates.  Kp is
+// symmetric quasi-definite for G > 0, C_user > 0, so an LDL' with 1x1 pivots exists for every
+// symmetric ordering.  The ordering is chosen for fill AND for triangular-solve parallelism:
+//   - G diagonal (every example and synthetic case): eliminate the G block first (its nodes
+//     are independent leaves), then order the Schur-complement graph S = pattern(C + B G^-1 B')
+//     by nested dissection (large) or minimum degree (small);
+//   - otherwise nested dissection / minimum degree on the whole graph of Kp.
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <queue>
+#include <set>
+
+#include "cpk.h"
+#include "host.hpp"
+
+namespace cpk {
+
+static constexpr int64_t kMdLimit = 60000;  // exact minimum degree up to this many nodes
+static constexpr int kNdLeaf = 4;
+
+// symmetric adjacency graph (no self loops) from a list of undirected edges
+static HCsr graph_from_edges(int64_t nv, std::vector<std::pair<int32_t, int32_t>> &edges) {
+    for (auto &e : edges)
+        if (e.first > e.second) std::swap(e.first, e.second);
+    std::sort(edges.begin(), edges.end());
+    edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
+    HCsr g;
+    g.nrows = g.ncols = nv;
+    g.ptr.assign(nv + 1, 0);
+    for (auto &e : edges) g.ptr[e.first + 1]++, g.ptr[e.second + 1]++;
+    for (int64_t i = 0; i < nv; i++) g.ptr[i + 1] += g.ptr[i];
+    g.ind.resize(g.ptr[nv]);
+    std::vector<int64_t> next(g.ptr.begin(), g.ptr.end() - 1);
+    for (auto &e : edges) g.ind[next[e.first]++] = e.second, g.ind[next[e.second]++] = e.first;
+    for (int64_t i = 0; i < nv; i++) std::sort(g.ind.begin() + g.ptr[i], g.ind.begin() + g.ptr[i + 1]);
+    return g;
+}
+
+// Exact minimum degree on the explicit elimination graph; ties broken by lowest index.
+std::vector<int32_t> min_degree(const HCsr &g) {
+    const int64_t nv = g.nrows;
+    std::vector<std::vector<int32_t>> adj(nv);
+    for (int64_t i = 0; i < nv; i++)
+        for (int64_t p = g.ptr[i]; p < g.ptr[i + 1]; p++)
+            if (g.ind[p] != i) adj[i].push_back(g.ind[p]);
+    std::set<std::pair<int64_t, int32_t>> pq;
+    for (int64_t i = 0; i < nv; i++) pq.insert({(int64_t)adj[i].size(), (int32_t)i});
+    std::vector<char> dead(nv, 0);
+    std::vector<int32_t> order;
+    order.reserve(nv);
+    std::vector<int32_t> mark(nv, -1), merged;
+    while (!pq.empty()) {
+        int32_t v = pq.begin()->second;
+        pq.erase(pq.begin());
+        dead[v] = 1;
+        order.push_back(v);
+        std::vector<int32_t> nb;
+        for (int32_t u : adj[v])
+            if (!dead[u]) nb.push_back(u);
+        for (int32_t u : nb) {
+            pq.erase({(int64_t)adj[u].size(), u});
+            // adj[u] <- (adj[u] U nb) \ {u, v, dead}
+            merged.clear();
+            for (int32_t w : adj[u])
+                if (!dead[w] && mark[w] != u) mark[w] = u, merged.push_back(w);
+            for (int32_t w : nb)
+                if (w != u && mark[w] != u) mark[w] = u, merged.push_back(w);
+            adj[u].swap(merged);
+            pq.insert({(int64_t)adj[u].size(), u});
+        }
+        adj[v].clear();
+        adj[v].shrink_to_fit();
+    }
+    return order;
+}
+
+// ---- nested dissection by BFS level structures (George-Liu) ------------------------------
+namespace {
+struct Nd {
+    const HCsr &g;
+    std::vector<int32_t> label;   // subset id of each node
+    std::vector<int32_t> dist;    // BFS distance (valid when stamp matches)
+    std::vector<int32_t> stamp;
+    std::vector<int32_t> out;
+    int64_t out_pos = 0;
+    int32_t next_label = 1, cur_stamp = 0;
+    int leaf;
+    explicit Nd(const HCsr &gg, int lf) : g(gg), label(gg.nrows, 0), dist(gg.nrows, 0), stamp(gg.nrows, -1),
+                                          out(gg.nrows), leaf(lf) {}
+
+    // BFS within nodes of `lab` from `src`; fills `bfs` in visit order, returns eccentricity.
+    int32_t bfs(int32_t src, int32_t lab, std::vector<int32_t> &bfs_order) {
+        cur_stamp++;
+        bfs_order.clear();
+        bfs_order.push_back(src);
+        stamp[src] = cur_stamp;
+        dist[src] = 0;
+        for (size_t h = 0; h < bfs_order.size(); h++) {
+            int32_t v = bfs_order[h];
+            for (int64_t p = g.ptr[v]; p < g.ptr[v + 1]; p++) {
+                int32_t w = g.ind[p];
+                if (label[w] != lab || stamp[w] == cur_stamp) continue;
+                stamp[w] = cur_stamp;
+                dist[w] = dist[v] + 1;
+                bfs_order.push_back(w);
+            }
+        }
+        return dist[bfs_order.back()];
+    }
+
+    void emit(std::vector<int32_t> &nodes) {
+        std::sort(nodes.begin(), nodes.end());
+        for (int32_t v : nodes) out[out_pos++] = v;
+    }
+
+    // order the nodes of subset `nodes` (all carry label `lab`)
+    void run(std::vector<int32_t> nodes, int32_t lab) {
+        std::vector<int32_t> order;
+        while (true) {
+            if ((int64_t)nodes.size() <= leaf) {
+                emit(nodes);
+                return;
+            }
+            // split into connected components first
+            bfs(nodes[0], lab, order);
+            if (order.size() < nodes.size()) {
+                int32_t la = next_label++, lb = next_label++;
+                std::vector<int32_t> a = order, b;
+                for (int32_t v : a) label[v] = la;
+                for (int32_t v : nodes)
+                    if (label[v] == lab) label[v] = lb, b.push_back(v);
+                run(std::move(a), la);
+                nodes.swap(b);
+                lab = lb;
+                continue;
+            }
+            // pseudo-peripheral node
+            int32_t start = order.back();
+            int32_t ecc = bfs(start, lab, order);
+            for (int it = 0; it < 4; it++) {
+                int32_t cand = order.back();
+                std::vector<int32_t> o2;
+                int32_t e2 = bfs(cand, lab, o2);
+                if (e2 <= ecc) break;
+                ecc = e2, start = cand, order.swap(o2);
+            }
+            bfs(start, lab, order);
+            if (ecc < 2) {  // too shallow to dissect: order by minimum degree locally
+                emit(nodes);
+                return;
+            }
+            // level sizes; split at the level reaching half of the nodes
+            std::vector<int64_t> lsz(ecc + 1, 0);
+            for (int32_t v : order) lsz[dist[v]]++;
+            int64_t acc = 0, half = (int64_t)nodes.size() / 2;
+            int32_t s = 1;
+            for (int32_t l = 0; l <= ecc; l++) {
+                acc += lsz[l];
+                if (acc >= half) {
+                    s = l;
+                    break;
+                }
+            }
+            s = std::max<int32_t>(1, std::min<int32_t>(s, ecc - 1));
+            // separator: level-s nodes adjacent to level s+1 (the rest join part A)
+            int32_t la = next_label++, lb = next_label++, ls = next_label++;
+            std::vector<int32_t> a, b, sep;
+            for (int32_t v : order) {
+                int32_t d = dist[v];
+                if (d < s) a.push_back(v);
+                else if (d > s) b.push_back(v);
+                else {
+                    bool touches = false;
+                    for (int64_t p = g.ptr[v]; p < g.ptr[v + 1] && !touches; p++) {
+                        int32_t w = g.ind[p];
+                        touches = label[w] == lab && stamp[w] == cur_stamp && dist[w] == s + 1;
+                    }
+                    (touches ? sep : a).push_back(v);
+                }
+            }
+            for (int32_t v : a) label[v] = la;
+            for (int32_t v : b) label[v] = lb;
+            for (int32_t v : sep) label[v] = ls;
+            run(std::move(a), la);
+            run(std::move(b), lb);
+            emit(sep);
+            return;
+        }
+    }
+};
+}  // namespace
+
+std::vector<int32_t> nested_dissection(const HCsr &g, int leaf_size) {
+    Nd nd(g, leaf_size);
+    std::vector<int32_t> all(g.nrows);
+    std::iota(all.begin(), all.end(), 0);
+    if (g.nrows) nd.run(std::move(all), 0);
+    return nd.out;
+}
+
+std::vector<int32_t> order_kp(const HCsr &Kp, int64_t n, int *kind_out) {
+    const int64_t N = Kp.nrows, m = N - n;
+    bool g_diag = true;
+    for (int64_t i = 0; i < n && g_diag; i++)
+        for (int64_t p = Kp.ptr[i]; p < Kp.ptr[i + 1]; p++)
+            if (Kp.ind[p] < n && Kp.ind[p] != i) {
+                g_diag = false;
+                break;
+            }
+    std::vector<int32_t> perm(N);
+    if (g_diag && m > 0) {
+        // Schur-complement graph on the m block: cliques of each G column's B entries + C pattern
+        std::vector<std::pair<int32_t, int32_t>> edges;
+        std::vector<int32_t> nb;
+        for (int64_t j = 0; j < n; j++) {
+            nb.clear();
+            for (int64_t p = Kp.ptr[j]; p < Kp.ptr[j + 1]; p++)
+                if (Kp.ind[p] >= n) nb.push_back(Kp.ind[p] - (int32_t)n);
+            for (size_t a = 0; a < nb.size(); a++)
+                for (size_t b = a + 1; b < nb.size(); b++) edges.emplace_back(nb[a], nb[b]);
+        }
+        for (int64_t i = 0; i < m; i++)
+            for (int64_t p = Kp.ptr[n + i]; p < Kp.ptr[n + i + 1]; p++) {
+                int32_t c = Kp.ind[p];
+                if (c >= n && c - n != i) edges.emplace_back((int32_t)i, c - (int32_t)n);
+            }
+        HCsr S = graph_from_edges(m, edges);
+        std::vector<int32_t> os;
+        if (m <= kMdLimit) {
+            os = min_degree(S);
+            *kind_out = ORD_GFIRST_MD;
+        } else {
+            os = nested_dissection(S, kNdLeaf);
+            *kind_out = ORD_GFIRST_ND;
+        }
+        for (int64_t i = 0; i < n; i++) perm[i] = (int32_t)i;
+        for (int64_t i = 0; i < m; i++) perm[n + i] = (int32_t)(n + os[i]);
+    } else {
+        std::vector<std::pair<int32_t, int32_t>> edges;
+        for (int64_t i = 0; i < N; i++)
+            for (int64_t p = Kp.ptr[i]; p < Kp.ptr[i + 1]; p++)
+                if (Kp.ind[p] != i) edges.emplace_back((int32_t)i, Kp.ind[p]);
+        HCsr g = graph_from_edges(N, edges);
+        if (N <= kMdLimit) {
+            perm = min_degree(g);
+            *kind_out = ORD_MD;
+        } else {
+            perm = nested_dissection(g, kNdLeaf);
+            *kind_out = ORD_ND;
+        }
+    }
+    return perm;
+}
+
+}  // namespace cpk

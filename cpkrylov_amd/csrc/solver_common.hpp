@@ -1,0 +1,148 @@
+// solver_common.hpp -- device state + generic streaming kernels shared by the six solvers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "dev.hpp"
+#include "devutil.hpp"
+
+namespace cpk {
+
+constexpr double kEps = 2.220446049250313e-16;  // MATLAB eps
+
+// Scalar state of a solve, resident in HBM.  Every recurrence scalar of the reference
+// solvers lives here and is updated by the single-thread epilogue of a reduction kernel, so
+// the host never sits on the iteration's critical path.
+struct DState {
+    int64_t k;        // completed iterations (MATLAB k / itn)
+    int64_t itmax;
+    int64_t nh, nh2, nh3;  // history lengths
+    int64_t hcap;
+    int stop;         // loop condition is false (or an error occurred)
+    int running;      // the current iteration is live
+    int err;          // 1: indefinite (beta < -100 eps or negative squared norm)
+    int flag;         // solver-specific flag (symmlq: moved to CG point)
+    int64_t err_iter;
+    double err_val;
+    double atol, rtol, btol, stopTol, bstopTol, residNorm;
+    // Lanczos family
+    double alpha, beta, beta1, oldeps, delta, gamma, gammabar, deltabar, epsln, cs, sn, tau, taubar;
+    // cpcg
+    double rn2, pAp, qCq;
+    // cpcglanczos
+    double dg, low, eta, zeta, rhobar, xxNorm2, xNorm, taul, deltal, opNorm2, oldbeta, bkerr, opNorm;
+    // cpsymmlq
+    double epsdelzeta, epsilonzeta, bstep, snprod, matnorm2, cgresid, lqresid, qrresid, den, betaold, epsilon, zcs,
+        zsn, zetabar;
+    // cpgmres / cpdqgmres
+    int64_t restart, mem, kin, hrow;
+    double hk1;
+    double *H, *c, *s, *g, *z;
+    double *hist, *hist2, *hist3, *aux;
+};
+
+__device__ __forceinline__ void push(double *h, int64_t &len, int64_t cap, double v) {
+    if (len < cap) h[len] = v;
+    len++;
+}
+
+__device__ __forceinline__ double msign(double a) { return (double)((a > 0) - (a < 0)); }
+
+// util/SymGivens.m:1-29
+__device__ __forceinline__ void sym_givens(double a, double b, double &c, double &s, double &d) {
+    if (b == 0) {
+        c = (a == 0) ? 1.0 : msign(a);
+        s = 0.0;
+        d = fabs(a);
+    } else if (a == 0) {
+        c = 0.0;
+        s = msign(b);
+        d = fabs(b);
+    } else if (fabs(b) > fabs(a)) {
+        double t = a / b;
+        s = msign(b) / sqrt(1 + t * t);
+        c = s * t;
+        d = b / s;
+    } else {
+        double t = b / a;
+        c = msign(a) / sqrt(1 + t * t);
+        s = c * t;
+        d = a / c;
+    }
+}
+
+constexpr int kEwGrid = 1024;  // fixed grid of the streaming vector kernels (deterministic partials)
+
+// Elementwise kernel over [0, N): F::setup() loads scalars (false => no-op), F::operator()(i).
+template <class F>
+__global__ __launch_bounds__(kBlock) void ew_kernel(int64_t N, F f) {
+    if (!f.setup()) return;
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) f(i);
+}
+
+// Elementwise + grid reduction of NV sums: F::operator()(i, acc), F::fin(tot) in the last workgroup.
+template <int NV, class F>
+__global__ __launch_bounds__(kBlock) void ewred_kernel(int64_t N, F f, RedBuf rb) {
+    if (!f.setup()) return;
+    double acc[NV];
+#pragma unroll
+    for (int j = 0; j < NV; j++) acc[j] = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) f(i, acc);
+    double tot[NV];
+    if (grid_sum<NV>(acc, rb, tot) && threadIdx.x == 0) f.fin(tot);
+}
+
+// Single-thread scalar step.
+template <class F>
+__global__ void scalar_kernel(F f) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) f();
+}
+
+inline int ew_grid(int64_t N) { return (int)std::max<int64_t>(1, std::min<int64_t>((N + kBlock - 1) / kBlock, kEwGrid)); }
+
+template <class F>
+inline void launch_ew(Ctx &c, int64_t N, const F &f) {
+    hipLaunchKernelGGL(ew_kernel<F>, dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f);
+}
+template <int NV, class F>
+inline void launch_ewred(Ctx &c, int64_t N, const F &f) {
+    c.ensure_partials((size_t)ew_grid(N) * NV);
+    hipLaunchKernelGGL((ewred_kernel<NV, F>), dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f,
+                       RedBuf{c.partials.p, c.counter.p});
+}
+template <class F>
+inline void launch_scalar(Ctx &c, const F &f) {
+    hipLaunchKernelGGL(scalar_kernel<F>, dim3(1), dim3(64), 0, c.stream, f);
+}
+
+// SpMV epilogue of the Krylov operator blkdiag(A, C) applied to a Lanczos/direction vector,
+// with the two inner products <y(1:n), x(1:n)> and <y(n+1:N), x(n+1:N)> of the result against
+// the input (alpha = dot(u,vk) + dot(t,qk), pAp and qCq).  F::select(st) picks the input
+// vector and the finalize runs F::fin(st, tot).
+template <class F>
+struct EpiKrylov {
+    DState *st;
+    const double *xsel;  // resolved input vector
+    double *y;
+    int64_t n;
+    RedBuf rb;
+    F f;
+    double dn = 0.0, dm = 0.0;
+    __device__ bool skip() { return f.skip(st); }
+    __device__ const double *xvec(const double *base) {
+        xsel = f.select(st, base);
+        return xsel;
+    }
+    __device__ void row(int64_t r, double acc) {
+        y[r] = acc;
+        if (r < n) dn += acc * xsel[r];
+        else dm += acc * xsel[r];
+    }
+    __device__ void finish() {
+        double v[2] = {dn, dm}, tot[2];
+        if (grid_sum<2>(v, rb, tot) && threadIdx.x == 0) f.fin(st, tot);
+    }
+};
+
+}  // namespace cpk

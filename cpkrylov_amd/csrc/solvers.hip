@@ -1,0 +1,1490 @@
+// solvers.hip -- the six constraint-preconditioned Krylov solvers on the device.
+//
+// Each solver restates its MATLAB kernel (kernels/cp*.m) as a short sequence of fused HIP
+// kernels per iteration.  Vectors are N-vectors [x-part; y-part], so the reference's pairs
+// (vk, qk), (u, t), (wv, wq), (x, y) each live in one HBM array and one streaming pass
+// updates both halves.  All recurrence scalars stay on the device (DState); a solver
+// iteration is captured once into a hipGraph and replayed in batches, and the host only
+// polls the stop flag between batches.  Elementwise updates keep MATLAB's left-to-right
+// evaluation order with FMA contraction disabled.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <string>
+
+#include "solver_common.hpp"
+#include "solvers.hpp"
+#include "spmv.hpp"
+
+namespace cpk {
+
+namespace {
+
+constexpr double kEps100 = 100 * kEps;
+
+// ----------------------------------------------------------------------------------------------
+// Krylov SpMV policies (first kernel of an iteration): pick the input vector from the
+// iteration index and run the scalar step that consumes the two inner products.
+// ----------------------------------------------------------------------------------------------
+struct PolStart {  // starts an iteration: decides `running` from `stop`
+    __device__ static bool start(DState *st) {
+        const bool s = st->stop != 0;
+        if (blockIdx.x == 0 && threadIdx.x == 0) st->running = s ? 0 : 1;
+        return s;
+    }
+};
+
+// cpminres.m:187-189 / cpcglanczos.m:601-606 / cpsymmlq.m:231-268 : u = A*vk; t = C*qk; alpha
+template <int KIND>
+struct PolLanczosSpmv {
+    const double *VQ;
+    int64_t N;
+    int slot_shift;  // vk = VQ[(kk + slot_shift) % 3]
+    __device__ bool skip(DState *st) { return PolStart::start(st); }
+    __device__ const double *select(DState *st, const double *) {
+        const int64_t kk = st->k + 1;
+        return VQ + ((kk + slot_shift) % 3) * N;
+    }
+    __device__ void fin(DState *st, const double *tot) {
+        const int64_t kk = st->k + 1;
+        if (KIND == 1) {  // cpcglanczos
+            st->alpha = tot[0] + tot[1];
+            st->dg = st->alpha - st->low * st->low * st->dg;
+            st->zeta = st->eta / st->dg;
+        } else if (KIND == 2) {  // cpsymmlq: the loop-head norm estimates (cpsymmlq.m:233-252)
+            const double matnorm = sqrt(st->matnorm2);
+            const double epsmat = matnorm * kEps;
+            double den = st->gammabar;
+            if (den == 0) den = epsmat;
+            st->den = den;
+            st->lqresid = hypot(st->epsdelzeta, st->epsilonzeta);
+            st->qrresid = st->snprod * st->beta1;
+            st->cgresid = st->qrresid * st->beta / fabs(den);
+            push(st->hist2, st->nh2, st->hcap, st->lqresid);
+            push(st->hist3, st->nh3, st->hcap, st->qrresid);
+            push(st->hist, st->nh, st->hcap, st->cgresid);
+            st->betaold = st->beta;
+            st->alpha = tot[0] + tot[1];
+        } else {  // cpminres
+            st->alpha = tot[0] + tot[1];
+        }
+        st->k = kk;
+    }
+};
+
+// cpcg.m:405-408 : Ap = A*p; pAp; Cq = C*q; qCq; alpha = residNorm2/(pAp+qCq)
+struct PolCgSpmv {
+    const double *PQ;
+    __device__ bool skip(DState *st) { return PolStart::start(st); }
+    __device__ const double *select(DState *, const double *) { return PQ; }
+    __device__ void fin(DState *st, const double *tot) {
+        const int64_t kk = st->k + 1;
+        st->pAp = tot[0];
+        st->qCq = tot[1];
+        st->alpha = st->rn2 / (st->pAp + st->qCq);
+        if (st->aux) {
+            st->aux[3 * (kk - 1) + 0] = st->pAp;
+            st->aux[3 * (kk - 1) + 1] = st->qCq;
+            st->aux[3 * (kk - 1) + 2] = st->alpha;
+        }
+        st->k = kk;
+    }
+};
+
+// GMRES family: u = A*V_k; t = C*Q_k (no inner products needed)
+struct PolArnoldiSpmv {
+    const double *V;
+    int64_t N;
+    int64_t ring;  // 0: GMRES (column k-1), >0: DQGMRES ring size mem+1
+    __device__ bool skip(DState *st) { return PolStart::start(st); }
+    __device__ const double *select(DState *st, const double *) {
+        const int64_t kk = st->k + 1;
+        const int64_t pos = ring ? (kk - 1) % ring : (kk - 1);
+        return V + pos * N;
+    }
+    __device__ void fin(DState *st, const double *) { st->k = st->k + 1; }
+};
+
+// Pre-step spmv (cpsymmlq.m:198-200): no running/stop logic.
+struct PolPlainSpmv {
+    const double *X;
+    __device__ bool skip(DState *) { return false; }
+    __device__ const double *select(DState *, const double *) { return X; }
+    __device__ void fin(DState *st, const double *tot) { st->alpha = tot[0] + tot[1]; }
+};
+
+template <class P>
+void launch_krylov_spmv(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n, const P &pol) {
+    EpiKrylov<P> e{st, nullptr, y, n, RedBuf{c.partials.p, c.counter.p}, pol};
+    hipLaunchKernelGGL(spmv_stream<EpiKrylov<P>>, dim3((unsigned)AC.nblk), dim3(kBlock), 0, c.stream, AC.ptr.p,
+                       AC.col.p, AC.val.p, AC.blk.p, (const double *)nullptr, (int64_t)0, e);
+}
+
+// ----------------------------------------------------------------------------------------------
+// shared Lanczos pieces
+// ----------------------------------------------------------------------------------------------
+// vkp1 = vprec(1:n) - alpha*vk - beta*vkm1 ; qkp1 = qk - vprec(n+1:N); qkp1 = qkp1 - alpha*qk - beta*qkm1
+// + beta_new = dot(u, vkp1) + dot(t, qkp1)      (cpminres.m:191-194, identical in the others)
+template <int KIND>
+struct LanczosStep {
+    DState *st;
+    double *VQ;
+    const double *vprec, *ut;
+    double *xy, *W;
+    int64_t n, N;
+    int sk, skm1, skp1;  // slot offsets relative to kk
+    double alpha, beta, zeta;
+    const double *vk, *vkm1;
+    double *vkp1;
+    __device__ bool setup() {
+        if (!st->running) return false;
+        const int64_t kk = st->k;
+        alpha = st->alpha;
+        beta = st->beta;
+        zeta = st->zeta;
+        vk = VQ + ((kk + sk) % 3) * N;
+        vkm1 = VQ + ((kk + skm1) % 3) * N;
+        vkp1 = VQ + ((kk + skp1) % 3) * N;
+        return true;
+    }
+    __device__ void operator()(int64_t i, double *acc) {
+        double v;
+        if (i < n) {
+            v = vprec[i] - alpha * vk[i] - beta * vkm1[i];
+            acc[0] += ut[i] * v;
+            if (KIND == 1) xy[i] = xy[i] + zeta * W[i];  // cpcglanczos.m:607 x = x + zeta*wv
+        } else {
+            v = vk[i] - vprec[i];
+            v = v - alpha * vk[i] - beta * vkm1[i];
+            acc[1] += ut[i] * v;
+            if (KIND == 1) xy[i] = xy[i] - zeta * W[i];  // y = y - zeta*wq
+        }
+        vkp1[i] = v;
+    }
+    __device__ void fin(const double *tot);
+};
+
+__device__ inline bool check_beta(DState *st, double raw, int64_t kk) {
+    if (raw < -kEps100) {
+        st->err = 1;
+        st->err_val = raw;
+        st->err_iter = kk;
+        st->stop = 1;
+        return false;
+    }
+    return true;
+}
+
+// cpminres.m:195-235
+template <>
+__device__ void LanczosStep<0>::fin(const double *tot) {
+    const double raw = tot[0] + tot[1];
+    const int64_t kk = st->k;
+    if (!check_beta(st, raw, kk)) return;
+    const double b = sqrt(fabs(raw));
+    const double oldeps = st->epsln;
+    const double delta = st->cs * st->deltabar + st->sn * st->alpha;
+    const double gammabar = st->sn * st->deltabar - st->cs * st->alpha;
+    st->epsln = st->sn * b;
+    st->deltabar = -st->cs * b;
+    const double gamma = hypot(gammabar, b);
+    const double cs = gammabar / gamma, sn = b / gamma;
+    st->tau = cs * st->taubar;
+    st->taubar = sn * st->taubar;
+    st->cs = cs, st->sn = sn;
+    st->oldeps = oldeps, st->delta = delta, st->gamma = gamma, st->gammabar = gammabar;
+    st->beta = b;
+    st->residNorm = st->taubar;
+    push(st->hist, st->nh, st->hcap, st->residNorm);
+    st->stop = !(st->residNorm > st->stopTol && kk < st->itmax);
+}
+
+// cpcglanczos.m:616-664
+template <>
+__device__ void LanczosStep<1>::fin(const double *tot) {
+    const double raw = tot[0] + tot[1];
+    const int64_t kk = st->k;
+    if (!check_beta(st, raw, kk)) return;
+    const double b = sqrt(fabs(raw));
+    st->beta = b;
+    st->low = b / st->dg;
+    st->eta = -st->low * st->eta;
+    if (st->btol > 0) {
+        const double rho = sqrt(st->rhobar * st->rhobar + st->low * st->low);
+        const double cs = st->rhobar / rho;
+        const double sn = st->low / rho;
+        const double num = st->zeta - st->deltal * st->taul;
+        const double taubar = num / st->rhobar;
+        st->taul = num / rho;
+        st->xNorm = sqrt(st->xxNorm2 + taubar * taubar);
+        st->xxNorm2 = st->xxNorm2 + st->taul * st->taul;
+        st->deltal = sn;
+        st->rhobar = -cs;
+        st->opNorm2 = st->opNorm2 + st->alpha * st->alpha + b * b + st->oldbeta * st->oldbeta;
+        st->opNorm = sqrt(st->opNorm2);
+        st->bkerr = st->opNorm * st->xNorm + st->beta1;
+        st->bstopTol = st->btol * st->bkerr;
+        if (st->aux) {
+            st->aux[3 * (kk - 1) + 0] = st->bkerr;
+            st->aux[3 * (kk - 1) + 1] = st->opNorm;
+            st->aux[3 * (kk - 1) + 2] = st->xNorm;
+        }
+    }
+    st->residNorm = b * fabs(st->zeta);
+    push(st->hist, st->nh, st->hcap, st->residNorm);
+    st->oldbeta = b;
+    st->stop = !(st->residNorm > st->stopTol && st->residNorm > st->bstopTol && kk < st->itmax);
+}
+
+// cpsymmlq.m:273-313
+template <>
+__device__ void LanczosStep<2>::fin(const double *tot) {
+    const double raw = tot[0] + tot[1];
+    const int64_t kk = st->k;
+    if (!check_beta(st, raw, kk)) return;
+    const double b = sqrt(fabs(raw));
+    st->beta = b;
+    st->matnorm2 = st->matnorm2 + st->alpha * st->alpha + b * b + st->betaold * st->betaold;
+    const double gamma = hypot(st->gammabar, st->betaold);
+    const double cs = st->gammabar / gamma, sn = st->betaold / gamma;
+    const double delta = cs * st->deltabar + sn * st->alpha;
+    st->gammabar = sn * st->deltabar - cs * st->alpha;
+    const double epsilon = sn * b;
+    st->deltabar = -cs * b;
+    const double zeta = st->epsdelzeta / gamma;
+    st->zcs = zeta * cs;
+    st->zsn = zeta * sn;
+    st->cs = cs, st->sn = sn;
+    st->bstep = st->bstep + st->snprod * cs * zeta;
+    st->snprod = st->snprod * sn;
+    st->epsdelzeta = st->epsilonzeta - delta * zeta;
+    st->epsilonzeta = -epsilon * zeta;
+    st->stop = !(st->cgresid > st->stopTol && kk < st->itmax);
+}
+
+// ----------------------------------------------------------------------------------------------
+// device kernels as functors
+// ----------------------------------------------------------------------------------------------
+// Common solver init: vkp1 = vprec(1:n), qkp1 = -vprec(n+1:N), beta = dot(u, vkp1), plus zeroing.
+template <int KIND>
+struct InitLanczos {
+    DState *st;
+    const double *vprec, *b;
+    double *v1, *v0, *z2, *xy;
+    int64_t n;
+    __device__ bool setup() { return true; }
+    __device__ void operator()(int64_t i, double *acc) {
+        double v;
+        if (i < n) {
+            v = vprec[i];
+            acc[0] += b[i] * v;
+        } else {
+            v = -vprec[i];
+        }
+        v1[i] = v;
+        if (v0) v0[i] = 0.0;
+        if (z2) z2[i] = 0.0;
+        xy[i] = 0.0;
+    }
+    __device__ void fin(const double *tot) {
+        const double raw = tot[0];
+        st->k = 0;
+        st->running = 0;
+        if (!check_beta(st, raw, 0)) return;
+        const double b1 = sqrt(fabs(raw));
+        if (KIND == 0) {  // cpminres.m:141-164
+            st->beta = b1;
+            st->residNorm = b1;
+            st->taubar = b1;
+            st->cs = -1, st->sn = 0, st->deltabar = 0, st->epsln = 0;
+            st->stopTol = st->atol + st->rtol * st->residNorm;
+            push(st->hist, st->nh, st->hcap, st->residNorm);
+            st->stop = !(st->residNorm > st->stopTol && 0 < st->itmax);
+        } else if (KIND == 1) {  // cpcglanczos.m:534-567
+            st->beta = b1;
+            st->beta1 = b1;
+            st->residNorm = b1;
+            push(st->hist, st->nh, st->hcap, st->residNorm);
+            st->dg = 0, st->low = 1, st->eta = b1;
+            st->rhobar = 1, st->xxNorm2 = 0, st->xNorm = 0, st->taul = 0, st->deltal = 0;
+            st->oldbeta = 0, st->opNorm2 = 0;
+            st->stopTol = st->atol + st->rtol * st->residNorm;
+            st->bstopTol = st->btol * st->beta1;
+            st->stop = !(st->residNorm > st->stopTol && st->residNorm > st->bstopTol && 0 < st->itmax);
+        } else {  // cpsymmlq.m:148-189
+            st->beta1 = b1;
+            st->beta = b1;
+            st->cgresid = b1;
+            st->stopTol = st->atol + st->rtol * st->cgresid;
+            if (st->cgresid <= st->stopTol) {
+                st->lqresid = b1, st->qrresid = b1;
+                push(st->hist, st->nh, st->hcap, st->cgresid);
+                push(st->hist2, st->nh2, st->hcap, st->lqresid);
+                push(st->hist3, st->nh3, st->hcap, st->qrresid);
+                st->flag = 2;  // done before the loop
+                st->stop = 1;
+            } else {
+                st->stop = 0;
+            }
+        }
+    }
+};
+
+// if beta > 0: v1 = v1/beta ; optional copy w = v1   (cpminres.m:143-149)
+struct NormalizeCopy {
+    DState *st;
+    double *v, *w;
+    int which;  // 0: beta, 1: residNorm, 2: hk1
+    double s;
+    __device__ bool setup() {
+        s = which == 0 ? st->beta : which == 1 ? st->residNorm : st->hk1;
+        return true;
+    }
+    __device__ void operator()(int64_t i) {
+        if (which == 0 ? s > 0 : s != 0) v[i] = v[i] / s;
+        if (w) w[i] = v[i];
+    }
+};
+
+// cpminres.m:202-232 (normalisation of vkp1 and the w/x/y updates)
+struct MinresUpdate {
+    DState *st;
+    double *VQ, *W, *xy;
+    int64_t n, N;
+    double beta, oldeps, delta, gamma, tau;
+    const double *vk, *w1, *w2;
+    double *vkp1, *wn;
+    __device__ bool setup() {
+        if (!st->running) return false;
+        const int64_t kk = st->k;
+        beta = st->beta, oldeps = st->oldeps, delta = st->delta, gamma = st->gamma, tau = st->tau;
+        vk = VQ + (kk % 3) * N;
+        vkp1 = VQ + ((kk + 1) % 3) * N;
+        wn = W + (kk % 3) * N;
+        w2 = W + ((kk + 2) % 3) * N;
+        w1 = W + ((kk + 1) % 3) * N;
+        return true;
+    }
+    __device__ void operator()(int64_t i) {
+        if (beta > 0) vkp1[i] = vkp1[i] / beta;
+        const double w = (vk[i] - oldeps * w1[i] - delta * w2[i]) / gamma;
+        wn[i] = w;
+        xy[i] = (i < n) ? xy[i] + tau * w : xy[i] - tau * w;
+    }
+};
+
+// cpcglanczos.m:626-637 : normalise vkp1; wv = vkp1 - low*wv
+struct CglUpdate {
+    DState *st;
+    double *VQ, *W;
+    int64_t N;
+    double beta, low;
+    double *vkp1;
+    __device__ bool setup() {
+        if (!st->running) return false;
+        beta = st->beta, low = st->low;
+        vkp1 = VQ + ((st->k + 1) % 3) * N;
+        return true;
+    }
+    __device__ void operator()(int64_t i) {
+        if (beta > 0) vkp1[i] = vkp1[i] / beta;
+        W[i] = vkp1[i] - low * W[i];
+    }
+};
+
+// cpsymmlq.m:280-306 : normalise vkp1; x/y LQ update; w update
+struct SymmlqUpdate {
+    DState *st;
+    double *VQ, *W, *xy;
+    int64_t n, N;
+    double beta, zcs, zsn, cs, sn;
+    const double *vk;
+    double *vkp1;
+    __device__ bool setup() {
+        if (!st->running) return false;
+        const int64_t kk = st->k;
+        beta = st->beta, zcs = st->zcs, zsn = st->zsn, cs = st->cs, sn = st->sn;
+        vk = VQ + ((kk + 1) % 3) * N;
+        vkp1 = VQ + ((kk + 2) % 3) * N;
+        return true;
+    }
+    __device__ void operator()(int64_t i) {
+        if (beta > 0) vkp1[i] = vkp1[i] / beta;
+        const double w = W[i], v = vk[i];
+        if (i < n) xy[i] = xy[i] + zcs * w + zsn * v;
+        else xy[i] = xy[i] - zcs * w - zsn * v;
+        W[i] = sn * w - cs * v;
+    }
+};
+
+// cpsymmlq.m:198-225 pre-step Lanczos vector (no vkm1 term)
+struct SymmlqPre {
+    DState *st;
+    const double *vk, *vprec, *ut;
+    double *vkp1;
+    int64_t n;
+    double alpha;
+    __device__ bool setup() {
+        alpha = st->alpha;
+        return true;
+    }
+    __device__ void operator()(int64_t i, double *acc) {
+        double v;
+        if (i < n) {
+            v = vprec[i] - alpha * vk[i];
+            acc[0] += ut[i] * v;
+        } else {
+            v = vk[i] - vprec[i];
+            v = v - alpha * vk[i];
+            acc[1] += ut[i] * v;
+        }
+        vkp1[i] = v;
+    }
+    __device__ void fin(const double *tot) {
+        const double raw = tot[0] + tot[1];
+        if (raw < -kEps100) {
+            st->err = 3;  // "Iter 0, 2nd Lanczos vec"
+            st->err_val = raw;
+            st->err_iter = 0;
+            st->stop = 1;
+            return;
+        }
+        const double b = sqrt(fabs(raw));
+        st->beta = b;
+        st->gammabar = st->alpha;
+        st->deltabar = b;
+        st->epsdelzeta = st->beta1;
+        st->epsilonzeta = 0;
+        st->bstep = 0;
+        st->snprod = 1;
+        st->matnorm2 = st->alpha * st->alpha + b * b;
+        st->k = 0;
+        st->stop = !(st->cgresid > st->stopTol && 0 < st->itmax);
+    }
+};
+
+// cpsymmlq.m:317-339 post-loop scalars (single thread)
+struct SymmlqPostScalar {
+    DState *st;
+    __device__ void operator()() {
+        const double matnorm = sqrt(st->matnorm2);
+        const double epsmat = matnorm * kEps;
+        double den = st->gammabar;
+        if (den == 0) den = epsmat;
+        st->den = den;
+        st->lqresid = hypot(st->epsdelzeta, st->epsilonzeta);
+        st->qrresid = st->snprod * st->beta1;
+        push(st->hist2, st->nh2, st->hcap, st->lqresid);
+        push(st->hist3, st->nh3, st->hcap, st->qrresid);
+        st->flag = 0;
+        if (st->cgresid < st->lqresid) {
+            st->zetabar = st->epsdelzeta / den;
+            st->bstep = st->bstep + st->snprod * st->zetabar;
+            st->flag = 1;
+        }
+    }
+};
+struct SymmlqMoveCg {
+    DState *st;
+    double *xy;
+    const double *W;
+    int64_t n;
+    double z;
+    __device__ bool setup() {
+        if (st->flag != 1) return false;
+        z = st->zetabar;
+        return true;
+    }
+    __device__ void operator()(int64_t i) { xy[i] = (i < n) ? xy[i] + z * W[i] : xy[i] - z * W[i]; }
+};
+// cpsymmlq.m:342-347 : x = x + (bstep/beta1)*vk ; y = y - (bstep/beta1)*qk, qk = -vprec2
+struct SymmlqFirstStep {
+    DState *st;
+    double *xy;
+    const double *vprec;
+    int64_t n;
+    double bs;
+    __device__ bool setup() {
+        bs = st->bstep / st->beta1;
+        return true;
+    }
+    __device__ void operator()(int64_t i) {
+        if (i < n) xy[i] = xy[i] + bs * vprec[i];
+        else xy[i] = xy[i] - bs * (-vprec[i]);
+    }
+};
+
+// ---- cpcg ----------------------------------------------------------------------------------
+struct CgInit0 {  // g = -b ; w = 0 ; x = 0 ; a = 0
+    const double *b;
+    double *GW, *XA;
+    int64_t n;
+    __device__ bool setup() { return true; }
+    __device__ void operator()(int64_t i) {
+        GW[i] = i < n ? -b[i] : 0.0;
+        XA[i] = 0.0;
+    }
+};
+struct CgInit1 {  // p = -r; q = -u; residNorm2 = g'*r   (cpcg.m:380-387)
+    DState *st;
+    const double *RU, *GW;
+    double *PQ;
+    int64_t n;
+    __device__ bool setup() { return true; }
+    __device__ void operator()(int64_t i, double *acc) {
+        PQ[i] = -RU[i];
+        if (i < n) acc[0] += GW[i] * RU[i];
+    }
+    __device__ void fin(const double *tot) {
+        st->k = 0;
+        st->running = 0;
+        st->rn2 = tot[0];
+        if (st->rn2 < 0) {
+            st->err = 2, st->err_val = st->rn2, st->err_iter = 0, st->stop = 1;
+            return;
+        }
+        st->residNorm = sqrt(st->rn2);
+        st->stopTol = st->atol + st->rtol * st->residNorm;
+        push(st->hist, st->nh, st->hcap, st->residNorm);
+        st->stop = !(st->residNorm > st->stopTol && 0 < st->itmax);
+    }
+};
+struct CgStep {  // x += alpha p; a += alpha q; g += alpha Ap; w += alpha Cq   (cpcg.m:415-418)
+    DState *st;
+    double *XA, *GW;
+    const double *PQ, *APCQ;
+    double alpha;
+    __device__ bool setup() {
+        if (!st->running) return false;
+        alpha = st->alpha;
+        return true;
+    }
+    __device__ void operator()(int64_t i) {
+        XA[i] = XA[i] + alpha * PQ[i];
+        GW[i] = GW[i] + alpha * APCQ[i];
+    }
+};
+struct CgResid {  // t = a + u; residNorm2_new = g'*r + t'*w   (cpcg.m:421-429)
+    DState *st;
+    const double *XA, *RU, *GW;
+    double *TT;
+    int64_t n;
+    __device__ bool setup() { return st->running != 0; }
+    __device__ void operator()(int64_t i, double *acc) {
+        if (i < n) {
+            acc[0] += GW[i] * RU[i];
+        } else {
+            const double t = XA[i] + RU[i];
+            TT[i] = t;
+            acc[1] += t * GW[i];
+        }
+    }
+    __device__ void fin(const double *tot) {
+        const int64_t kk = st->k;
+        const double nw = tot[0] + tot[1];
+        st->beta = nw / st->rn2;
+        st->rn2 = nw;
+        if (st->rn2 < 0) {
+            st->err = 2, st->err_val = st->rn2, st->err_iter = kk, st->stop = 1;
+            return;
+        }
+        st->residNorm = sqrt(st->rn2);
+        push(st->hist, st->nh, st->hcap, st->residNorm);
+        st->stop = !(st->residNorm > st->stopTol && kk < st->itmax);
+    }
+};
+struct CgDir {  // p = -r + beta*p; q = -t + beta*q
+    DState *st;
+    const double *RU, *TT;
+    double *PQ;
+    int64_t n;
+    double beta;
+    __device__ bool setup() {
+        if (!st->running) return false;
+        beta = st->beta;
+        return true;
+    }
+    __device__ void operator()(int64_t i) { PQ[i] = (i < n ? -RU[i] : -TT[i]) + beta * PQ[i]; }
+};
+
+// ---- GMRES family --------------------------------------------------------------------------
+// Start of a GMRES cycle / DQGMRES init:
+//   V1 = w(1:n); Q1 = (restart ? y : 0) - w(n+1:N); residNorm = sqrt(dot(u,V1) + dot(t,Q1))
+struct ArnoldiStart {
+    DState *st;
+    const double *w, *ut, *xy;
+    double *v1;
+    int64_t n;
+    int restart_cycle;  // outer > 1 (cpgmres.m:166-171)
+    int dq;             // DQGMRES: dot(u, V1) only (cpdqgmres.m:428)
+    int first;          // first cycle: sets stopTol and pushes the history
+    __device__ bool setup() { return true; }
+    __device__ void operator()(int64_t i, double *acc) {
+        double v;
+        if (i < n) {
+            v = w[i];
+            acc[0] += ut[i] * v;
+        } else {
+            v = restart_cycle ? xy[i] - w[i] : -w[i];
+            if (!dq) acc[1] += ut[i] * v;
+        }
+        v1[i] = v;
+    }
+    __device__ void fin(const double *tot) {
+        const double rn2 = tot[0] + tot[1];
+        st->k = 0;
+        st->running = 0;
+        if (rn2 < 0) {
+            st->err = 4, st->err_val = rn2, st->err_iter = 0, st->stop = 1;
+            return;
+        }
+        st->residNorm = sqrt(rn2);
+        if (first) {
+            st->stopTol = st->atol + st->rtol * st->residNorm;
+            push(st->hist, st->nh, st->hcap, st->residNorm);
+        }
+        st->g[0] = st->residNorm;
+        const int64_t lim = dq ? st->itmax : st->restart;
+        st->stop = !(st->residNorm > st->stopTol && 0 < lim);
+    }
+};
+
+// Restart residual: u = b - A*x (rows < n of TMP = blkdiag(A,C)*xy), t = C*y   (cpgmres.m:167-168)
+struct GmresRestartRhs {
+    const double *b, *tmp;
+    double *ut;
+    int64_t n;
+    __device__ bool setup() { return true; }
+    __device__ void operator()(int64_t i) { ut[i] = i < n ? b[i] - tmp[i] : tmp[i]; }
+};
+
+// The Arnoldi window of iteration kk: GMRES j = 1..kk at column j-1;
+// DQGMRES j = max(1, kk-mem+1)..kk at ring slot (j-1) % (mem+1).
+struct Window {
+    int64_t kk, jlo, nv, ring;
+    __device__ int64_t slot(int64_t j) const { return ring ? (j - 1) % ring : (j - 1); }
+};
+__device__ inline Window window(const DState *st, int64_t ring) {
+    Window w;
+    w.kk = st->k;
+    w.ring = ring;
+    w.jlo = ring ? max((int64_t)1, w.kk - st->mem + 1) : 1;
+    w.nv = w.kk - w.jlo + 1;
+    return w;
+}
+// H storage: GMRES column-major (restart+1) x restart; DQGMRES ring of (mem+2) rows, width mem+2,
+// indexed by the reference's (j, kk) with kk the diagonal-compressed column.
+__device__ inline double &Hg(DState *st, int64_t i1, int64_t j1) {  // H(i1, j1), 1-based
+    return st->H[(i1 - 1) + (j1 - 1) * (st->restart + 1)];
+}
+__device__ inline double &Hd(DState *st, int64_t j, int64_t kk) {  // H(j, kk), 1-based
+    const int64_t W = st->mem + 2;
+    return st->H[(j % W) * W + (kk - 1)];
+}
+
+// V(:,k+1) = w(1:n) ; Q(:,k+1) = Q(:,k) - w(n+1:N) ; H(j,k) = dot(V_j,u) + dot(Q_j,t) for the window
+// (cpgmres.m:212-215, cpdqgmres.m:479-484).  All window dots in one streaming pass.
+constexpr int kDotGroup = 8;
+__global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double *V, const double *w,
+                                                              const double *ut, int64_t n, int64_t N, int64_t ring,
+                                                              int64_t maxv, RedBuf rb) {
+    if (!st->running) return;
+    const Window win = window(st, ring);
+    const int64_t kk = win.kk;
+    double *vnew = V + (ring ? (kk % ring) : kk) * N;
+    const double *vk = V + win.slot(kk) * N;
+    // phase 0: new basis vector (fused with the first dot group)
+    for (int64_t g0 = 0; g0 < win.nv; g0 += kDotGroup) {
+        double acc[2 * kDotGroup];
+#pragma unroll
+        for (int j = 0; j < 2 * kDotGroup; j++) acc[j] = 0.0;
+        const double *vj[kDotGroup];
+#pragma unroll
+        for (int j = 0; j < kDotGroup; j++) vj[j] = (g0 + j < win.nv) ? V + win.slot(win.jlo + g0 + j) * N : nullptr;
+        for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) {
+            const double u = ut[i];
+            if (g0 == 0) vnew[i] = i < n ? w[i] : vk[i] - w[i];
+            const int part = i < n ? 0 : 1;
+#pragma unroll
+            for (int j = 0; j < kDotGroup; j++)
+                if (vj[j]) acc[2 * j + part] += vj[j][i] * u;
+        }
+        block_sum<2 * kDotGroup>(acc);
+        if (threadIdx.x == 0)
+            for (int j = 0; j < 2 * kDotGroup && 2 * g0 + j < 2 * win.nv; j++)
+                st_agent(rb.partials + (size_t)blockIdx.x * 2 * maxv + 2 * g0 + j, acc[j]);
+    }
+    __shared__ int s_last;
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned prev = __hip_atomic_fetch_add(rb.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (prev == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __shared__ double hv[2];
+    if (ring && threadIdx.x == 0) {  // fresh ring row for H(kk, .)
+        for (int64_t c = 1; c <= st->mem + 2; c++) Hd(st, kk, c) = 0.0;
+    }
+    for (int64_t j = 0; j < 2 * win.nv; j++) {
+        double a[1] = {0.0};
+        for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x)
+            a[0] += ld_agent(rb.partials + (size_t)b * 2 * maxv + j);
+        block_sum<1>(a);
+        if (threadIdx.x == 0) hv[j & 1] = a[0];
+        __syncthreads();
+        if (threadIdx.x == 0 && (j & 1)) {
+            const int64_t jj = win.jlo + j / 2;
+            const double h = hv[0] + hv[1];
+            if (ring) Hd(st, jj, 2 + kk - jj) = h;
+            else Hg(st, jj, kk) = h;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(rb.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// V(:,k+1) -= H(j,k) V(:,j) for the window in order; H(k+1,k) = sqrt(dot(u,V_{k+1}) + dot(t,Q_{k+1}));
+// then rotations, SymGivens and the g update (cpgmres.m:214-247, cpdqgmres.m:481-521).
+struct ArnoldiOrth {
+    DState *st;
+    double *V;
+    const double *ut;
+    int64_t n, N, ring;
+    Window win;
+    double *vnew;
+    __device__ bool setup() {
+        if (!st->running) return false;
+        win = window(st, ring);
+        vnew = V + (ring ? (win.kk % ring) : win.kk) * N;
+        return true;
+    }
+    __device__ double h(int64_t j) const {
+        return ring ? Hd(st, j, 2 + win.kk - j) : Hg(st, j, win.kk);
+    }
+    __device__ void operator()(int64_t i, double *acc) {
+        double v = vnew[i];
+        for (int64_t j = win.jlo; j <= win.kk; j++) v = v - h(j) * V[win.slot(j) * N + i];
+        vnew[i] = v;
+        acc[i < n ? 0 : 1] += ut[i] * v;
+    }
+    __device__ void fin(const double *tot) {
+        const int64_t kk = win.kk;
+        const double hn2 = tot[0] + tot[1];
+        if (hn2 < 0) {
+            st->err = 4, st->err_val = hn2, st->err_iter = kk, st->stop = 1;
+            return;
+        }
+        const double hk1 = sqrt(hn2);
+        st->hk1 = hk1;
+        if (!ring) {  // cpgmres.m:219-247
+            Hg(st, kk + 1, kk) = hk1;
+            for (int64_t j = 1; j <= kk - 1; j++) {
+                const double Hjk = st->c[j - 1] * Hg(st, j, kk) + st->s[j - 1] * Hg(st, j + 1, kk);
+                Hg(st, j + 1, kk) = st->s[j - 1] * Hg(st, j, kk) - st->c[j - 1] * Hg(st, j + 1, kk);
+                Hg(st, j, kk) = Hjk;
+            }
+            double c, s, d;
+            sym_givens(Hg(st, kk, kk), Hg(st, kk + 1, kk), c, s, d);
+            st->c[kk - 1] = c, st->s[kk - 1] = s, Hg(st, kk, kk) = d;
+            Hg(st, kk + 1, kk) = 0;
+            st->g[kk] = s * st->g[kk - 1];
+            st->g[kk - 1] = c * st->g[kk - 1];
+            st->residNorm = fabs(st->g[kk]);
+            push(st->hist, st->nh, st->hcap, st->residNorm);
+            st->stop = !(st->residNorm > st->stopTol && kk < st->restart);
+        } else {  // cpdqgmres.m:489-539
+            const int64_t mem = st->mem, M1 = mem + 1;
+            const int64_t kpos = (kk - 1) % M1, kp1pos = kk % M1, rotpos = (kk - 1) % mem;
+            Hd(st, kk, 1) = hk1;
+            for (int64_t j = max((int64_t)1, kk - mem); j <= kk - 1; j++) {
+                const int64_t jr = (j - 1) % mem, k1 = kk - j + 1, k2 = k1 + 1;
+                const double Hjk = st->c[jr] * Hd(st, j, k2) + st->s[jr] * Hd(st, j + 1, k1);
+                Hd(st, j + 1, k1) = st->s[jr] * Hd(st, j, k2) - st->c[jr] * Hd(st, j + 1, k1);
+                Hd(st, j, k2) = Hjk;
+            }
+            double c, s, d;
+            sym_givens(Hd(st, kk, 2), Hd(st, kk, 1), c, s, d);
+            st->c[rotpos] = c, st->s[rotpos] = s, Hd(st, kk, 2) = d;
+            Hd(st, kk, 1) = 0;
+            st->g[kp1pos] = s * st->g[kpos];
+            st->g[kpos] = c * st->g[kpos];
+            st->residNorm = fabs(st->g[kp1pos]);
+            push(st->hist, st->nh, st->hcap, st->residNorm);
+            st->stop = !(st->residNorm > st->stopTol && kk < st->itmax);
+        }
+    }
+};
+
+// GMRES: V(:,k+1) /= H(k+1,k) (lucky breakdown if 0)
+struct GmresNormalize {
+    DState *st;
+    double *V;
+    int64_t N;
+    double h;
+    double *v;
+    __device__ bool setup() {
+        if (!st->running) return false;
+        h = st->hk1;
+        v = V + st->k * N;
+        return true;
+    }
+    __device__ void operator()(int64_t i) {
+        if (h != 0) v[i] = v[i] / h;
+    }
+};
+
+// DQGMRES: normalise V(:,kp1pos); PV(:,kpos) = (V(:,kpos) - sum H(j,kk) PV(:,jpos)) / H(k,2);
+// x = x + g(kpos)*PV(:,kpos); y = y - g(kpos)*PQ(:,kpos)   (cpdqgmres.m:493-536)
+struct DqgmresDirection {
+    DState *st;
+    double *V, *PV, *xy;
+    int64_t n, N;
+    int64_t kk, mem, M1, kpos, jlo;
+    double h, hkk, gk;
+    __device__ bool setup() {
+        if (!st->running) return false;
+        kk = st->k, mem = st->mem, M1 = mem + 1;
+        kpos = (kk - 1) % M1;
+        jlo = max((int64_t)1, kk - mem);
+        h = st->hk1;
+        hkk = Hd(st, kk, 2);
+        gk = st->g[kpos];
+        return true;
+    }
+    __device__ void operator()(int64_t i) {
+        double *vn = V + (kk % M1) * N;
+        if (h != 0) vn[i] = vn[i] / h;
+        double pv = V[kpos * N + i];
+        for (int64_t j = jlo; j <= kk - 1; j++) pv = pv - Hd(st, j, 2 + kk - j) * PV[((j - 1) % M1) * N + i];
+        pv = pv / hkk;
+        PV[kpos * N + i] = pv;
+        xy[i] = i < n ? xy[i] + gk * pv : xy[i] - gk * pv;
+    }
+};
+
+// z = H(1:k,1:k) \ g(1:k): column-oriented back substitution (cpgmres.m:257)
+struct GmresBackSolve {
+    DState *st;
+    __device__ void operator()() {
+        const int64_t k = st->k;
+        for (int64_t i = 0; i < k; i++) st->z[i] = st->g[i];
+        for (int64_t j = k; j >= 1; j--) {
+            st->z[j - 1] = st->z[j - 1] / Hg(st, j, j);
+            for (int64_t i = 1; i < j; i++) st->z[i - 1] = st->z[i - 1] - st->z[j - 1] * Hg(st, i, j);
+        }
+    }
+};
+// x = x + V(:,1:k)*z ; q = 0 + Q(:,1:k)*z ; y = y - q   (cpgmres.m:258-260)
+struct GmresUpdateX {
+    DState *st;
+    const double *V;
+    double *xy;
+    int64_t n, N, k;
+    __device__ bool setup() {
+        k = st->k;
+        return true;
+    }
+    __device__ void operator()(int64_t i) {
+        double t = 0.0;
+        for (int64_t j = 0; j < k; j++) t = t + V[j * N + i] * st->z[j];
+        if (i < n) xy[i] = xy[i] + t;
+        else xy[i] = xy[i] - (0.0 + t);
+    }
+};
+
+// reg_cpkrylov.m:157 : b1 = b(1:n) - A*xy0(1:n) - B'*xy0(n+1:N)
+struct ShiftRhs {
+    const double *b, *t1, *t2;
+    double *b1;
+    __device__ bool setup() { return true; }
+    __device__ void operator()(int64_t i) { b1[i] = b[i] - t1[i] - t2[i]; }
+};
+// x = [xy0(1:n) + dx; xy0(n+1:N) + dy]
+struct Recover {
+    const double *xy0, *dxy;
+    double *x;
+    __device__ bool setup() { return true; }
+    __device__ void operator()(int64_t i) { x[i] = xy0[i] + dxy[i]; }
+};
+struct AnyNonzero {  // any(b(n+1:n+m))
+    const double *b;
+    int64_t n;
+    int *out;
+    __device__ bool setup() { return true; }
+    __device__ void operator()(int64_t i, double *acc) {
+        if (b[n + i] != 0) acc[0] = 1.0;
+    }
+    __device__ void fin(const double *tot) { *out = tot[0] != 0 ? 1 : 0; }
+};
+struct Copy {
+    const double *src;
+    double *dst;
+    __device__ bool setup() { return true; }
+    __device__ void operator()(int64_t i) { dst[i] = src[i]; }
+};
+
+}  // namespace
+
+// ==============================================================================================
+// host driver
+// ==============================================================================================
+struct SolveCore {
+    Ctx &c;
+    Precond &M;
+    const DMat &AC;
+    int64_t n, m, N;
+    int method;
+    bool print = true;
+    double atol = 1e-6, rtol = 1e-6, btol = 0, itmax = 0, restart = 50, mem = 50;
+    DBuf<DState> dst;
+    DState h{};
+    DBuf<double> hist, hist2, hist3, aux, H, cvec, svec, gvec, zvec;
+    std::vector<DBuf<double>> vecs;
+    int64_t printed = 0;
+    int batch = 16;
+    bool use_graph = true;
+
+    SolveCore(Ctx &cc, Precond &MM, const DMat &ACm, int meth, const cpk_opts *o)
+        : c(cc), M(MM), AC(ACm), n(MM.n), m(MM.m), N(MM.N), method(meth) {
+        const double itmax_default = (meth == CPK_GMRES || meth == CPK_DQGMRES) ? (double)(n + m) : (double)n;
+        itmax = itmax_default;
+        if (o) {
+            if (o->has_atol) atol = o->atol;
+            if (o->has_rtol) rtol = o->rtol;
+            if (o->has_btol) btol = o->btol;
+            if (o->has_itmax) itmax = o->itmax;
+            if (o->has_restart) restart = o->restart;
+            if (o->has_mem) mem = std::max(1.0, o->mem);  // cpdqgmres.m:116-118
+            if (o->has_print) print = o->print != 0;
+        }
+        if (const char *e = getenv("CPK_NO_GRAPH")) use_graph = atoi(e) == 0;
+        if (const char *e = getenv("CPK_BATCH")) batch = std::max(1, atoi(e));
+    }
+
+    double *vec(size_t i) {
+        while (vecs.size() <= i) {
+            vecs.emplace_back();
+            vecs.back().alloc(N);
+        }
+        return vecs[i].p;
+    }
+    // a fresh contiguous allocation of `count` N-vectors (slot rings)
+    std::vector<DBuf<double>> rings;
+    double *ring(size_t count) {
+        rings.emplace_back();
+        rings.back().alloc(count * (size_t)N);
+        return rings.back().p;
+    }
+
+    void setup_state(int64_t hcap, int64_t maxv) {
+        dst.alloc(1);
+        std::memset(&h, 0, sizeof h);
+        h.itmax = (int64_t)std::min(itmax, 9.0e15);
+        if (h.itmax < 0) h.itmax = 0;
+        h.atol = atol, h.rtol = rtol, h.btol = btol;
+        h.hcap = hcap;
+        hist.alloc(hcap);
+        hist2.alloc(hcap);
+        hist3.alloc(hcap);
+        aux.alloc(3 * hcap);
+        h.hist = hist.p, h.hist2 = hist2.p, h.hist3 = hist3.p, h.aux = aux.p;
+        h.restart = (int64_t)restart;
+        h.mem = (int64_t)mem;
+        if (maxv > 0) {
+            const int64_t R = h.restart, Mm = h.mem;
+            if (method == CPK_GMRES) {
+                H.alloc((R + 1) * R);
+                cvec.alloc(R), svec.alloc(R), gvec.alloc(R + 1), zvec.alloc(R);
+            } else {
+                H.alloc((Mm + 2) * (Mm + 2));
+                cvec.alloc(Mm), svec.alloc(Mm), gvec.alloc(Mm + 1), zvec.alloc(1);
+            }
+            H.zero(c.stream), cvec.zero(c.stream), svec.zero(c.stream), gvec.zero(c.stream);
+            h.H = H.p, h.c = cvec.p, h.s = svec.p, h.g = gvec.p, h.z = zvec.p;
+        }
+        CPK_HIP(hipMemcpyAsync(dst.p, &h, sizeof h, hipMemcpyHostToDevice, c.stream));
+        size_t need = std::max<size_t>((size_t)AC.nblk * 2, (size_t)M.dKp.nblk * 2);
+        need = std::max<size_t>(need, (size_t)kEwGrid * 2);
+        need = std::max<size_t>(need, (size_t)kEwGrid * 2 * std::max<int64_t>(maxv, 1));
+        c.ensure_partials(need);
+    }
+
+    void pull() {
+        CPK_HIP(hipMemcpyAsync(&h, dst.p, sizeof h, hipMemcpyDeviceToHost, c.stream));
+        CPK_HIP(hipStreamSynchronize(c.stream));
+    }
+
+    // replay `body` (one iteration) in batches until the device sets `stop`
+    void loop(const std::function<void()> &body, const std::function<void()> &printer) {
+        pull();
+        if (h.stop) return;
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        if (use_graph) {
+            CPK_HIP(hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
+            for (int b = 0; b < batch; b++) body();
+            CPK_HIP(hipStreamEndCapture(c.stream, &graph));
+            CPK_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+        }
+        const int64_t guard = h.k + (int64_t)std::min(itmax, 4.0e9) + 2 * batch + 2;
+        for (;;) {
+            if (exec) CPK_HIP(hipGraphLaunch(exec, c.stream));
+            else
+                for (int b = 0; b < batch; b++) body();
+            pull();
+            if (print && printer) printer();
+            if (h.stop) break;
+            if (h.k > guard) {
+                if (exec) (void)hipGraphExecDestroy(exec), (void)hipGraphDestroy(graph);
+                throw Error(CPK_ERR_HIP, "solver loop did not terminate");
+            }
+        }
+        if (exec) {
+            CPK_HIP(hipGraphExecDestroy(exec));
+            CPK_HIP(hipGraphDestroy(graph));
+        }
+    }
+
+    std::vector<double> fetch(const DBuf<double> &d, int64_t len) {
+        std::vector<double> v(std::max<int64_t>(len, 0));
+        if (len > 0) CPK_HIP(hipMemcpy(v.data(), d.p, len * sizeof(double), hipMemcpyDeviceToHost));
+        return v;
+    }
+
+    void print_hist_lines(const char *fmt, int64_t offset = 0) {
+        if (h.nh <= printed) return;
+        auto v = fetch(hist, std::min(h.nh, h.hcap));
+        for (int64_t i = printed; i < (int64_t)v.size(); i++) printf(fmt, (long long)(i + offset), v[i]);
+        printed = (int64_t)v.size();
+        fflush(stdout);
+    }
+
+    void raise_error() {
+        char buf[256];
+        if (h.err == 1) {
+            if (method == CPK_CGLANCZOS)
+                snprintf(buf, sizeof buf,
+                         "CPCGLanczos:IndefiniteError: Iter %lld, beta (before sqrt) = %g : preconditioner not second-order sufficient",
+                         (long long)h.err_iter, h.err_val);
+            else
+                snprintf(buf, sizeof buf,
+                         "Iter %lld, beta (before sqrt) = %g : preconditioner does not behave as a spd matrix.",
+                         (long long)h.err_iter, h.err_val);
+        } else if (h.err == 3) {
+            snprintf(buf, sizeof buf,
+                     "Iter 0, 2nd Lanczos vec, beta (before sqrt) = %g : preconditioner does not behave as a spd matrix.",
+                     h.err_val);
+        } else if (h.err == 2) {
+            snprintf(buf, sizeof buf, "Iter %lld, residNorm2 = %g < 0: complex residual norm", (long long)h.err_iter,
+                     h.err_val);
+        } else {
+            snprintf(buf, sizeof buf, "Iter %lld: negative squared norm %g (complex square root)",
+                     (long long)h.err_iter, h.err_val);
+        }
+        throw Error(CPK_ERR_INDEFINITE, buf);
+    }
+
+    // ------------------------------------------------------------------------------------------
+    void minres_like(int kind, const double *b, double *xy, cpk_stats *stats);
+    void cg(const double *b, double *xy, cpk_stats *stats);
+    void gmres(const double *b, double *xy, cpk_stats *stats);
+    void dqgmres(const double *b, double *xy, cpk_stats *stats);
+
+    void finish_stats(cpk_stats *stats) {
+        if (!stats) return;
+        stats->niters = h.k;
+        stats->status = 0;
+        auto cp = [&](double *dstp, const DBuf<double> &src, int64_t len, int64_t *outlen, int prefix, double pv) {
+            *outlen = len + (prefix ? 1 : 0);
+            if (!dstp) return;
+            if (*outlen > stats->hist_cap) throw Error(CPK_ERR_ARGS, "history buffer too small");
+            int64_t off = 0;
+            if (prefix) dstp[0] = pv, off = 1;
+            if (len > 0) CPK_HIP(hipMemcpy(dstp + off, src.p, len * sizeof(double), hipMemcpyDeviceToHost));
+        };
+        if (method == CPK_SYMMLQ) {
+            const int prefix = h.flag != 2;  // cgresidHistory = [beta1; cgresidHistory]
+            cp(stats->hist, hist, std::min(h.nh, h.hcap), &stats->hist_len, prefix, h.beta1);
+            cp(stats->hist_lq, hist2, std::min(h.nh2, h.hcap), &stats->lq_len, 0, 0);
+            cp(stats->hist_qr, hist3, std::min(h.nh3, h.hcap), &stats->qr_len, 0, 0);
+        } else {
+            cp(stats->hist, hist, std::min(h.nh, h.hcap), &stats->hist_len, 0, 0);
+            stats->lq_len = stats->qr_len = 0;
+        }
+    }
+};
+
+// ---- cpminres / cpcglanczos / cpsymmlq ------------------------------------------------------
+void SolveCore::minres_like(int kind, const double *b, double *xy, cpk_stats *stats) {
+    const int64_t hcap = (int64_t)std::min(itmax, 1.0e8) + 4;
+    setup_state(hcap, 0);
+    DState *st = dst.p;
+    double *VQ = ring(3);  // Lanczos vectors [vk; qk] for k-1, k, k+1
+    double *W = ring(3);   // [wv; wq] (3 slots for minres, 1 for the others)
+    double *UT = vec(0), *VPREC = vec(1);
+    // vprec = M * [u; t] with u = b, t = 0
+    launch_set_concat(c, UT, b, n, m);
+    M.apply(UT, N, VPREC, nullptr);
+    if (kind == 0)
+        launch_ewred<1>(c, N, InitLanczos<0>{st, VPREC, b, VQ + N, VQ, W + 2 * N, xy, n});
+    else if (kind == 1)
+        launch_ewred<1>(c, N, InitLanczos<1>{st, VPREC, b, VQ + N, VQ, nullptr, xy, n});
+    else
+        launch_ewred<1>(c, N, InitLanczos<2>{st, VPREC, b, VQ + N, VQ, W, xy, n});
+    launch_ew(c, N, NormalizeCopy{st, VQ + N, kind == 2 ? nullptr : W, 0, 0.0});
+    CPK_HIP(hipGetLastError());
+    pull();
+    if (h.err) raise_error();
+    if (kind == 0) {
+        if (print) {
+            printf("\n**** Constraint-preconditioned version of MINRES ****\n\n");
+            printf("stopTol = %e\n", h.stopTol);
+            printf("%5s  %9s\n", "iter", "|resid|");
+        }
+        auto body = [&]() {
+            launch_krylov_spmv(c, AC, st, UT, n, PolLanczosSpmv<0>{VQ, N, 0});
+            M.apply(UT, n, VPREC, &st->running);
+            launch_ewred<2>(c, N, LanczosStep<0>{st, VQ, VPREC, UT, xy, W, n, N, 0, 2, 1});
+            launch_ew(c, N, MinresUpdate{st, VQ, W, xy, n, N});
+        };
+        if (print) print_hist_lines("%5lld  %9.2e\n");
+        loop(body, [&]() { print_hist_lines("%5lld  %9.2e\n"); });
+        if (h.err) raise_error();
+        if (print) printf("\n");
+        if (stats) stats->solved = h.residNorm <= h.stopTol;
+    } else if (kind == 1) {
+        if (print) {
+            printf("\n**** Constraint-preconditioned version of CP-CGLanczos ****\n\n");
+            printf("stopTol = %e, bstopTol = %e\n", h.stopTol, h.bstopTol);
+            printf("%5s  %9s", "iter", "|resid|");
+            if (btol > 0) printf("  %9s  %9s  %9s", "bkerr", "|op|", "|x|");
+            printf("\n");
+        }
+        auto pr = [&]() {
+            if (h.nh <= printed) return;
+            auto v = fetch(hist, std::min(h.nh, h.hcap));
+            auto a = fetch(aux, 3 * std::min(h.nh, h.hcap));
+            for (int64_t i = printed; i < (int64_t)v.size(); i++) {
+                printf("%5lld  %9.2e", (long long)i, v[i]);
+                if (btol > 0)
+                    printf("  %9.2e  %9.2e  %9.2e", i ? v[i] / a[3 * (i - 1)] : 0.0, i ? a[3 * (i - 1) + 1] : 0.0,
+                           i ? a[3 * (i - 1) + 2] : 0.0);
+                printf("\n");
+            }
+            printed = (int64_t)v.size();
+        };
+        auto body = [&]() {
+            launch_krylov_spmv(c, AC, st, UT, n, PolLanczosSpmv<1>{VQ, N, 0});
+            M.apply(UT, n, VPREC, &st->running);
+            launch_ewred<2>(c, N, LanczosStep<1>{st, VQ, VPREC, UT, xy, W, n, N, 0, 2, 1});
+            launch_ew(c, N, CglUpdate{st, VQ, W, N});
+        };
+        if (print) pr();
+        loop(body, pr);
+        if (h.err) raise_error();
+        if (print) printf("\n");
+        if (stats) {
+            stats->solved = 0, stats->status = 0;
+            if (h.residNorm <= h.stopTol) stats->solved = 1, stats->status = 1;
+            if (btol > 0 && h.residNorm <= h.bstopTol) stats->solved = 1, stats->status = 2;
+        }
+        finish_stats(stats);
+        if (stats) {
+            stats->solved = 0, stats->status = 0;
+            if (h.residNorm <= h.stopTol) stats->solved = 1, stats->status = 1;
+            if (btol > 0 && h.residNorm <= h.bstopTol) stats->solved = 1, stats->status = 2;
+        }
+        return;
+    } else {
+        // cpsymmlq: the cpsymmlq.m:182 `printf` quirk is not reproduced
+        if (print) {
+            printf("\n**** Constraint-preconditioned version of SYMMLQ ****\n\n");
+            printf("the printed |cgresid| is one iter ahead, unless the solver\nstops at iter = 0\n\n");
+            printf("stopTol = %e\n", h.stopTol);
+            printf("%5s   %9s   %9s   %9s\n", "iter", "|cgresid|", "|lqresid|", "|qrresid|");
+        }
+        if (h.flag != 2) {
+            // pre-step: second Lanczos vector (cpsymmlq.m:193-225), vk = VQ[1], vkp1 -> VQ[2]
+            launch_krylov_spmv(c, AC, st, UT, n, PolPlainSpmv{VQ + N});
+            M.apply(UT, n, VPREC, nullptr);
+            launch_ewred<2>(c, N, SymmlqPre{st, VQ + N, VPREC, UT, VQ + 2 * N, n});
+            launch_ew(c, N, NormalizeCopy{st, VQ + 2 * N, nullptr, 0, 0.0});
+            CPK_HIP(hipGetLastError());
+            pull();
+            if (h.err) raise_error();
+            auto pr = [&]() {
+                if (h.nh <= printed) return;
+                auto cgv = fetch(hist, std::min(h.nh, h.hcap));
+                auto lq = fetch(hist2, std::min(h.nh2, h.hcap));
+                auto qr = fetch(hist3, std::min(h.nh3, h.hcap));
+                for (int64_t i = printed; i < (int64_t)cgv.size(); i++)
+                    printf("%5lld  %9.2e   %9.2e    %9.2e\n", (long long)i, cgv[i], lq[i], qr[i]);
+                printed = (int64_t)cgv.size();
+            };
+            auto body = [&]() {
+                launch_krylov_spmv(c, AC, st, UT, n, PolLanczosSpmv<2>{VQ, N, 1});
+                M.apply(UT, n, VPREC, &st->running);
+                launch_ewred<2>(c, N, LanczosStep<2>{st, VQ, VPREC, UT, xy, W, n, N, 1, 0, 2});
+                launch_ew(c, N, SymmlqUpdate{st, VQ, W, xy, n, N});
+            };
+            loop(body, pr);
+            if (h.err) raise_error();
+            launch_scalar(c, SymmlqPostScalar{st});
+            launch_ew(c, N, SymmlqMoveCg{st, xy, W, n});
+            launch_set_concat(c, UT, b, n, m);
+            M.apply(UT, N, VPREC, nullptr);
+            launch_ew(c, N, SymmlqFirstStep{st, xy, VPREC, n});
+            CPK_HIP(hipGetLastError());
+            pull();
+            if (print) printf("%5lld     ---      %9.2e    %9.2e\n\n", (long long)h.k, h.lqresid, h.qrresid);
+        } else if (print) {
+            printf("%5lld  %9.2e   %9.2e    %9.2e\n", 0LL, h.cgresid, h.lqresid, h.qrresid);
+        }
+        if (stats) stats->solved = h.cgresid <= h.stopTol;
+    }
+    finish_stats(stats);
+}
+
+// ---- cpcg -------------------------------------------------------------------------------------
+void SolveCore::cg(const double *b, double *xy, cpk_stats *stats) {
+    const int64_t hcap = (int64_t)std::min(itmax, 1.0e8) + 4;
+    setup_state(hcap, 0);
+    DState *st = dst.p;
+    double *GW = vec(0), *PQ = vec(1), *APCQ = vec(2), *RU = vec(3), *TT = vec(4);
+    double *XA = xy;
+    launch_ew(c, N, CgInit0{b, GW, XA, n});
+    M.apply(GW, N, RU, nullptr);
+    launch_ewred<1>(c, N, CgInit1{st, RU, GW, PQ, n});
+    CPK_HIP(hipGetLastError());
+    pull();
+    if (h.err) raise_error();
+    if (print) {
+        printf("\n**** Constraint-preconditioned version of CG ****\n\n");
+        printf("stopTol = %e\n", h.stopTol);
+        printf("%5s  %9s  %9s  %9s  %9s\n", "iter", "resid", "pr-curv", "du-curv", "steplen");
+        printf("%5d  %9.2e  ", 0, h.residNorm);
+        printed = 1;
+    }
+    auto pr = [&]() {
+        if (h.nh <= printed) return;
+        auto v = fetch(hist, std::min(h.nh, h.hcap));
+        auto a = fetch(aux, 3 * std::min(h.nh, h.hcap));
+        for (int64_t i = printed; i < (int64_t)v.size(); i++) {
+            printf("%9.2e  %9.2e  %9.2e\n", a[3 * (i - 1)], a[3 * (i - 1) + 1], a[3 * (i - 1) + 2]);
+            printf("%5lld  %9.2e  ", (long long)i, v[i]);
+        }
+        printed = (int64_t)v.size();
+    };
+    auto body = [&]() {
+        launch_krylov_spmv(c, AC, st, APCQ, n, PolCgSpmv{PQ});
+        launch_ew(c, N, CgStep{st, XA, GW, PQ, APCQ});
+        M.apply(GW, N, RU, &st->running);
+        launch_ewred<2>(c, N, CgResid{st, XA, RU, GW, TT, n});
+        launch_ew(c, N, CgDir{st, RU, TT, PQ, n});
+    };
+    loop(body, pr);
+    if (h.err) raise_error();
+    if (print) printf("\n\n");
+    if (stats) stats->solved = h.residNorm <= h.stopTol;
+    finish_stats(stats);
+}
+
+// ---- cpgmres ----------------------------------------------------------------------------------
+void SolveCore::gmres(const double *b, double *xy, cpk_stats *stats) {
+    const int64_t R = (int64_t)restart;
+    if (R < 1) throw Error(CPK_ERR_ARGS, "restart must be >= 1");
+    // the cycles can overrun itmax by up to restart-1 iterations (cpgmres.m:148,203)
+    const int64_t hcap = (int64_t)(std::ceil(std::min(itmax, 1.0e8) / (double)R) * R) + 4;
+    setup_state(hcap, R);
+    DState *st = dst.p;
+    DBuf<double> Vb;
+    Vb.alloc((size_t)(R + 1) * N);
+    double *V = Vb.p;
+    double *UT = vec(0), *Wv = vec(1), *TMP = vec(2);
+    CPK_HIP(hipMemsetAsync(xy, 0, N * sizeof(double), c.stream));
+    const double outermax = std::ceil(itmax / (double)R);
+    int64_t outer = 0;
+    bool finished = false;
+    if (print) printf("\n**** Constraint-preconditioned version of GMRES(%lld) ****\n\n", (long long)R);
+    while (!finished && outer < outermax) {
+        outer++;
+        if (outer == 1) {
+            launch_set_concat(c, UT, b, n, m);  // u = b, t = 0
+            M.apply(UT, n, Wv, nullptr);        // M * [u; -t]
+        } else {
+            launch_spmv(c, AC, xy, TMP, nullptr);  // [A*x; C*y]
+            launch_ew(c, N, GmresRestartRhs{b, TMP, UT, n});
+            M.apply(UT, n, Wv, nullptr);
+        }
+        launch_ewred<2>(c, N, ArnoldiStart{st, Wv, UT, xy, V, n, outer > 1 ? 1 : 0, 0, outer == 1 ? 1 : 0});
+        launch_ew(c, N, NormalizeCopy{st, V, nullptr, 1, 0.0});
+        CPK_HIP(hipGetLastError());
+        pull();
+        if (h.err) raise_error();
+        if (print && outer == 1) {
+            printf("stopTol = %e\n", h.stopTol);
+            printf("%5s  %9s\n", "iter", "|resid|");
+            print_hist_lines("%5lld  %14.7e\n");
+        }
+        const int64_t base = (outer - 1) * R, hist0 = h.nh;
+        auto body = [&]() {
+            launch_krylov_spmv(c, AC, st, UT, n, PolArnoldiSpmv{V, N, 0});
+            M.apply(UT, n, Wv, &st->running);
+            hipLaunchKernelGGL(arnoldi_dots_kernel, dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, st, V, Wv, UT, n, N,
+                               (int64_t)0, R, RedBuf{c.partials.p, c.counter.p});
+            launch_ewred<2>(c, N, ArnoldiOrth{st, V, UT, n, N, 0, Window{}, nullptr});
+            launch_ew(c, N, GmresNormalize{st, V, N});
+        };
+        loop(body, [&]() {  // printed iteration = (outer - 1) * restart + k  (cpgmres.m:252)
+            if (h.nh <= printed) return;
+            auto v = fetch(hist, std::min(h.nh, h.hcap));
+            for (int64_t i = std::max(printed, hist0); i < (int64_t)v.size(); i++)
+                printf("%5lld  %14.7e\n", (long long)(base + (i - hist0) + 1), v[i]);
+            printed = (int64_t)v.size();
+        });
+        if (h.err) raise_error();
+        launch_scalar(c, GmresBackSolve{st});
+        launch_ew(c, N, GmresUpdateX{st, V, xy, n, N, 0});
+        CPK_HIP(hipGetLastError());
+        pull();
+        finished = h.residNorm <= h.stopTol;
+    }
+    if (stats) {
+        finish_stats(stats);
+        stats->niters = (outer - 1) * R + h.k;
+        stats->solved = h.residNorm <= h.stopTol;
+    }
+}
+
+// ---- cpdqgmres --------------------------------------------------------------------------------
+void SolveCore::dqgmres(const double *b, double *xy, cpk_stats *stats) {
+    const double memd = std::min(mem, itmax);  // cpdqgmres.m:125
+    mem = std::max(1.0, memd);
+    const int64_t Mm = (int64_t)mem, M1 = Mm + 1;
+    const int64_t hcap = (int64_t)std::min(itmax, 1.0e8) + 4;
+    setup_state(hcap, Mm);
+    DState *st = dst.p;
+    DBuf<double> Vb, PVb;
+    Vb.alloc((size_t)M1 * N);
+    PVb.alloc((size_t)M1 * N);
+    double *V = Vb.p, *PV = PVb.p;
+    double *UT = vec(0), *Wv = vec(1);
+    CPK_HIP(hipMemsetAsync(xy, 0, N * sizeof(double), c.stream));
+    if (print) printf("\n**** Constraint-preconditioned version of DQGMRES - mem = %lld ****\n\n", (long long)Mm);
+    launch_set_concat(c, UT, b, n, m);
+    M.apply(UT, N, Wv, nullptr);  // M * [u; t], t = 0 (cpdqgmres.m:425)
+    launch_ewred<2>(c, N, ArnoldiStart{st, Wv, UT, xy, V, n, 0, 1, 1});
+    launch_ew(c, N, NormalizeCopy{st, V, nullptr, 1, 0.0});
+    CPK_HIP(hipGetLastError());
+    pull();
+    if (h.err) {
+        char buf[160];
+        snprintf(buf, sizeof buf, "Undefined variable k (dot(u,V1) = %g < 0, cpdqgmres.m:158-160)", h.err_val);
+        throw Error(CPK_ERR_INDEFINITE, buf);
+    }
+    if (print) {
+        printf("stopTol = %e\n", h.stopTol);
+        printf("%5s  %9s\n", "iter", "|resid|");
+    }
+    auto body = [&]() {
+        launch_krylov_spmv(c, AC, st, UT, n, PolArnoldiSpmv{V, N, M1});
+        M.apply(UT, n, Wv, &st->running);
+        hipLaunchKernelGGL(arnoldi_dots_kernel, dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, st, V, Wv, UT, n, N, M1,
+                           Mm, RedBuf{c.partials.p, c.counter.p});
+        launch_ewred<2>(c, N, ArnoldiOrth{st, V, UT, n, N, M1, Window{}, nullptr});
+        launch_ew(c, N, DqgmresDirection{st, V, PV, xy, n, N});
+    };
+    if (print) print_hist_lines("%5lld  %14.7e\n");
+    loop(body, [&]() { print_hist_lines("%5lld  %14.7e\n"); });
+    if (h.err) raise_error();
+    if (stats) stats->solved = h.residNorm <= h.stopTol;
+    finish_stats(stats);
+}
+
+// ==============================================================================================
+void method_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, Precond &M, const cpk_opts *opts,
+                         double *d_xy, cpk_stats *stats) {
+    if (method < CPK_CG || method > CPK_DQGMRES) throw Error(CPK_ERR_ARGS, "unknown method");
+    CPK_HIP(hipEventRecord(c.ev0, c.stream));
+    SolveCore s(c, M, AC, method, opts);
+    switch (method) {
+    case CPK_MINRES: s.minres_like(0, d_b, d_xy, stats); break;
+    case CPK_CGLANCZOS: s.minres_like(1, d_b, d_xy, stats); break;
+    case CPK_SYMMLQ: s.minres_like(2, d_b, d_xy, stats); break;
+    case CPK_CG: s.cg(d_b, d_xy, stats); break;
+    case CPK_GMRES: s.gmres(d_b, d_xy, stats); break;
+    case CPK_DQGMRES: s.dqgmres(d_b, d_xy, stats); break;
+    }
+    CPK_HIP(hipEventRecord(c.ev1, c.stream));
+    CPK_HIP(hipEventSynchronize(c.ev1));
+    if (stats) {
+        float ms = 0;
+        CPK_HIP(hipEventElapsedTime(&ms, c.ev0, c.ev1));
+        stats->loop_ms = ms;
+        stats->bytes_moved = method_bytes(method, AC, M, stats->niters, opts);
+    }
+}
+
+void reg_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, const DMat &Kp, Precond &M,
+                      const cpk_opts *opts, double *d_x, cpk_stats *stats) {
+    const int64_t n = M.n, m = M.m, N = M.N;
+    auto t0 = std::chrono::steady_clock::now();
+    DBuf<int> flag;
+    flag.alloc(1);
+    DBuf<double> xy0, b1, dxy, t1, t2;
+    xy0.alloc(N), b1.alloc(std::max<int64_t>(n, 1)), dxy.alloc(N), t1.alloc(N), t2.alloc(N);
+    int shift = 0;
+    if (m > 0) {
+        c.ensure_partials((size_t)kEwGrid);
+        launch_ewred<1>(c, m, AnyNonzero{d_b, n, flag.p});
+        CPK_HIP(hipMemcpyAsync(&shift, flag.p, sizeof(int), hipMemcpyDeviceToHost, c.stream));
+        CPK_HIP(hipStreamSynchronize(c.stream));
+    }
+    const double *bb = d_b;
+    if (shift) {
+        // xy0 = M * [zeros(n,1); b(n+1:n+m)]   (reg_cpkrylov.m:156)
+        CPK_HIP(hipMemsetAsync(t1.p, 0, n * sizeof(double), c.stream));
+        CPK_HIP(hipMemcpyAsync(t1.p + n, d_b + n, m * sizeof(double), hipMemcpyDeviceToDevice, c.stream));
+        M.apply(t1.p, N, xy0.p, nullptr);
+        launch_spmv(c, AC, xy0.p, t1.p, nullptr);            // rows < n: A*xy0(1:n)
+        launch_spmv_colmask(c, Kp, n, xy0.p, t2.p, nullptr);  // rows < n: B'*xy0(n+1:N)
+        launch_ew(c, n, ShiftRhs{d_b, t1.p, t2.p, b1.p});
+        bb = b1.p;
+    }
+    method_solve_device(c, method, bb, AC, M, opts, shift ? dxy.p : d_x, stats);
+    if (shift) launch_ew(c, N, Recover{xy0.p, dxy.p, d_x});
+    CPK_HIP(hipStreamSynchronize(c.stream));
+    if (stats) stats->stime = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// Algorithmic HBM bytes of one method call: per iteration the Krylov SpMV,
+// the preconditioner apply and the streaming vector kernels, counted as ideal single touches.
+double method_bytes(int method, const DMat &AC, const Precond &M, int64_t iters, const cpk_opts *opts) {
+    const double N = (double)M.N;
+    const double spmv = 12.0 * AC.nnz + 4.0 * (N + 1) + 8.0 * N /*x*/ + 8.0 * N /*y*/;
+    const double mapply = M.apply_bytes();
+    double vec = 0;
+    switch (method) {
+    case CPK_MINRES: vec = 8 * N * (5 + 8); break;      // lanczos step (5 streams) + update (8 streams)
+    case CPK_CGLANCZOS: vec = 8 * N * (7 + 4); break;
+    case CPK_SYMMLQ: vec = 8 * N * (5 + 7); break;
+    case CPK_CG: vec = 8 * N * (6 + 5 + 4); break;
+    case CPK_GMRES:
+    case CPK_DQGMRES: {
+        double w = 50;
+        if (opts && method == CPK_GMRES && opts->has_restart) w = opts->restart;
+        if (opts && method == CPK_DQGMRES && opts->has_mem) w = opts->mem;
+        vec = 8 * N * (3 + w / 2 + w / 2 + 3);
+        break;
+    }
+    }
+    return (double)iters * (spmv + mapply + vec);
+}
+
+}  // namespace cpk

@@ -1,0 +1,13 @@
+// solvers.hpp -- host entry points of the device solvers (solvers.hip).
+#pragma once
+#include "dev.hpp"
+
+namespace cpk {
+// [x, y, stats, flag] = method(b, A, C, M, opts): d_b (n), d_xy (N), AC = blkdiag(A, C)
+void method_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, Precond &M, const cpk_opts *opts,
+                         double *d_xy, cpk_stats *stats);
+// reg_cpkrylov's shift + method + recovery (reg_cpkrylov.m:150-175): d_b (N), d_x (N)
+void reg_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, const DMat &Kp, Precond &M,
+                      const cpk_opts *opts, double *d_x, cpk_stats *stats);
+double method_bytes(int method, const DMat &AC, const Precond &M, int64_t iters, const cpk_opts *opts);
+}  // namespace cpk

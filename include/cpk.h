@@ -1,0 +1,178 @@
+/*
+ * cpk.h -- C ABI of libcpk, the MI355X-native constraint-preconditioned Krylov engine.
+ *
+ * Drop-in boundary for optimizers/cpkrylov (MATLAB).  Each entry point names the reference
+ * interface it replaces; INTEGRATION.md shows the MEX gateway / opSpot subclass / ctypes
+ * binding a maintainer adds on the reference side.
+ *
+ * Conventions
+ *   - Every function returns an int status (cpk_status).  On failure cpk_last_error()
+ *     returns a message (thread-local, valid until the next call on that thread).
+ *     No C++ exception crosses this boundary.
+ *   - Input arrays are borrowed read-only for the duration of the call; the library
+ *     copies what it keeps (to host memory and HBM).  Output arrays are caller-allocated.
+ *   - Handles are owned by the library and freed by the matching *_destroy.
+ *   - One host thread per context; a handle is not re-entrant.
+ *   - All arithmetic is IEEE fp64.  Vectors are laid out [x-part (n); y-part (m)], as the
+ *     reference's [x1; x2] (reg_cpkrylov.m:166-173).
+ */
+#ifndef CPK_H
+#define CPK_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CPK_ABI_VERSION 1
+
+typedef enum {
+    CPK_OK = 0,
+    CPK_ERR_INDEFINITE = 1, /* beta < -100*eps, or a negative squared norm (cpminres.m:195-199 etc.) */
+    CPK_ERR_DIM = 2,        /* dimension mismatch (opLDL2.m:61-75) */
+    CPK_ERR_ARGS = 3,       /* bad argument (reg_cpkrylov.m:122-125 "not enough inputs") */
+    CPK_ERR_HIP = 4,        /* HIP runtime failure */
+    CPK_ERR_RCCL = 5,       /* RCCL failure */
+    CPK_ERR_FACTOR = 6,     /* zero pivot in the static-pivot LDL' (ldl at opLDL2.m:82) */
+    CPK_ERR_NOMEM = 7,
+    CPK_ERR_UNSUPPORTED = 8
+} cpk_status;
+
+/* Method ids: the function handles @cpcg, @cpcglanczos, @cpminres, @cpsymmlq, @cpgmres,
+ * @cpdqgmres passed to reg_cpkrylov (reg_cpkrylov.m:67-68, :163). */
+typedef enum {
+    CPK_CG = 0,
+    CPK_CGLANCZOS = 1,
+    CPK_MINRES = 2,
+    CPK_SYMMLQ = 3,
+    CPK_GMRES = 4,
+    CPK_DQGMRES = 5
+} cpk_method;
+
+/* The MATLAB `opts` struct.  A field takes effect only when its has_* flag is set
+ * (MATLAB isfield(), e.g. cpminres.m:98-111); otherwise each solver's own default applies.
+ * nitref/itref_tol/force_itref/residual_update are the fields reg_cpkrylov copies into M
+ * (reg_cpkrylov.m:135-148), with opLDL2's setter semantics (opLDL2.m:97-115). */
+typedef struct {
+    double atol, rtol, btol;
+    double itmax, restart, mem;
+    double print;
+    double nitref, itref_tol, force_itref, residual_update;
+    int has_atol, has_rtol, has_btol, has_itmax, has_restart, has_mem, has_print;
+    int has_nitref, has_itref_tol, has_force_itref, has_residual_update;
+} cpk_opts;
+
+/* stats / flag outputs (cpminres.m:250-252, cpsymmlq.m:363-367, cpcglanczos.m:681-694,
+ * reg_cpkrylov.m:177-178).  History buffers are caller-allocated with capacity hist_cap
+ * (itmax + 2 suffices for every method); a NULL buffer is skipped. */
+typedef struct {
+    int64_t niters;
+    int solved;          /* flag.solved */
+    int status;          /* cpcglanczos stats.status: 0 max iters, 1 residual small, 2 backward error small */
+    double *hist;        /* residHistory (cpsymmlq: cgresidHistory) */
+    double *hist_lq;     /* cpsymmlq lqresidHistory */
+    double *hist_qr;     /* cpsymmlq qrresidHistory */
+    int64_t hist_cap;
+    int64_t hist_len, lq_len, qr_len;
+    double ptime;        /* s, preconditioner setup (reg_cpkrylov.m:128-132) */
+    double stime;        /* s, shift + method + recovery (reg_cpkrylov.m:150-175) */
+    double loop_ms;      /* device time of the method call (HIP events on the solver stream) */
+    double bytes_moved;  /* algorithmic HBM bytes of the method call (DESIGN.md section 5 model) */
+} cpk_stats;
+
+/* Factor summary of a preconditioner. */
+typedef struct {
+    int64_t n, m, N;
+    int64_t nnz_kp;      /* nnz(Kp) */
+    int64_t nnz_l;       /* nnz of the strict lower factor */
+    int64_t nblocks;     /* SpTRSV work blocks */
+    int64_t nrounds;     /* kernel launches per triangular sweep */
+    int64_t max_block_levels;
+    int64_t depth;       /* elimination-tree height */
+    int64_t ordering;    /* 0 natural, 1 G-first + nested dissection, 2 G-first + minimum degree,
+                            3 nested dissection, 4 minimum degree */
+} cpk_pc_info;
+
+typedef struct cpk_ctx_s *cpk_ctx;
+typedef struct cpk_mat_s *cpk_mat;
+typedef struct cpk_pc_s *cpk_pc;
+
+const char *cpk_last_error(void);
+int cpk_abi_version(void);
+
+/* ---- context: device, streams, RCCL communicator ------------------------------------- */
+/* Fill `id` (128 bytes) with an RCCL unique id on rank 0; broadcast it to the other ranks. */
+int cpk_get_unique_id(unsigned char id[128]);
+/* device < 0: use the current device.  nranks == 1: no communicator (unique_id may be NULL). */
+int cpk_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id, cpk_ctx *out);
+int cpk_ctx_destroy(cpk_ctx ctx);
+int cpk_ctx_synchronize(cpk_ctx ctx);
+
+/* ---- sparse matrices (MATLAB sparse arrays A, B, C, G; reg_cpkrylov.m:1) -------------- */
+/* MATLAB-native CSC: jc[ncols+1], ir[nnz] (0-based, mwIndex = size_t), pr[nnz].
+ * ctx may be NULL for a host-only matrix (cpk_analyze); such a matrix cannot be used on a device. */
+int cpk_mat_create_csc(cpk_ctx ctx, int64_t nrows, int64_t ncols, const size_t *jc, const size_t *ir,
+                       const double *pr, cpk_mat *out);
+/* CSR with 64-bit row pointers and 32-bit column indices. */
+int cpk_mat_create_csr(cpk_ctx ctx, int64_t nrows, int64_t ncols, const int64_t *rowptr,
+                       const int32_t *colind, const double *val, cpk_mat *out);
+int cpk_mat_destroy(cpk_mat A);
+/* y = A*x on the device (host vectors in/out); replaces MATLAB sparse mtimes A*v. */
+int cpk_mat_spmv(cpk_mat A, const double *x, double *y);
+
+/* ---- preconditioner: M = opLDL2(A, B, C), Kp = [A B'; B C] (ops/opLDL2.m:60-92) ------ */
+int cpk_pc_create(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptime, cpk_pc *out);
+int cpk_pc_destroy(cpk_pc M);
+/* M.nitref = ...; M.itref_tol = ...; etc. (opLDL2.m:45-50, 97-115), has_* fields select. */
+int cpk_pc_set(cpk_pc M, const cpk_opts *opts);
+int cpk_pc_get(cpk_pc M, double *nitref, double *itref_tol, double *force_itref, double *residual_update);
+/* y = M*x (opLDL2.multiply, opLDL2.m:161-188).  Host vectors of length N. */
+int cpk_pc_apply(cpk_pc M, const double *x, double *y);
+/* Same on device pointers, enqueued on the context stream. */
+int cpk_pc_apply_device(cpk_pc M, const double *d_x, double *d_y);
+/* x = Kp*b (opLDL2.divide, opLDL2.m:193-195). */
+int cpk_pc_divide(cpk_pc M, const double *b, double *x);
+int cpk_pc_get_info(cpk_pc M, cpk_pc_info *info);
+/* Export the factors P'*Kp*P = L*D*L': strict-lower L in CSC (Lcolptr[N+1], Lrowind[nnz_l],
+ * Lval[nnz_l]), D[N], perm[N] (perm[k] = original index of pivot k).  Any pointer may be NULL. */
+int cpk_pc_export(cpk_pc M, int64_t *Lcolptr, int32_t *Lrowind, double *Lval, double *D, int32_t *perm);
+
+/* ---- host-only analysis (no GPU needed) ------------------------------------------------- */
+/* The host half of cpk_pc_create: Kp assembly, fill-reducing ordering, static-pivot LDL' and
+ * the triangular-sweep schedule.  Matrices for this call may be created with ctx == NULL. */
+typedef struct cpk_analysis_s *cpk_analysis;
+int cpk_analyze(cpk_mat A11, cpk_mat B, cpk_mat C22, cpk_analysis *out);
+int cpk_analysis_destroy(cpk_analysis an);
+int cpk_analysis_get_info(cpk_analysis an, cpk_pc_info *info);
+int cpk_analysis_export(cpk_analysis an, int64_t *Lcolptr, int32_t *Lrowind, double *Lval, double *D,
+                        int32_t *perm);
+/* Sweep schedule: round_ptr[nrounds+1] (blocks per round), blk_lvl[nblocks+1] (levels per
+ * block, indices into lvl_row), lvl_row[nlevels+1] (first row of each level; last = N). */
+int cpk_analysis_schedule(cpk_analysis an, int64_t *nlevels, int64_t *round_ptr, int64_t *blk_lvl,
+                          int64_t *lvl_row);
+
+/* ---- solvers --------------------------------------------------------------------------- */
+/* [x, y, stats, flag] = method(b, A, C, M, opts)   (kernels/cp*.m, e.g. cpminres.m:1).
+ * b: n, x: n, y: m (host). */
+int cpk_method_solve(cpk_ctx ctx, int method, const double *b, cpk_mat A, cpk_mat C, cpk_pc M,
+                     const cpk_opts *opts, double *x, double *y, cpk_stats *stats);
+/* Same with device-resident b (n) and xy (N = [x; y]); nothing crosses PCIe except the
+ * stop flag polled between iteration batches and the history copied back at the end. */
+int cpk_method_solve_device(cpk_ctx ctx, int method, const double *d_b, cpk_mat A, cpk_mat C, cpk_pc M,
+                            const cpk_opts *opts, double *d_xy, cpk_stats *stats);
+/* [x, stats, flag] = reg_cpkrylov(method, b, A, B, C, G, opts)  (reg_cpkrylov.m:1-180).
+ * b: N, x: N (host).  If M_out != NULL the preconditioner built here is returned. */
+int cpk_reg_solve(cpk_ctx ctx, int method, const double *b, cpk_mat A, cpk_mat B, cpk_mat C, cpk_mat G,
+                  const cpk_opts *opts, double *x, cpk_stats *stats, cpk_pc *M_out);
+/* reg_cpkrylov's shift + method + recovery with an existing M, device-resident b and x (N). */
+int cpk_reg_solve_device(cpk_ctx ctx, int method, const double *d_b, cpk_mat A, cpk_mat B, cpk_mat C,
+                         cpk_pc M, const cpk_opts *opts, double *d_x, cpk_stats *stats);
+
+/* [c, s, d] = SymGivens(a, b)  (util/SymGivens.m:1-29) */
+int cpk_symgivens(double a, double b, double *c, double *s, double *d);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

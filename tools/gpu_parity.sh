@@ -1,0 +1,5 @@
+set -e
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+python -c "import torch; print(torch.cuda.is_available(), torch.cuda.get_device_name(0))" > gpurun_out/dev.txt 2>&1 || true
+timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -x -q -m gpu > gpurun_out/parity1.log 2>&1
