@@ -102,16 +102,50 @@ Schedule build_schedule(const Factor &f, int64_t R) {
         if (f.parent[v] >= 0) height[f.parent[v]] = std::max(height[f.parent[v]], height[v] + 1);
         s.depth = std::max<int64_t>(s.depth, height[v] + 1);
     }
-    // bottom-up greedy subtree clustering (children always precede parents)
+    std::vector<int32_t> closed_round(N, -1);  // >= 0 iff v roots a cluster
+    // (1) Layer peeling: round r takes the maximal subtrees of at most R rows of the tree that
+    //     remains after rounds 0..r-1.  On bushy (nested-dissection) trees the remainder
+    //     shrinks geometrically and a few rounds suffice.
+    std::vector<int32_t> alive(N);
+    std::iota(alive.begin(), alive.end(), 0);
+    std::vector<char> is_alive(N, 1);
+    std::vector<int64_t> sz(N, 0);
+    std::vector<int32_t> root_of(N, -1);
+    int32_t round = 0;
+    while (!alive.empty()) {
+        for (int32_t v : alive) sz[v] = 0;
+        for (int32_t v : alive) {  // ascending: children before parents
+            sz[v] += 1;
+            if (f.parent[v] >= 0 && is_alive[f.parent[v]]) sz[f.parent[v]] += sz[v];
+        }
+        const size_t before = alive.size();
+        for (size_t q = alive.size(); q-- > 0;) {  // descending: parents before children
+            const int32_t v = alive[q], p = f.parent[v];
+            if (sz[v] > R) root_of[v] = -1;
+            else if (p < 0 || sz[p] > R) root_of[v] = v, closed_round[v] = round;
+            else root_of[v] = root_of[p];
+        }
+        std::vector<int32_t> rest;
+        rest.reserve(alive.size());
+        for (int32_t v : alive) {
+            if (root_of[v] >= 0) is_alive[v] = 0;
+            else rest.push_back(v);
+        }
+        alive.swap(rest);
+        round++;
+        if (!alive.empty() && round >= 8 && alive.size() * 2 > before) break;  // chain-like tree
+    }
+    // (2) Greedy bottom-up clustering of what peeling left (chain-like upper trees): a node's
+    //     open cluster absorbs its children's open clusters, closing the largest ones until it
+    //     fits in R rows.  Peeled children are already-closed clusters.
     std::vector<int64_t> open_size(N, 0);
     std::vector<int32_t> open_dep(N, -1);
-    std::vector<int32_t> closed_round(N, -1);  // >= 0 iff v roots a closed cluster
     std::vector<int32_t> tmp;
-    for (int64_t v = 0; v < N; v++) {
+    for (int32_t v : alive) {
         int64_t total = 1;
-        int32_t dep = -1;
-        tmp.assign(kids.begin() + cptr[v], kids.begin() + cptr[v + 1]);
-        for (int32_t c : tmp) total += open_size[c];
+        tmp.clear();
+        for (int64_t q = cptr[v]; q < cptr[v + 1]; q++)
+            if (closed_round[kids[q]] < 0) tmp.push_back(kids[q]), total += open_size[kids[q]];
         if (total > R) {
             std::sort(tmp.begin(), tmp.end(), [&](int32_t a, int32_t b) {
                 return open_size[a] != open_size[b] ? open_size[a] > open_size[b] : a < b;
@@ -120,18 +154,18 @@ Schedule build_schedule(const Factor &f, int64_t R) {
                 if (total <= R) break;
                 closed_round[c] = open_dep[c] + 1;
                 total -= open_size[c];
-                open_size[c] = 0;
             }
         }
+        int32_t dep = -1;
         for (int64_t q = cptr[v]; q < cptr[v + 1]; q++) {
-            int32_t c = kids[q];
+            const int32_t c = kids[q];
             dep = std::max(dep, closed_round[c] >= 0 ? closed_round[c] : open_dep[c]);
         }
         open_size[v] = total;
         open_dep[v] = dep;
         if (f.parent[v] < 0) closed_round[v] = dep + 1;
     }
-    // cluster membership (top-down)
+    // cluster membership (top-down): a non-root joins its parent's cluster
     std::vector<int32_t> cl(N);
     for (int64_t v = N - 1; v >= 0; v--) cl[v] = closed_round[v] >= 0 ? (int32_t)v : cl[f.parent[v]];
     std::vector<int64_t> csize(N, 0);
@@ -139,12 +173,11 @@ Schedule build_schedule(const Factor &f, int64_t R) {
     int32_t nrounds = 0;
     for (int64_t v = 0; v < N; v++)
         if (closed_round[v] >= 0) nrounds = std::max(nrounds, closed_round[v] + 1);
-    // pack clusters of one round into blocks of <= R rows (clusters taken in root order)
+    // pack the clusters of one round into blocks of <= R rows (clusters taken in root order)
     std::vector<std::vector<int32_t>> roots_by_round(nrounds);
     for (int64_t v = 0; v < N; v++)
         if (closed_round[v] >= 0) roots_by_round[closed_round[v]].push_back((int32_t)v);
     std::vector<int32_t> cluster_block(N, -1);
-    std::vector<int64_t> block_round;
     int32_t nb = 0;
     s.round_ptr.assign(1, 0);
     for (int32_t r = 0; r < nrounds; r++) {
@@ -165,7 +198,7 @@ Schedule build_schedule(const Factor &f, int64_t R) {
     std::vector<int32_t> level(N, 0);
     for (int64_t j = 0; j < N; j++)
         for (int64_t p = f.Lp[j]; p < f.Lp[j + 1]; p++) {
-            int32_t i = f.Li[p];
+            const int32_t i = f.Li[p];
             if (block[i] == block[j]) level[i] = std::max(level[i], level[j] + 1);
         }
     // new order: blocks ascending (= rounds ascending), then level, then old index
@@ -185,7 +218,7 @@ Schedule build_schedule(const Factor &f, int64_t R) {
         std::stable_sort(first, last, [&](int32_t a, int32_t c) { return level[a] < level[c]; });
         int32_t prev = -1;
         for (int64_t q = s.blk_row[b]; q < s.blk_row[b + 1]; q++) {
-            int32_t l = level[s.order[q]];
+            const int32_t l = level[s.order[q]];
             if (l != prev) s.lvl_row.push_back(q), prev = l;
         }
         s.blk_lvl.push_back((int64_t)s.lvl_row.size());

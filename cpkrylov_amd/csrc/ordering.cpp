@@ -125,18 +125,24 @@ struct Nd {
                 emit(nodes);
                 return;
             }
-            // split into connected components first
+            // split into connected components first (one linear pass over the subset)
             bfs(nodes[0], lab, order);
             if (order.size() < nodes.size()) {
-                int32_t la = next_label++, lb = next_label++;
-                std::vector<int32_t> a = order, b;
-                for (int32_t v : a) label[v] = la;
-                for (int32_t v : nodes)
-                    if (label[v] == lab) label[v] = lb, b.push_back(v);
-                run(std::move(a), la);
-                nodes.swap(b);
-                lab = lb;
-                continue;
+                std::vector<std::pair<int32_t, std::vector<int32_t>>> comps;
+                const int32_t stamp0 = cur_stamp;  // every BFS below gets a newer stamp
+                for (int32_t v : nodes) {
+                    if (label[v] != lab || stamp[v] > stamp0) continue;  // relabelled or seen
+                    if (stamp[v] == stamp0) {  // the component found by the first BFS
+                        comps.emplace_back(next_label++, order);
+                    } else {
+                        std::vector<int32_t> c;
+                        bfs(v, lab, c);
+                        comps.emplace_back(next_label++, std::move(c));
+                    }
+                    for (int32_t w : comps.back().second) label[w] = comps.back().first;
+                }
+                for (auto &c : comps) run(std::move(c.second), c.first);
+                return;
             }
             // pseudo-peripheral node
             int32_t start = order.back();

@@ -1,0 +1,111 @@
+"""Host half of the preconditioner (no GPU): ordering, static-pivot LDL', sweep schedule.
+
+The device sweeps are replayed here in numpy following the schedule exactly (rounds, blocks,
+intra-block levels, MATLAB's accumulation order); the replay must (a) never read an
+unfinished value and (b) equal the oracle's column-oriented solve with the same factors bit
+for bit -- the contract the HIP kernels implement."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import cpkrylov_amd as cpk
+import fixtures as F
+from cpkrylov_amd.synthetic import saddle_system
+from oracle import oracle as O
+
+
+def _systems():
+    out = []
+    for name in ("cvxqp1_m", "cvxqp2_s"):
+        P = F.load(name)
+        out.append((name, P["G"], P["B"], -P["C"]))
+    S = saddle_system(N=20000)
+    out.append(("synthetic20k", S["G"], S["B"], -S["C"]))
+    return out
+
+
+SYSTEMS = _systems()
+
+
+def replay(an, x):
+    L, D, perm = an["L"], an["D"], an["perm"]
+    rp, bl, lr = an["round_ptr"], an["blk_lvl"], an["lvl_row"]
+    N = len(D)
+    Lr = L.tocsr()
+    Lr.sort_indices()
+    Lc = L.tocsc()
+    Lc.sort_indices()
+    w = np.full(N, np.nan)
+    for r in range(len(rp) - 1):
+        for b in range(rp[r], rp[r + 1]):
+            for lv in range(bl[b], bl[b + 1]):
+                for k in range(lr[lv], lr[lv + 1]):
+                    acc = x[perm[k]]
+                    for e in range(Lr.indptr[k], Lr.indptr[k + 1]):
+                        assert not np.isnan(w[Lr.indices[e]]), "forward dependency not ready"
+                        acc -= Lr.data[e] * w[Lr.indices[e]]
+                    w[k] = acc
+    done = np.zeros(N, bool)
+    y = np.zeros(N)
+    for r in range(len(rp) - 2, -1, -1):
+        for b in range(rp[r], rp[r + 1]):
+            for lv in range(bl[b + 1] - 1, bl[b] - 1, -1):
+                for k in range(lr[lv], lr[lv + 1]):
+                    acc = w[k] / D[k]
+                    for e in range(Lc.indptr[k + 1] - 1, Lc.indptr[k] - 1, -1):
+                        assert done[Lc.indices[e]], "backward dependency not ready"
+                        acc -= Lc.data[e] * w[Lc.indices[e]]
+                    w[k] = acc
+                    done[k] = True
+                    y[perm[k]] = acc
+    return y
+
+
+@pytest.mark.parametrize("name,G,B,C22", SYSTEMS, ids=[s[0] for s in SYSTEMS])
+def test_factor_and_schedule(name, G, B, C22):
+    an = cpk.analyze(G, B, C22)
+    N = an["info"]["N"]
+    perm = an["perm"]
+    assert np.array_equal(np.sort(perm), np.arange(N))  # P is a permutation (P*P' = I)
+    Kp = sp.bmat([[G, B.T], [B, C22]]).tocsr()
+    L1 = an["L"] + sp.eye(N)
+    R = Kp[perm][:, perm] - L1 @ sp.diags(an["D"]) @ L1.T
+    scale = abs(L1) @ sp.diags(np.abs(an["D"])) @ abs(L1).T  # componentwise backward error
+    assert abs(R).max() <= 1e-14 * max(abs(scale).max(), abs(Kp).max())
+    # schedule covers every row once, rounds/blocks/levels consistent
+    assert an["lvl_row"][0] == 0 and an["lvl_row"][-1] == N
+    assert np.all(np.diff(an["lvl_row"]) > 0)
+    assert an["blk_lvl"][-1] == len(an["lvl_row"]) - 1
+    x = np.random.default_rng(5).standard_normal(N)
+    y = replay(an, x)
+    Mo = O.LDL2(G, B, C22, factors=(an["L"], an["D"], perm))
+    Mo.set(nitref=0)
+    assert np.array_equal(y, Mo @ x)
+    assert np.linalg.norm(Kp @ y - x) <= 1e-6 * np.linalg.norm(x)
+
+
+def test_synthetic_s10_shape_of_schedule():
+    """At 200k dofs the nested-dissection schedule needs only a few launches per sweep."""
+    S = saddle_system(N=200000)
+    an = cpk.analyze(S["G"], S["B"], -S["C"])
+    assert an["info"]["ordering"] == 1  # G-first + nested dissection
+    assert an["info"]["nrounds"] <= 4
+    assert an["info"]["nnz_l"] <= an["info"]["nnz_kp"]
+
+
+def test_dimension_errors():
+    P = F.load("cvxqp2_s")
+    with pytest.raises(cpk.CpkError) as e:
+        cpk.analyze(P["G"], P["B"][:, :10], -P["C"])
+    assert "Incompatible dimensions" in str(e.value)
+    with pytest.raises(cpk.CpkError) as e:
+        cpk.analyze(P["G"][:, :10], P["B"], -P["C"])
+    assert "must be square" in str(e.value)
+
+
+def test_zero_pivot_reported():
+    P = F.load("cvxqp2_s")
+    G0 = sp.csr_matrix(P["G"].shape)
+    with pytest.raises(cpk.CpkError) as e:
+        cpk.analyze(G0, P["B"], -P["C"])
+    assert e.value.code == 6

@@ -1,0 +1,130 @@
+"""CPU oracle (test infrastructure) pinned against the reference's own checks.
+
+The reference has no tests and records no outputs.  What pins the
+oracle: (1) the examples' known-answer check against the direct solve K\\rhs
+(cpk_exprog1.m:101-104, cpk_exprog2.m:100-103); (2) algebraic invariants of each method;
+(3) the committed golden vectors (regression: bit-exact reproduction)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import fixtures as F
+from golden.make_golden import CASES, case_file, run
+from oracle import oracle as O
+
+
+@pytest.mark.parametrize("name,method,extra", CASES)
+def test_oracle_reproduces_golden(name, method, extra):
+    x, st = run(name, method, extra)
+    g = np.load(case_file(name, method, extra), allow_pickle=False)
+    assert st["niters"] == int(g["niters"]) and st["solved"] == bool(g["solved"])
+    for k in st:
+        if k.endswith("History"):
+            assert np.array_equal(st[k], g[k]), k
+    assert np.array_equal(x, g["x"])
+
+
+@pytest.mark.parametrize("name,method,extra", CASES)
+def test_oracle_known_answer(name, method, extra):
+    """The examples' own check: the solution agrees with K\\rhs to the accuracy the stopping
+    test implies (measured: 4.5e-7 / 7.0e-7 on cvxqp1_m, 6.6e-5 - 8.6e-5 on cvxqp2_s)."""
+    P = F.load(name)
+    g = np.load(case_file(name, method, extra), allow_pickle=False)
+    err = np.linalg.norm(g["x"] - P["x_direct"]) / np.linalg.norm(P["x_direct"])
+    if bool(g["solved"]):
+        assert err < (1e-6 if name == "cvxqp1_m" else 1e-4), err
+        h = g["residHistory"] if "residHistory" in g else g["cgresidHistory"]
+        assert h[-1] <= 1e-6 + 1e-6 * h[0]
+    else:
+        assert int(g["niters"]) == 500  # itmax attained (cpdqgmres with mem = 20 stalls)
+
+
+def test_minres_invariants():
+    P = F.load("cvxqp1_m")
+    g = np.load(case_file("cvxqp1_m", "minres", {}), allow_pickle=False)
+    h = g["residHistory"]
+    assert len(h) == int(g["niters"]) + 1
+    assert np.all(np.diff(h) <= 1e-12 * h[0])  # MINRES residual norms never increase
+    # residHistory(1)^2 = <b1, M*[b1; 0]>_1 with b1 the shifted rhs (cpminres.m:131-141)
+    n, m = P["n"], P["m"]
+    M = O.LDL2(P["G"], P["B"], -P["C"], order="rcm")
+    M.set(nitref=1, force_itref=1)
+    b = P["rhs"]
+    xy0 = M @ np.concatenate([np.zeros(n), b[n:]])
+    b1 = b[:n] - P["Q"] @ xy0[:n] - P["B"].T @ xy0[n:]
+    v = M @ np.concatenate([b1, np.zeros(m)])
+    assert abs(np.sqrt(b1 @ v[:n]) - h[0]) <= 1e-12 * h[0]
+
+
+def test_gmres_niters_formula():
+    # niters = (outer - 1) * restart + k   (cpgmres.m:267)
+    g = np.load(case_file("cvxqp2_s", "gmres", {"restart": 20}), allow_pickle=False)
+    assert len(g["residHistory"]) == int(g["niters"]) + 1
+    assert int(g["niters"]) == 380
+
+
+def test_symmlq_history_alignment():
+    g = np.load(case_file("cvxqp1_m", "symmlq", {}), allow_pickle=False)
+    k = int(g["niters"])
+    # cgresidHistory = [beta1; ...] (cpsymmlq.m:331): k+1 entries; lq/qr: k+1 entries (:326-327)
+    assert len(g["cgresidHistory"]) == k + 1
+    assert len(g["lqresidHistory"]) == k + 1 and len(g["qrresidHistory"]) == k + 1
+    assert g["cgresidHistory"][0] == g["qrresidHistory"][0]
+
+
+SYMGIVENS_TABLE = [  # (a, b) -> (c, s, d) following util/SymGivens.m branch by branch
+    (0.0, 0.0, (1.0, 0.0, 0.0)),
+    (3.0, 0.0, (1.0, 0.0, 3.0)),
+    (-3.0, 0.0, (-1.0, 0.0, 3.0)),
+    (0.0, 2.0, (0.0, 1.0, 2.0)),
+    (0.0, -2.0, (0.0, -1.0, 2.0)),
+    (3.0, 4.0, (0.6, 0.8, 5.0)),     # |b| > |a|
+    (4.0, 3.0, (0.8, 0.6, 5.0)),     # |b| <= |a|
+    (-4.0, 3.0, (-0.8, 0.6, 5.0)),     # d = a / c
+    (1.0, 1.0, (1 / np.sqrt(2), 1 / np.sqrt(2), np.sqrt(2))),
+]
+
+
+@pytest.mark.parametrize("a,b,exp", SYMGIVENS_TABLE)
+def test_symgivens_branches(a, b, exp):
+    c, s, d = O.symgivens(a, b)
+    assert np.allclose((c, s, d), exp, rtol=1e-15, atol=0)
+
+
+def test_opldl2_setters():
+    P = F.load("cvxqp2_s")
+    M = O.LDL2(P["G"], P["B"], -P["C"])
+    assert M.props() == dict(nitref=3, itref_tol=1e-8, force_itref=0, residual_update=0)
+    M.set(nitref=2.5)
+    assert M.props()["nitref"] == 3  # MATLAB round half away from zero
+    M.set(nitref=-4)
+    assert M.props()["nitref"] == 0
+    M.set(force_itref=2)
+    assert M.props()["force_itref"] == 0  # neither false nor true -> false
+    M.set(force_itref=1)
+    assert M.props()["force_itref"] == 1
+    M.set(itref_tol=-1)
+    assert M.props()["itref_tol"] == -1  # the `sef.itref_tol` typo: no clamping
+
+
+def test_residual_update_is_noop():
+    """Spot operators are value objects: op.Aty / op.Cy written inside multiply are lost, so
+    residual_update changes nothing."""
+    P = F.load("cvxqp1_m")
+    M = O.LDL2(P["G"], P["B"], -P["C"], order="rcm")
+    z = np.random.default_rng(0).standard_normal(P["n"] + P["m"])
+    M.set(nitref=1, force_itref=1)
+    y0 = M @ z
+    M.set(residual_update=1)
+    assert np.array_equal(M @ z, y0)
+    assert np.array_equal(M @ z, y0)  # and stays so on the next call
+
+
+def test_indefinite_error():
+    """beta < -100*eps raises (cpminres.m:136-139): use a G that is not positive on the
+    nullspace of B."""
+    P = F.load("cvxqp2_s")
+    Gneg = -P["G"]
+    with pytest.raises(O.OracleError) as e:
+        O.reg_cpkrylov("minres", P["rhs"], P["Q"], P["B"], P["C"], Gneg, dict(F.EXPROG_OPTS), order="rcm")
+    assert "does not behave as a spd matrix" in str(e.value)
