@@ -1,0 +1,200 @@
+#!/usr/bin/env python
+"""Krylov iters/sec of CP-MINRES on the synthetic 10M-dof saddle-point system (S10).
+
+Metric (BASELINE.json): "Krylov iters/sec + SpMV GB/s (% HBM peak), cpminres 10M-dof".
+  step      one converging cpminres solve (the method call, kernels/cpminres.m) with the
+            example options (cpk_exprog1.m:79-90: atol = rtol = 1e-6, itmax = 500, nitref = 1,
+            force_itref, residual_update); b1 (the shifted rhs, reg_cpkrylov.m:152-160) and the
+            solution are HBM-resident, the factorization (ptime) and the shift are outside the
+            timed region.
+  value     Krylov iterations completed by all ranks / max over ranks of the timed wall time.
+  roofline  the saddle-point SpMV r = x - Kp*y (the refinement residual inside every M*z):
+            algorithmic bytes per launch / its HIP-event-timed average duration, vs 8 TB/s.
+  cpu_baseline  the C restatement (oracle/) of the same solve on one host core, timed on a
+            bounded sample of the same workload.
+Multi-GPU (torchrun, one process per GPU): each rank runs an independent replica of the solve
+(replicas only this round) and the line reports the aggregate.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
+EXPROG_OPTS = dict(print=False, atol=1.0e-6, rtol=1.0e-6, itmax=500,
+                   residual_update=True, nitref=1, force_itref=True, itref_tol=1.0e-8)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--size", type=int, default=10_000_000, help="total dofs N (S10: 10,000,000)")
+    ap.add_argument("--method", default="minres")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-reps", type=int, default=20)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import torch
+
+    import cpkrylov_amd as cpk
+    from cpkrylov_amd import _lib
+    from cpkrylov_amd.synthetic import saddle_system
+
+    t_setup = time.perf_counter()
+    S = saddle_system(N=args.size)
+    n, m, N = S["n"], S["m"], S["N"]
+    ctx = cpk.Context(device=local)
+    A, B, Cm, G = (cpk.Matrix(S[k], ctx) for k in ("Q", "B", "C", "G"))
+    M = cpk.opLDL2(G, B, -S["C"], ctx=ctx)
+    M.nitref, M.itref_tol = EXPROG_OPTS["nitref"], EXPROG_OPTS["itref_tol"]
+    M.residual_update, M.force_itref = EXPROG_OPTS["residual_update"], EXPROG_OPTS["force_itref"]
+    dev = torch.device("cuda", local)
+    b = torch.from_numpy(S["rhs"]).to(dev)
+    b1 = torch.empty(n, dtype=torch.float64, device=dev)
+    xy0 = torch.empty(N, dtype=torch.float64, device=dev)
+    xy = torch.empty(N, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize(dev)
+    shifted = C.c_int()
+    _lib.check(_lib.lib.cpk_reg_shift_device(ctx.h, C.c_void_p(b.data_ptr()), A.h, B.h, Cm.h, M.h,
+                                             C.c_void_p(b1.data_ptr()), C.c_void_p(xy0.data_ptr()), C.byref(shifted)))
+    opts = _lib.make_opts(EXPROG_OPTS)
+    mid = _lib.METHODS[args.method]
+    cap = int(EXPROG_OPTS["itmax"]) + 4
+    hist = np.zeros(cap)
+    st = _lib.Stats()
+    st.hist = hist.ctypes.data_as(C.POINTER(C.c_double))
+    st.hist_cap = cap
+
+    def step():
+        _lib.check(_lib.lib.cpk_method_solve_device(ctx.h, mid, C.c_void_p(b1.data_ptr()), A.h, Cm.h, M.h,
+                                                    C.byref(opts), C.c_void_p(xy.data_ptr()), C.byref(st)))
+        return int(st.niters)
+
+    setup_s = time.perf_counter() - t_setup
+    for _ in range(args.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    iters = 0
+    loop_ms = 0.0
+    for _ in range(args.steps):
+        iters += step()
+        loop_ms += st.loop_ms
+    ctx.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    solved = bool(st.solved)
+    niters_last = int(st.niters)
+    hist_gpu = hist[:st.hist_len].copy()
+    bytes_per_iter = st.bytes_moved / max(niters_last, 1)
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        it = torch.tensor([float(iters)], dtype=torch.float64, device=dev)
+        dist.all_reduce(it, op=dist.ReduceOp.SUM)
+        total_iters = float(it.item())
+    else:
+        total_iters = float(iters)
+
+    prof = _lib.Profile()
+    _lib.check(_lib.lib.cpk_profile_kernels(ctx.h, A.h, Cm.h, M.h, args.profile_reps, C.byref(prof)))
+    gbs = lambda byts, ms: byts / (ms * 1e-3) / 1e9  # noqa: E731
+    achieved = gbs(prof.resid_bytes, prof.resid_ms)
+    roofline = {"bound": "hbm", "kernel": "spmv_stream<EpiResid> (r = x - Kp*y)", "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "bytes_per_launch": prof.resid_bytes, "avg_ms": round(prof.resid_ms, 5)}
+    kernels = {k: {"avg_ms": round(getattr(prof, k + "_ms"), 5), "bytes": getattr(prof, k + "_bytes"),
+                   "GBps": round(gbs(getattr(prof, k + "_bytes"), getattr(prof, k + "_ms")), 1)}
+               for k in ("spmv", "resid", "fwd", "bwd", "apply")}
+    kernels["fwd"]["launches"] = kernels["bwd"]["launches"] = int(prof.fwd_launches)
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, parity = cpu_baseline(S, b1.cpu().numpy(), M, args, hist_gpu, niters_last)
+
+    ms_per_step = dt / args.steps * 1e3
+    value = total_iters / dt
+    if rank == 0:
+        line = {
+            "metric": "Krylov iters/sec + SpMV GB/s (% HBM peak), cpminres 10M-dof, 1/2/4/8 GPU",
+            "value": round(value, 2), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"S10 synthetic symmetric saddle-point system, cp{args.method} to convergence "
+                                   "(cpk_exprog1 options), step = one method call",
+                       "N": N, "n": n, "m": m, "nnz_kp": M.info["nnz_kp"], "nnz_l": M.info["nnz_l"],
+                       "sweep_launches": M.info["nrounds"], "elim_tree_depth": M.info["depth"],
+                       "parallelism": "single" if world == 1 else f"replicas{world}", "seed": S["seed"]},
+            "iters_per_step": round(total_iters / args.steps / world, 2), "solved": solved,
+            "roofline": roofline,
+            "roofline_iteration": {"bytes_per_iter": bytes_per_iter,
+                                   "achieved": round(bytes_per_iter * total_iters / world / dt / 1e9, 1),
+                                   "frac": round(bytes_per_iter * total_iters / world / dt / 1e9 / HBM_PEAK_GBS, 4)},
+            "kernels": kernels,
+            "device_loop_ms_per_step": round(loop_ms / args.steps, 3),
+            "setup_s": round(setup_s, 2),
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(S, b1, M_gpu, args, hist_gpu, niters_gpu):
+    """The oracle's cpminres on the same system and shifted rhs, one host core."""
+    from oracle import oracle as O
+    L, D, perm = M_gpu.export_factors()
+    Mo = O.LDL2(S["G"], S["B"], -S["C"], perm=perm)  # the oracle's own factorization, same pivot order
+    Mo.set(nitref=EXPROG_OPTS["nitref"], itref_tol=EXPROG_OPTS["itref_tol"],
+           force_itref=1.0, residual_update=1.0)
+    # probe two iterations to size a 10-30 s sample
+    t = time.perf_counter()
+    O.method(args.method, b1, S["Q"], S["C"], Mo, dict(EXPROG_OPTS, itmax=2))
+    per_iter = (time.perf_counter() - t) / 3.0  # init M-apply + 2 iterations
+    itmax = int(max(2, min(EXPROG_OPTS["itmax"], args.cpu_seconds / max(per_iter, 1e-9))))
+    t = time.perf_counter()
+    x, y, st = O.method(args.method, b1, S["Q"], S["C"], Mo, dict(EXPROG_OPTS, itmax=itmax))
+    dt = time.perf_counter() - t
+    it = int(st["niters"])
+    cpu = {"value": round(it / dt, 4), "unit": "iters/s", "cores": 1, "kind": "port",
+           "sample": f"oracle cp{args.method} on S10 (same b1, same pivot order), {it} iterations "
+                     f"(itmax {itmax}, solved {bool(st['solved'])}), {dt:.1f} s, gcc -O2 single thread"}
+    parity = None
+    if st["solved"]:
+        h = st["residHistory"]
+        parity = {"niters_gpu": niters_gpu, "niters_oracle": it, "niters_equal": niters_gpu == it,
+                  "max_hist_dev_over_h0": float(np.max(np.abs(h - hist_gpu[:len(h)])) / h[0])
+                  if len(h) == len(hist_gpu) else None}
+    return cpu, parity
+
+
+if __name__ == "__main__":
+    main()

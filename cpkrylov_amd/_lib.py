@@ -39,6 +39,12 @@ class PcInfo(C.Structure):
                                          "max_block_levels", "depth", "ordering")]
 
 
+class Profile(C.Structure):
+    _fields_ = [(k, C.c_double) for k in ("spmv_ms", "spmv_bytes", "resid_ms", "resid_bytes", "fwd_ms", "fwd_bytes",
+                                          "bwd_ms", "bwd_bytes", "apply_ms", "apply_bytes")] + \
+               [("fwd_launches", C.c_int64), ("bwd_launches", C.c_int64)]
+
+
 P = C.POINTER
 vp = C.c_void_p
 _SIGS = {
@@ -73,6 +79,8 @@ _SIGS = {
     "cpk_reg_solve": ([vp, C.c_int, P(C.c_double), vp, vp, vp, vp, P(Opts), P(C.c_double), P(Stats), P(vp)],
                       C.c_int),
     "cpk_reg_solve_device": ([vp, C.c_int, vp, vp, vp, vp, vp, P(Opts), vp, P(Stats)], C.c_int),
+    "cpk_reg_shift_device": ([vp, vp, vp, vp, vp, vp, vp, vp, P(C.c_int)], C.c_int),
+    "cpk_profile_kernels": ([vp, vp, vp, vp, C.c_int, P(Profile)], C.c_int),
     "cpk_symgivens": ([C.c_double, C.c_double, P(C.c_double), P(C.c_double), P(C.c_double)], C.c_int),
 }
 for _name, (_args, _res) in _SIGS.items():

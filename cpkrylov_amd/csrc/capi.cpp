@@ -345,6 +345,25 @@ int cpk_reg_solve_device(cpk_ctx ctx, int method, const double *d_b, cpk_mat A, 
     API_END
 }
 
+int cpk_reg_shift_device(cpk_ctx ctx, const double *d_b, cpk_mat A, cpk_mat B, cpk_mat C, cpk_pc M, double *d_b1,
+                         double *d_xy0, int *shifted) {
+    API_BEGIN
+    need(ctx && d_b && d_b1 && d_xy0 && B, "NULL argument");
+    check_method_dims(A, C, M);
+    const DMat &AC = A->blkdiag_with(C);
+    int s = reg_shift_device(ctx->c, d_b, AC, M->p->dKp, *M->p, d_b1, d_xy0);
+    if (shifted) *shifted = s;
+    API_END
+}
+
+int cpk_profile_kernels(cpk_ctx ctx, cpk_mat A, cpk_mat C, cpk_pc M, int reps, cpk_profile *out) {
+    API_BEGIN
+    need(ctx && out, "NULL argument");
+    check_method_dims(A, C, M);
+    profile_kernels(ctx->c, A->blkdiag_with(C), *M->p, reps, out);
+    API_END
+}
+
 int cpk_reg_solve(cpk_ctx ctx, int method, const double *b, cpk_mat A, cpk_mat B, cpk_mat C, cpk_mat G,
                   const cpk_opts *opts, double *x, cpk_stats *stats, cpk_pc *M_out) {
     API_BEGIN

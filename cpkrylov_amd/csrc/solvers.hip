@@ -1431,14 +1431,11 @@ void method_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, 
     }
 }
 
-void reg_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, const DMat &Kp, Precond &M,
-                      const cpk_opts *opts, double *d_x, cpk_stats *stats) {
+int reg_shift_device(Ctx &c, const double *d_b, const DMat &AC, const DMat &Kp, Precond &M, double *d_b1,
+                     double *d_xy0) {
     const int64_t n = M.n, m = M.m, N = M.N;
-    auto t0 = std::chrono::steady_clock::now();
     DBuf<int> flag;
     flag.alloc(1);
-    DBuf<double> xy0, b1, dxy, t1, t2;
-    xy0.alloc(N), b1.alloc(std::max<int64_t>(n, 1)), dxy.alloc(N), t1.alloc(N), t2.alloc(N);
     int shift = 0;
     if (m > 0) {
         c.ensure_partials((size_t)kEwGrid);
@@ -1446,21 +1443,70 @@ void reg_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, con
         CPK_HIP(hipMemcpyAsync(&shift, flag.p, sizeof(int), hipMemcpyDeviceToHost, c.stream));
         CPK_HIP(hipStreamSynchronize(c.stream));
     }
-    const double *bb = d_b;
     if (shift) {
+        DBuf<double> t1, t2;
+        t1.alloc(N), t2.alloc(N);
         // xy0 = M * [zeros(n,1); b(n+1:n+m)]   (reg_cpkrylov.m:156)
         CPK_HIP(hipMemsetAsync(t1.p, 0, n * sizeof(double), c.stream));
         CPK_HIP(hipMemcpyAsync(t1.p + n, d_b + n, m * sizeof(double), hipMemcpyDeviceToDevice, c.stream));
-        M.apply(t1.p, N, xy0.p, nullptr);
-        launch_spmv(c, AC, xy0.p, t1.p, nullptr);            // rows < n: A*xy0(1:n)
-        launch_spmv_colmask(c, Kp, n, xy0.p, t2.p, nullptr);  // rows < n: B'*xy0(n+1:N)
-        launch_ew(c, n, ShiftRhs{d_b, t1.p, t2.p, b1.p});
-        bb = b1.p;
+        M.apply(t1.p, N, d_xy0, nullptr);
+        launch_spmv(c, AC, d_xy0, t1.p, nullptr);            // rows < n: A*xy0(1:n)
+        launch_spmv_colmask(c, Kp, n, d_xy0, t2.p, nullptr);  // rows < n: B'*xy0(n+1:N)
+        launch_ew(c, n, ShiftRhs{d_b, t1.p, t2.p, d_b1});    // b1 = b(1:n) - A*xy0(1:n) - B'*xy0(n+1:N)
+        CPK_HIP(hipStreamSynchronize(c.stream));
+    } else {
+        CPK_HIP(hipMemcpyAsync(d_b1, d_b, n * sizeof(double), hipMemcpyDeviceToDevice, c.stream));
+        CPK_HIP(hipMemsetAsync(d_xy0, 0, N * sizeof(double), c.stream));
     }
-    method_solve_device(c, method, bb, AC, M, opts, shift ? dxy.p : d_x, stats);
-    if (shift) launch_ew(c, N, Recover{xy0.p, dxy.p, d_x});
+    return shift;
+}
+
+void reg_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, const DMat &Kp, Precond &M,
+                      const cpk_opts *opts, double *d_x, cpk_stats *stats) {
+    const int64_t n = M.n, N = M.N;
+    auto t0 = std::chrono::steady_clock::now();
+    DBuf<double> xy0, b1, dxy;
+    xy0.alloc(N), b1.alloc(std::max<int64_t>(n, 1)), dxy.alloc(N);
+    const int shift = reg_shift_device(c, d_b, AC, Kp, M, b1.p, xy0.p);
+    method_solve_device(c, method, b1.p, AC, M, opts, shift ? dxy.p : d_x, stats);
+    if (shift) launch_ew(c, N, Recover{xy0.p, dxy.p, d_x});  // x = [xy0(1:n) + dx; xy0(n+1:N) + dy]
     CPK_HIP(hipStreamSynchronize(c.stream));
     if (stats) stats->stime = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *out) {
+    const int64_t N = M.N;
+    reps = std::max(reps, 1);
+    DBuf<double> x, y, z;
+    x.alloc(N), y.alloc(N), z.alloc(N);
+    CPK_HIP(hipMemsetAsync(y.p, 0, N * sizeof(double), c.stream));
+    launch_set_concat(c, x.p, nullptr, 0, N);  // zeros
+    std::vector<double> h(N);
+    for (int64_t i = 0; i < N; i++) h[i] = 1.0 + 1e-3 * (double)(i % 1000);
+    CPK_HIP(hipMemcpy(x.p, h.data(), N * sizeof(double), hipMemcpyHostToDevice));
+    auto timeit = [&](const std::function<void()> &f) {
+        f();  // warm
+        CPK_HIP(hipEventRecord(c.ev0, c.stream));
+        for (int r = 0; r < reps; r++) f();
+        CPK_HIP(hipEventRecord(c.ev1, c.stream));
+        CPK_HIP(hipEventSynchronize(c.ev1));
+        float ms = 0;
+        CPK_HIP(hipEventElapsedTime(&ms, c.ev0, c.ev1));
+        return (double)ms / reps;
+    };
+    const double Nn = (double)N, l = (double)M.dF.nnz;
+    out->spmv_ms = timeit([&]() { launch_spmv(c, AC, x.p, y.p, nullptr); });
+    out->spmv_bytes = 12.0 * AC.nnz + 4.0 * (Nn + 1) + 8.0 * Nn + 8.0 * Nn;
+    out->resid_ms = timeit([&]() { launch_spmv_resid(c, M.dKp, x.p, M.n, y.p, z.p, nullptr, nullptr); });
+    out->resid_bytes = 12.0 * M.dKp.nnz + 4.0 * (Nn + 1) + 8.0 * Nn /*y*/ + 8.0 * Nn /*x*/ + 8.0 * Nn /*r*/;
+    out->fwd_ms = timeit([&]() { launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr); });
+    out->fwd_bytes = 12.0 * l + 4.0 * (Nn + 1) + 4.0 * Nn /*perm*/ + 8.0 * Nn /*x*/ + 8.0 * Nn /*w*/;
+    out->bwd_ms = timeit([&]() { launch_sptrsv_bwd(c, M.dF, M.w.p, z.p, false, nullptr, nullptr); });
+    out->bwd_bytes = 12.0 * l + 4.0 * (Nn + 1) + 4.0 * Nn + 8.0 * Nn /*D*/ + 8.0 * Nn /*w in*/ + 8.0 * Nn /*w out*/ +
+                     8.0 * Nn /*y*/;
+    out->apply_ms = timeit([&]() { M.apply(x.p, M.n, z.p, nullptr); });
+    out->apply_bytes = M.apply_bytes();
+    out->fwd_launches = out->bwd_launches = (int64_t)M.dF.round_ptr.size() - 1;
 }
 
 // Algorithmic HBM bytes of one method call: per iteration the Krylov SpMV,

@@ -9,5 +9,8 @@ void method_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, 
 // reg_cpkrylov's shift + method + recovery (reg_cpkrylov.m:150-175): d_b (N), d_x (N)
 void reg_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, const DMat &Kp, Precond &M,
                       const cpk_opts *opts, double *d_x, cpk_stats *stats);
+int reg_shift_device(Ctx &c, const double *d_b, const DMat &AC, const DMat &Kp, Precond &M, double *d_b1,
+                     double *d_xy0);
+void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *out);
 double method_bytes(int method, const DMat &AC, const Precond &M, int64_t iters, const cpk_opts *opts);
 }  // namespace cpk

@@ -169,6 +169,26 @@ int cpk_reg_solve(cpk_ctx ctx, int method, const double *b, cpk_mat A, cpk_mat B
 int cpk_reg_solve_device(cpk_ctx ctx, int method, const double *d_b, cpk_mat A, cpk_mat B, cpk_mat C,
                          cpk_pc M, const cpk_opts *opts, double *d_x, cpk_stats *stats);
 
+/* The driver's shift step alone (reg_cpkrylov.m:152-160): if any(b(n+1:N)), xy0 = M*[0; b2]
+ * and b1 = b(1:n) - A*xy0(1:n) - B'*xy0(n+1:N); else b1 = b(1:n), xy0 = 0.  Device pointers:
+ * d_b (N), d_b1 (n), d_xy0 (N).  *shifted reports whether the shift was taken. */
+int cpk_reg_shift_device(cpk_ctx ctx, const double *d_b, cpk_mat A, cpk_mat B, cpk_mat C, cpk_pc M,
+                         double *d_b1, double *d_xy0, int *shifted);
+
+/* ---- measurement ----------------------------------------------------------------------- */
+/* Average device time (HIP events on the context stream, `reps` back-to-back launches) and
+ * algorithmic HBM bytes per launch of each kernel class of an
+ * iteration.  Times in ms. */
+typedef struct {
+    double spmv_ms, spmv_bytes;      /* Krylov operator blkdiag(A, C) SpMV (u = A*v, t = C*q) */
+    double resid_ms, resid_bytes;    /* saddle-point SpMV r = x - Kp*y (refinement residual) */
+    double fwd_ms, fwd_bytes;        /* forward sweep w = L \ P'x (all rounds) */
+    double bwd_ms, bwd_bytes;        /* backward sweep y = P (L' \ (D \ w)) (all rounds) */
+    double apply_ms, apply_bytes;    /* one M*z with the current properties */
+    int64_t fwd_launches, bwd_launches;
+} cpk_profile;
+int cpk_profile_kernels(cpk_ctx ctx, cpk_mat A, cpk_mat C, cpk_pc M, int reps, cpk_profile *out);
+
 /* [c, s, d] = SymGivens(a, b)  (util/SymGivens.m:1-29) */
 int cpk_symgivens(double a, double b, double *c, double *s, double *d);
 
