@@ -93,13 +93,24 @@ struct DFactor {
     DBuf<int32_t> perm;     // perm[k] = original index of pivot k
     DBuf<int32_t> blk_lvl;  // [nblk + 1]
     DBuf<int32_t> lvl_row;  // [nlvl + 1]
+    DBuf<int32_t> meta;     // [nblk][8]: r0, r1, l0, l1, fwd e0, e1, bwd e0, e1
+    bool pipelined = true;  // round 0 through the persistent pipelined kernel
     std::vector<int64_t> round_ptr;  // host copy: blocks per round
+    int sweep_rows[2] = {192, 2048}, sweep_cap[2] = {576, 8192}, sweep_threads[2] = {64, 512};  // round 0 / rest
     size_t bytes() const {
         return fptr.bytes() + fcol.bytes() + fval.bytes() + bptr.bytes() + bcol.bytes() + bval.bytes() + D.bytes() +
-               perm.bytes() + blk_lvl.bytes() + lvl_row.bytes();
+               perm.bytes() + blk_lvl.bytes() + lvl_row.bytes() + meta.bytes();
     }
 };
 void make_dfactor(const Factor &f, const Schedule &s, DFactor &d);
+size_t sweep_lds_bytes(int R, int CAP);
+// Sweep configuration: rows and entries staged per block, threads per block.
+// CPK_SWEEP="rows,cap,threads" overrides the default.
+// CPK_SWEEP="R0,CAP0,T0,R1,CAP1,T1": round 0 / upper rounds.
+struct SweepConfig {
+    int rows[2] = {192, 2048}, cap[2] = {576, 8192}, threads[2] = {64, 512};
+};
+SweepConfig sweep_config();
 
 // ---- launchers (kernels.hip) -------------------------------------------------------------
 // Flags: a kernel is a no-op when *run == 0 or *active == 0 (either pointer may be null).
@@ -116,6 +127,8 @@ void launch_spmv_colmask(Ctx &c, const DMat &A, int64_t col_min, const double *x
 // forward sweep w = L \ (P' * xin), backward sweep out (=|+=) P * (L' \ (D \ w))
 void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
                        const int *active);
+// diagnostic: the forward sweep without its level phase (staging + write-back only)
+void launch_sptrsv_fwd_diag(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w);
 void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
                        const int *active);
 // small vector helpers
@@ -130,6 +143,7 @@ struct Analysis {
     Schedule S;
     int ordering = 0;
     double seconds = 0;
+    SweepConfig sweep;
 };
 Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22);
 

@@ -81,10 +81,26 @@ Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int /*nthrea
     return f;
 }
 
-Schedule build_schedule(const Factor &f, int64_t R) {
+Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1) {
     const int64_t N = f.N;
     Schedule s;
     s.N = N;
+    // Node weights: a block is staged in LDS when it holds at most R rows, at most CAP forward
+    // entries (rows of L) and at most CAP backward entries (columns of L).  With
+    // wt(v) = max(CAP/R, fwd(v), bwd(v)), a cluster of total weight <= CAP meets all three.
+    std::vector<int64_t> ent(N), wt0(N), wt1(N);
+    {
+        const int64_t u0 = std::max<int64_t>(1, CAP0 / std::max<int64_t>(R0, 1));
+        const int64_t u1 = std::max<int64_t>(1, CAP1 / std::max<int64_t>(R1, 1));
+        std::vector<int64_t> fl(N, 0);
+        for (int32_t i : f.Li) fl[i]++;
+        for (int64_t v = 0; v < N; v++) {
+            ent[v] = std::max(fl[v], f.Lp[v + 1] - f.Lp[v]);
+            wt0[v] = std::max(u0, ent[v]);
+            wt1[v] = std::max(u1, ent[v]);
+        }
+    }
+    auto capof = [&](int32_t r) { return r == 0 ? CAP0 : CAP1; };
     // children lists
     std::vector<int64_t> cptr(N + 2, 0);
     for (int64_t v = 0; v < N; v++)
@@ -114,15 +130,17 @@ Schedule build_schedule(const Factor &f, int64_t R) {
     int32_t round = 0;
     while (!alive.empty()) {
         for (int32_t v : alive) sz[v] = 0;
+        const std::vector<int64_t> &wt = round == 0 ? wt0 : wt1;
+        const int64_t CAP = capof(round);
         for (int32_t v : alive) {  // ascending: children before parents
-            sz[v] += 1;
+            sz[v] += wt[v];
             if (f.parent[v] >= 0 && is_alive[f.parent[v]]) sz[f.parent[v]] += sz[v];
         }
         const size_t before = alive.size();
         for (size_t q = alive.size(); q-- > 0;) {  // descending: parents before children
             const int32_t v = alive[q], p = f.parent[v];
-            if (sz[v] > R) root_of[v] = -1;
-            else if (p < 0 || sz[p] > R) root_of[v] = v, closed_round[v] = round;
+            if (sz[v] > CAP) root_of[v] = -1;
+            else if (p < 0 || sz[p] > CAP) root_of[v] = v, closed_round[v] = round;
             else root_of[v] = root_of[p];
         }
         std::vector<int32_t> rest;
@@ -141,17 +159,19 @@ Schedule build_schedule(const Factor &f, int64_t R) {
     std::vector<int64_t> open_size(N, 0);
     std::vector<int32_t> open_dep(N, -1);
     std::vector<int32_t> tmp;
+    const int64_t CAP = CAP1;
+    const std::vector<int64_t> &wt = wt1;
     for (int32_t v : alive) {
-        int64_t total = 1;
+        int64_t total = wt[v];
         tmp.clear();
         for (int64_t q = cptr[v]; q < cptr[v + 1]; q++)
             if (closed_round[kids[q]] < 0) tmp.push_back(kids[q]), total += open_size[kids[q]];
-        if (total > R) {
+        if (total > CAP) {
             std::sort(tmp.begin(), tmp.end(), [&](int32_t a, int32_t b) {
                 return open_size[a] != open_size[b] ? open_size[a] > open_size[b] : a < b;
             });
             for (int32_t c : tmp) {
-                if (total <= R) break;
+                if (total <= CAP) break;
                 closed_round[c] = open_dep[c] + 1;
                 total -= open_size[c];
             }
@@ -169,7 +189,7 @@ Schedule build_schedule(const Factor &f, int64_t R) {
     std::vector<int32_t> cl(N);
     for (int64_t v = N - 1; v >= 0; v--) cl[v] = closed_round[v] >= 0 ? (int32_t)v : cl[f.parent[v]];
     std::vector<int64_t> csize(N, 0);
-    for (int64_t v = 0; v < N; v++) csize[cl[v]]++;
+    for (int64_t v = 0; v < N; v++) csize[cl[v]] += (closed_round[cl[v]] == 0 ? wt0[v] : wt1[v]);
     int32_t nrounds = 0;
     for (int64_t v = 0; v < N; v++)
         if (closed_round[v] >= 0) nrounds = std::max(nrounds, closed_round[v] + 1);
@@ -181,9 +201,10 @@ Schedule build_schedule(const Factor &f, int64_t R) {
     int32_t nb = 0;
     s.round_ptr.assign(1, 0);
     for (int32_t r = 0; r < nrounds; r++) {
-        int64_t fill = R + 1;
+        const int64_t cap = capof(r);
+        int64_t fill = cap + 1;
         for (int32_t c : roots_by_round[r]) {
-            if (fill + csize[c] > R) {
+            if (fill + csize[c] > cap) {
                 nb++;
                 fill = 0;
             }

@@ -54,8 +54,9 @@ struct Factor {
 Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int nthreads);
 
 // ---- SpTRSV schedule ---------------------------------------------------------------------
-// The elimination tree is cut into blocks: sets of whole subtrees of at most R rows, solved
-// by one workgroup each.  Blocks form rounds (block-level sets): a round's blocks only
+// The elimination tree is cut into blocks: sets of whole subtrees of at most R rows and at
+// most CAP forward / backward factor entries (so a block fits in LDS), solved by one
+// workgroup each.  Blocks form rounds (block-level sets): a round's blocks only
 // depend on earlier rounds, so one kernel launch per round and sweep suffices.  Inside a
 // block, rows are grouped into intra-block levels separated by workgroup barriers.
 struct Schedule {
@@ -68,7 +69,9 @@ struct Schedule {
     int64_t max_levels = 0;
     int64_t depth = 0;
 };
-Schedule build_schedule(const Factor &f, int64_t R);
+// Round 0 (the wide bottom of the tree) uses blocks of (R0 rows, CAP0 entries); the upper
+// rounds use (R1, CAP1), typically larger so that few launches cover the top of the tree.
+Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1);
 // Apply the schedule's relabel to the factor (values unchanged, exact data movement).
 Factor relabel(const Factor &f, const Schedule &s);
 

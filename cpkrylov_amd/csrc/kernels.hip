@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "dev.hpp"
 #include "devutil.hpp"
@@ -87,6 +88,17 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d) {
     d.blk_lvl.upload(bl);
     d.lvl_row.upload(lr);
     d.round_ptr = s.round_ptr;
+    // per-block metadata records for the pipelined round-0 kernel
+    std::vector<int32_t> meta((size_t)d.nblk * 8);
+    for (int64_t b = 0; b < d.nblk; b++) {
+        const int64_t l0 = s.blk_lvl[b], l1 = s.blk_lvl[b + 1];
+        const int64_t r0 = s.lvl_row[l0], r1 = s.lvl_row[l1];
+        int32_t *m = &meta[(size_t)b * 8];
+        m[0] = (int32_t)r0, m[1] = (int32_t)r1, m[2] = (int32_t)l0, m[3] = (int32_t)l1;
+        m[4] = (int32_t)fptr[r0], m[5] = (int32_t)fptr[r1], m[6] = (int32_t)bptr[r0], m[7] = (int32_t)bptr[r1];
+    }
+    d.meta.upload(meta);
+    d.pipelined = getenv("CPK_NO_PIPE") == nullptr;
 }
 
 // ---- SpMV launchers --------------------------------------------------------------------------
@@ -184,44 +196,170 @@ void launch_spmv_resid_norm(Ctx &c, const DMat &A, const double *xin, int64_t ne
 // One workgroup per schedule block.  A block holds whole elimination subtrees; its rows are
 // contiguous and grouped by intra-block level, so a level is a contiguous row range and the
 // only synchronisation inside a block is a workgroup barrier between levels.  Rows of other
-// blocks that a block reads were written by an earlier launch (earlier round).
-__global__ __launch_bounds__(kBlock) void sptrsv_fwd_kernel(
-    int64_t blk0, const int32_t *__restrict__ blk_lvl, const int32_t *__restrict__ lvl_row,
+// blocks that a block reads were finished by an earlier launch (earlier round).
+//
+// Staged path (the block fits in LDS): phase 1 streams the block's row pointers, entries and
+// inputs from HBM with consecutive lanes on consecutive addresses, and folds every reference
+// to a row OUTSIDE the block into its product val*w[col] right away (that value is final);
+// phase 2 runs the levels entirely out of LDS; phase 3 writes the block's rows back
+// contiguously.  Each row still subtracts its terms in the reference's order, one rounding per
+// product and per subtraction, so the result is bit-identical to the direct path.
+// LDS image of a staged block (dynamic shared memory, sized per launch):
+//   double w[R] | double v[CAP + 4] | int16 c[CAP + 4] | int16 p[R + 1] | int16 lv[R + 1]
+struct SweepLds {
+    double *w, *v;
+    int16_t *c, *p, *lv;
+    __device__ SweepLds(char *smem, int R, int CAP) {
+        w = reinterpret_cast<double *>(smem);
+        v = w + R;
+        c = reinterpret_cast<int16_t *>(v + CAP + 4);
+        p = c + CAP + 4;
+        lv = p + R + 1;
+    }
+};
+size_t sweep_lds_bytes(int R, int CAP) {
+    return ((size_t)8 * R + 10 * ((size_t)CAP + 4) + 4 * ((size_t)R + 1) + 15) & ~(size_t)15;
+}
+
+// The level phase, out of LDS.  Per level every thread takes whole rows and consumes a row's
+// entries four at a time without branches: the (col, val) arrays are padded by four entries,
+// absent terms subtract +0.0 (which leaves every bit of the accumulator unchanged) and the
+// selects replace predicated loads, so a row costs a handful of instructions.  The terms are
+// still subtracted one at a time in the reference's order.  skip_first: the first level holds
+// only rows without entries (their values are already in place), as in round 0 forward.
+template <int TPB, bool BWD>
+__device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_first = false) {
+    int l = BWD ? nl - 1 : 0;
+    int li0 = 0;
+    if (skip_first && !BWD) l = 1, li0 = 1;
+    if (li0 >= nl) return;
+    int a = S.lv[l], z = S.lv[l + 1];
+    for (int li = li0; li < nl; li++) {
+        const int ln = BWD ? l - 1 : l + 1;
+        int an = 0, zn = 0;
+        if (li + 1 < nl) an = S.lv[ln], zn = S.lv[ln + 1];
+        for (int k = a + (int)threadIdx.x; k < z; k += TPB) {
+            const int e1 = S.p[k + 1];
+            double acc = S.w[k];
+            for (int e = S.p[k]; e < e1; e += 4) {
+                int c[4];
+                double v[4], x[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) c[j] = S.c[e + j], v[j] = S.v[e + j];
+#pragma unroll
+                for (int j = 0; j < 4; j++) x[j] = S.w[(c[j] >= 0 && e + j < e1) ? c[j] : 0];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const double t = (c[j] >= 0) ? v[j] * x[j] : v[j];
+                    acc -= (e + j < e1) ? t : 0.0;
+                }
+            }
+            S.w[k] = acc;
+        }
+        __syncthreads();
+        l = ln, a = an, z = zn;
+    }
+}
+
+template <int TPB, int MODE = 0>  // MODE 1 (diagnostic): staging + write-back only, no level phase
+__global__ __launch_bounds__(TPB) void sptrsv_fwd_kernel(
+    int64_t blk0, int R, int CAP, int skip_first, const int32_t *__restrict__ blk_lvl, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from, double *w,
     const int *run, const int *active) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
     const int64_t b = blk0 + blockIdx.x;
     const int l0 = blk_lvl[b], l1 = blk_lvl[b + 1];
-    for (int l = l0; l < l1; l++) {
-        const int r0 = lvl_row[l], r1 = lvl_row[l + 1];
-        for (int k = r0 + (int)threadIdx.x; k < r1; k += kBlock) {
+    const int r0 = lvl_row[l0], r1 = lvl_row[l1];
+    const uint32_t e0 = ptr[r0], e1 = ptr[r1];
+    const int nr = r1 - r0, ne = (int)(e1 - e0);
+    const int tid = threadIdx.x;
+    if (nr <= R && ne <= CAP) {
+        SweepLds S(smem, R, CAP);
+#pragma unroll 4
+        for (int i = tid; i < nr; i += TPB) {
+            S.p[i] = (int16_t)(ptr[r0 + i] - e0);
+            const int32_t src = perm[r0 + i];
+            const double x = xin[src];
+            S.w[i] = (src >= neg_from) ? -x : x;
+        }
+        if (tid == 0) S.p[nr] = (int16_t)ne;
+        for (int l = tid; l <= l1 - l0; l += TPB) S.lv[l] = (int16_t)(lvl_row[l0 + l] - r0);
+#pragma unroll 4
+        for (int e = tid; e < ne; e += TPB) {
+            const int32_t c = col[e0 + e];
+            const double v = val[e0 + e];
+            const bool local = c >= r0 && c < r1;
+            S.c[e] = local ? (int16_t)(c - r0) : (int16_t)-1;
+            S.v[e] = local ? v : v * w[c];
+        }
+        __syncthreads();
+        if (MODE == 0) sweep_levels<TPB, false>(S, l1 - l0, skip_first != 0);
+        for (int i = tid; i < nr; i += TPB) w[r0 + i] = S.w[i];
+        return;
+    }
+    for (int l = l0; l < l1; l++) {  // direct path: oversized block
+        const int a = lvl_row[l], z = lvl_row[l + 1];
+        for (int k = a + tid; k < z; k += TPB) {
             const int32_t src = perm[k];
             double acc = xin[src];
             if (src >= neg_from) acc = -acc;
-            const uint32_t e1 = ptr[k + 1];
-            for (uint32_t e = ptr[k]; e < e1; e++) acc -= val[e] * w[col[e]];
+            const uint32_t q1 = ptr[k + 1];
+            for (uint32_t e = ptr[k]; e < q1; e++) acc -= val[e] * w[col[e]];
             w[k] = acc;
         }
         __syncthreads();
     }
 }
 
-template <bool ADD>
-__global__ __launch_bounds__(kBlock) void sptrsv_bwd_kernel(
-    int64_t blk0, const int32_t *__restrict__ blk_lvl, const int32_t *__restrict__ lvl_row,
+template <int TPB, bool ADD>
+__global__ __launch_bounds__(TPB) void sptrsv_bwd_kernel(
+    int64_t blk0, int R, int CAP, const int32_t *__restrict__ blk_lvl, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, double *w, double *out, const int *run,
     const int *active) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
     const int64_t b = blk0 + blockIdx.x;
     const int l0 = blk_lvl[b], l1 = blk_lvl[b + 1];
-    for (int l = l1 - 1; l >= l0; l--) {
-        const int r0 = lvl_row[l], r1 = lvl_row[l + 1];
-        for (int k = r0 + (int)threadIdx.x; k < r1; k += kBlock) {
+    const int r0 = lvl_row[l0], r1 = lvl_row[l1];
+    const uint32_t e0 = ptr[r0], e1 = ptr[r1];
+    const int nr = r1 - r0, ne = (int)(e1 - e0);
+    const int tid = threadIdx.x;
+    if (nr <= R && ne <= CAP) {
+        SweepLds S(smem, R, CAP);
+#pragma unroll 4
+        for (int i = tid; i < nr; i += TPB) {
+            S.p[i] = (int16_t)(ptr[r0 + i] - e0);
+            S.w[i] = w[r0 + i] / D[r0 + i];
+        }
+        if (tid == 0) S.p[nr] = (int16_t)ne;
+        for (int l = tid; l <= l1 - l0; l += TPB) S.lv[l] = (int16_t)(lvl_row[l0 + l] - r0);
+#pragma unroll 4
+        for (int e = tid; e < ne; e += TPB) {
+            const int32_t c = col[e0 + e];
+            const double v = val[e0 + e];
+            const bool local = c >= r0 && c < r1;
+            S.c[e] = local ? (int16_t)(c - r0) : (int16_t)-1;
+            S.v[e] = local ? v : v * w[c];
+        }
+        __syncthreads();
+        sweep_levels<TPB, true>(S, l1 - l0);
+        for (int i = tid; i < nr; i += TPB) {
+            const double z = S.w[i];
+            w[r0 + i] = z;
+            const int32_t dst = perm[r0 + i];
+            out[dst] = ADD ? out[dst] + z : z;
+        }
+        return;
+    }
+    for (int l = l1 - 1; l >= l0; l--) {  // direct path: oversized block
+        const int a = lvl_row[l], z = lvl_row[l + 1];
+        for (int k = a + tid; k < z; k += TPB) {
             double acc = w[k] / D[k];
-            const uint32_t e1 = ptr[k + 1];
-            for (uint32_t e = ptr[k]; e < e1; e++) acc -= val[e] * w[col[e]];
+            const uint32_t q1 = ptr[k + 1];
+            for (uint32_t e = ptr[k]; e < q1; e++) acc -= val[e] * w[col[e]];
             w[k] = acc;
             const int32_t dst = perm[k];
             if (ADD) out[dst] = out[dst] + acc;
@@ -231,32 +369,225 @@ __global__ __launch_bounds__(kBlock) void sptrsv_bwd_kernel(
     }
 }
 
-void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                       const int *active) {
+// ---- persistent, software-pipelined sweep for the wide round 0 -------------------------------
+// Round 0 holds ~all rows in tens of thousands of small blocks.  A block's life is HBM latency
+// (staging) followed by LDS latency (levels), and LDS caps residency, so each workgroup here
+// walks a strided list of blocks and overlaps them: while block b runs its levels out of LDS,
+// the independent loads of block b + G (row pointers, perm, level bounds, entries) are already
+// in flight into registers.  Only the dependent gathers (x[perm] forward, w[col] of rows in
+// later rounds backward) stay exposed.  Per-block metadata is one 32-byte record (scalar load).
+// Arithmetic and order are those of the one-block-per-workgroup kernels: bit-identical.
+struct BlkMeta {
+    int32_t r0, r1, l0, l1, fe0, fe1, be0, be1;
+};
+
+template <int TPB, int RPT, int EPT, bool BWD, bool ADD>
+__global__ __launch_bounds__(TPB) void sptrsv_pipe_kernel(
+    int64_t blk0, int64_t nblk, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
+    const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
+    const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,
+    int64_t neg_from, double *w, double *out, const int *run, const int *active) {
+    constexpr int R = RPT * TPB, CAP = EPT * TPB;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (skip(run, active)) return;
+    SweepLds S(smem, R, CAP);
+    const int tid = threadIdx.x;
+    const int64_t G = gridDim.x;
+    // prefetched registers of the next block
+    uint32_t q[RPT];
+    int32_t sp[RPT], lvr[RPT];
+    double wr[RPT], dr[RPT];
+    int32_t cc[EPT];
+    double vv[EPT];
+    auto issue = [&](const BlkMeta &m) {
+        const int nr = m.r1 - m.r0, nl = m.l1 - m.l0;
+        const uint32_t e0 = BWD ? (uint32_t)m.be0 : (uint32_t)m.fe0;
+        const int ne = BWD ? m.be1 - m.be0 : m.fe1 - m.fe0;
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const int i = tid + j * TPB;
+            if (i < nr) {
+                q[j] = ptr[m.r0 + i];
+                sp[j] = perm[m.r0 + i];
+                if (BWD) wr[j] = w[m.r0 + i], dr[j] = D[m.r0 + i];
+            }
+            if (i < nl) lvr[j] = lvl_row[m.l0 + i];
+        }
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            const int e = tid + j * TPB;
+            if (e < ne) cc[j] = col[e0 + e], vv[j] = val[e0 + e];
+        }
+    };
+    int64_t b = blk0 + blockIdx.x;
+    const int64_t bend = blk0 + nblk;
+    if (b >= bend) return;
+    BlkMeta cur = meta[b];
+    issue(cur);
+    while (true) {
+        const int nr = cur.r1 - cur.r0, nl = cur.l1 - cur.l0;
+        const uint32_t e0 = BWD ? (uint32_t)cur.be0 : (uint32_t)cur.fe0;
+        const int ne = BWD ? cur.be1 - cur.be0 : cur.fe1 - cur.fe0;
+        const int r0 = cur.r0, r1 = cur.r1;
+        // registers -> LDS, with the dependent gathers
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const int i = tid + j * TPB;
+            if (i < nr) {
+                S.p[i] = (int16_t)(q[j] - e0);
+                if (BWD) {
+                    S.w[i] = wr[j] / dr[j];
+                } else {
+                    const double x = xin[sp[j]];
+                    S.w[i] = (sp[j] >= neg_from) ? -x : x;
+                }
+            }
+            if (i < nl) S.lv[i] = (int16_t)(lvr[j] - r0);
+        }
+        int32_t dst[RPT];
+#pragma unroll
+        for (int j = 0; j < RPT; j++) dst[j] = sp[j];
+        if (tid == 0) S.p[nr] = (int16_t)ne, S.lv[nl] = (int16_t)nr;
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            const int e = tid + j * TPB;
+            if (e < ne) {
+                const int32_t c = cc[j];
+                const bool local = c >= r0 && c < r1;
+                S.c[e] = local ? (int16_t)(c - r0) : (int16_t)-1;
+                S.v[e] = local ? vv[j] : vv[j] * w[c];
+            }
+        }
+        __syncthreads();
+        const int64_t bn = b + G;
+        BlkMeta nxt;
+        if (bn < bend) {
+            nxt = meta[bn];
+            issue(nxt);  // in flight during the level phase
+        }
+        sweep_levels<TPB, BWD>(S, nl, true);
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const int i = tid + j * TPB;
+            if (i < nr) {
+                const double z = S.w[i];
+                w[r0 + i] = z;
+                if (BWD) out[dst[j]] = ADD ? out[dst[j]] + z : z;
+            }
+        }
+        if (bn >= bend) break;
+        __syncthreads();
+        b = bn;
+        cur = nxt;
+    }
+}
+
+template <int TPB, int RPT, int EPT>
+static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
+                       double *w, double *out, const int *run, const int *active) {
+    if (F.sweep_threads[0] != TPB || F.sweep_rows[0] != RPT * TPB || F.sweep_cap[0] != EPT * TPB) return false;
+    const int64_t nb = F.round_ptr[1] - F.round_ptr[0];
+    const size_t lds = sweep_lds_bytes(RPT * TPB, EPT * TPB);
+    int occ = 0;
+    const void *fn = bwd ? (add ? (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, true, true>
+                                : (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, true, false>)
+                         : (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, false, false>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, TPB, lds) != hipSuccess || occ < 1) occ = 1;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t grid = std::min<int64_t>(nb, (int64_t)occ * cus);
+    const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
+    if (!bwd)
+        hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false>), dim3((unsigned)grid), dim3(TPB), lds,
+                           c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
+                           F.perm.p, xin, neg_from, w, out, run, active);
+    else if (add)
+        hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, true>), dim3((unsigned)grid), dim3(TPB), lds,
+                           c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
+                           F.perm.p, xin, neg_from, w, out, run, active);
+    else
+        hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, false>), dim3((unsigned)grid), dim3(TPB), lds,
+                           c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
+                           F.perm.p, xin, neg_from, w, out, run, active);
+    return true;
+}
+
+// round 0 through the pipelined kernel when its configuration is one of the instantiated ones
+static bool pipe_round0(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
+                        double *w, double *out, const int *run, const int *active) {
+    if (!F.pipelined || F.round_ptr.size() < 2) return false;
+    return pipe_round<128, 2, 6>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
+           pipe_round<64, 3, 9>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
+           pipe_round<64, 4, 12>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
+           pipe_round<128, 1, 4>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
+           pipe_round<256, 1, 3>(c, F, bwd, add, xin, neg_from, w, out, run, active);
+}
+
+template <int TPB, int MODE>
+static void fwd_round(Ctx &c, const DFactor &F, int64_t r, const double *xin, int64_t neg_from, double *w,
+                      const int *run, const int *active) {
+    const int i = r == 0 ? 0 : 1;
+    const int64_t b0 = F.round_ptr[r], nb = F.round_ptr[r + 1] - b0;
+    if (!nb) return;
+    hipLaunchKernelGGL((sptrsv_fwd_kernel<TPB, MODE>), dim3((unsigned)nb), dim3(TPB),
+                       sweep_lds_bytes(F.sweep_rows[i], F.sweep_cap[i]), c.stream, b0, F.sweep_rows[i],
+                       F.sweep_cap[i], r == 0 ? 1 : 0, F.blk_lvl.p, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.perm.p,
+                       xin, neg_from, w, run, active);
+}
+
+template <int TPB, bool ADD>
+static void bwd_round(Ctx &c, const DFactor &F, int64_t r, double *w, double *out, const int *run,
+                      const int *active) {
+    const int i = r == 0 ? 0 : 1;
+    const int64_t b0 = F.round_ptr[r], nb = F.round_ptr[r + 1] - b0;
+    if (!nb) return;
+    hipLaunchKernelGGL((sptrsv_bwd_kernel<TPB, ADD>), dim3((unsigned)nb), dim3(TPB),
+                       sweep_lds_bytes(F.sweep_rows[i], F.sweep_cap[i]), c.stream, b0, F.sweep_rows[i],
+                       F.sweep_cap[i], F.blk_lvl.p, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, w,
+                       out, run, active);
+}
+
+template <int MODE>
+static void fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
+                    const int *active) {
     const int64_t R = (int64_t)F.round_ptr.size() - 1;
     for (int64_t r = 0; r < R; r++) {
-        const int64_t b0 = F.round_ptr[r], nb = F.round_ptr[r + 1] - b0;
-        if (!nb) continue;
-        hipLaunchKernelGGL(sptrsv_fwd_kernel, dim3((unsigned)nb), dim3(kBlock), 0, c.stream, b0, F.blk_lvl.p,
-                           F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.perm.p, xin, neg_from, w, run, active);
+        if (r == 0 && MODE == 0 && pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active)) continue;
+        switch (F.sweep_threads[r == 0 ? 0 : 1]) {
+        case 64: fwd_round<64, MODE>(c, F, r, xin, neg_from, w, run, active); break;
+        case 128: fwd_round<128, MODE>(c, F, r, xin, neg_from, w, run, active); break;
+        case 512: fwd_round<512, MODE>(c, F, r, xin, neg_from, w, run, active); break;
+        default: fwd_round<256, MODE>(c, F, r, xin, neg_from, w, run, active); break;
+        }
     }
     CPK_HIP(hipGetLastError());
+}
+
+void launch_sptrsv_fwd_diag(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w) {
+    fwd_all<1>(c, F, xin, neg_from, w, nullptr, nullptr);
+}
+
+void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
+                       const int *active) {
+    fwd_all<0>(c, F, xin, neg_from, w, run, active);
 }
 
 void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
                        const int *active) {
     const int64_t R = (int64_t)F.round_ptr.size() - 1;
     for (int64_t r = R - 1; r >= 0; r--) {
-        const int64_t b0 = F.round_ptr[r], nb = F.round_ptr[r + 1] - b0;
-        if (!nb) continue;
-        if (add)
-            hipLaunchKernelGGL(sptrsv_bwd_kernel<true>, dim3((unsigned)nb), dim3(kBlock), 0, c.stream, b0,
-                               F.blk_lvl.p, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, w, out, run,
-                               active);
-        else
-            hipLaunchKernelGGL(sptrsv_bwd_kernel<false>, dim3((unsigned)nb), dim3(kBlock), 0, c.stream, b0,
-                               F.blk_lvl.p, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, w, out, run,
-                               active);
+        if (r == 0 && pipe_round0(c, F, true, add, nullptr, 0, w, out, run, active)) continue;
+        switch (F.sweep_threads[r == 0 ? 0 : 1] * 2 + (add ? 1 : 0)) {
+        case 128: bwd_round<64, false>(c, F, r, w, out, run, active); break;
+        case 129: bwd_round<64, true>(c, F, r, w, out, run, active); break;
+        case 256: bwd_round<128, false>(c, F, r, w, out, run, active); break;
+        case 257: bwd_round<128, true>(c, F, r, w, out, run, active); break;
+        case 1024: bwd_round<512, false>(c, F, r, w, out, run, active); break;
+        case 1025: bwd_round<512, true>(c, F, r, w, out, run, active); break;
+        case 513: bwd_round<256, true>(c, F, r, w, out, run, active); break;
+        default: bwd_round<256, false>(c, F, r, w, out, run, active); break;
+        }
     }
     CPK_HIP(hipGetLastError());
 }

@@ -9,6 +9,8 @@
 // (a functional no-op).  With force_itref the residual norms do not influence the loop and
 // the residual after the last refinement step is never read, so neither is computed.
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cmath>
 #include <memory>
@@ -17,7 +19,21 @@
 
 namespace cpk {
 
-static constexpr int64_t kSchedBlockRows = 1024;
+SweepConfig sweep_config() {
+    SweepConfig cfg;
+    if (const char *e = getenv("CPK_SWEEP")) {
+        int v[6] = {0, 0, 0, 0, 0, 0};
+        const int got = sscanf(e, "%d,%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5]);
+        if (got == 3) v[3] = v[0], v[4] = v[1], v[5] = v[2];
+        auto ok = [](int r, int c, int t) {
+            return r > 0 && r <= 16384 && c > 0 && c <= 16384 && (t == 64 || t == 128 || t == 256 || t == 512) &&
+                   sweep_lds_bytes(r, c) <= 160 * 1024;
+        };
+        if ((got == 3 || got == 6) && ok(v[0], v[1], v[2]) && ok(v[3], v[4], v[5]))
+            for (int i = 0; i < 2; i++) cfg.rows[i] = v[3 * i], cfg.cap[i] = v[3 * i + 1], cfg.threads[i] = v[3 * i + 2];
+    }
+    return cfg;
+}
 
 Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22) {
     auto t0 = std::chrono::steady_clock::now();
@@ -26,7 +42,8 @@ Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22) {
     an.n = A11.nrows, an.m = C22.nrows, an.N = an.n + an.m;
     std::vector<int32_t> perm = order_kp(an.Kp, an.n, &an.ordering);
     Factor f0 = ldl_factor(an.Kp, perm, 1);
-    an.S = build_schedule(f0, kSchedBlockRows);
+    an.sweep = sweep_config();
+    an.S = build_schedule(f0, an.sweep.rows[0], an.sweep.cap[0], an.sweep.rows[1], an.sweep.cap[1]);
     an.F = relabel(f0, an.S);
     an.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return an;
@@ -43,6 +60,9 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
     pc->S = std::move(an.S);
     make_dmat(pc->Kp, pc->dKp);
     make_dfactor(pc->F, pc->S, pc->dF);
+    for (int i = 0; i < 2; i++)
+        pc->dF.sweep_rows[i] = an.sweep.rows[i], pc->dF.sweep_cap[i] = an.sweep.cap[i],
+        pc->dF.sweep_threads[i] = an.sweep.threads[i];
     pc->w.alloc(pc->N);
     pc->r.alloc(pc->N);
     pc->active.alloc(1);

@@ -123,3 +123,26 @@ def test_divide_and_transpose(gpu_ctx):
     M.nitref = 3
     y = M * z
     assert np.linalg.norm(Kp @ y - z) <= 1e-8 * np.linalg.norm(z)
+
+
+@pytest.mark.parametrize("sweep", ["1024,3072,256", "512,1536,128", "256,768,64", "64,128,64", "256,768,128,2048,8192,512", "192,576,64", "128,512,128"])
+@pytest.mark.parametrize("name", ["cvxqp1_m", "cvxqp2_s", "synthetic"])
+def test_precond_apply_bitexact_sweep_configs(gpu_ctx, name, sweep, monkeypatch):
+    """Every LDS staging configuration (and the direct path for blocks that do not fit) gives
+    the same bits as the oracle's column-oriented solve."""
+    import cpkrylov_amd as cpk
+    from cpkrylov_amd.synthetic import saddle_system
+    monkeypatch.setenv("CPK_SWEEP", sweep)
+    if name == "synthetic":
+        S = saddle_system(N=50000)
+        G, B, C = S["G"], S["B"], S["C"]
+    else:
+        P = F.load(name)
+        G, B, C = P["G"], P["B"], P["C"]
+    M = cpk.opLDL2(G, B, -C)
+    M.nitref, M.force_itref = 1, True
+    L, D, perm = M.export_factors()
+    Mo = O.LDL2(G, B, -C, factors=(L, D, perm))
+    Mo.set(nitref=1.0, force_itref=1.0)
+    z = np.random.default_rng(11).standard_normal(M.n)
+    assert np.array_equal(M * z, Mo @ z)
