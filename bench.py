@@ -42,11 +42,15 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-reps", type=int, default=20)
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE passes")
+    ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
 def main():
     args = parse()
+    if args.pmc_probe:
+        return pmc_probe(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -138,6 +142,11 @@ def main():
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(S, b1.cpu().numpy(), M, args, hist_gpu, niters_last)
+    pmc = None
+    if rank == 0 and world == 1 and not args.no_pmc:
+        pmc = pmc_traffic(args)
+        if pmc and "resid" in pmc:
+            roofline["traffic"] = pmc["resid"]["bytes"]
 
     ms_per_step = dt / args.steps * 1e3
     value = total_iters / dt
@@ -161,6 +170,7 @@ def main():
             "device_loop_ms_per_step": round(loop_ms / args.steps, 3),
             "setup_s": round(setup_s, 2),
             "cpu_baseline": cpu,
+            "pmc": pmc,
             "parity": parity,
         }
         print(json.dumps(line), flush=True)
@@ -194,6 +204,91 @@ def cpu_baseline(S, b1, M_gpu, args, hist_gpu, niters_gpu):
                   "max_hist_dev_over_h0": float(np.max(np.abs(h - hist_gpu[:len(h)])) / h[0])
                   if len(h) == len(hist_gpu) else None}
     return cpu, parity
+
+
+PMC_REPS = 5
+
+
+def pmc_probe(args):
+    """Child program run under rocprofv3 --pmc: the kernel profile of S10 and nothing else.
+    Launch order (solvers.hip profile_kernels): (1 + reps) Krylov SpMVs, (1 + reps) residual
+    SpMVs, then the forward and backward sweeps, round by round."""
+    import cpkrylov_amd as cpk
+    from cpkrylov_amd import _lib
+    from cpkrylov_amd.synthetic import saddle_system
+    S = saddle_system(N=args.size)
+    ctx = cpk.Context(device=0)
+    A, Cm = cpk.Matrix(S["Q"], ctx), cpk.Matrix(S["C"], ctx)
+    M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+    M.nitref, M.force_itref = EXPROG_OPTS["nitref"], EXPROG_OPTS["force_itref"]
+    prof = _lib.Profile()
+    _lib.check(_lib.lib.cpk_profile_kernels(ctx.h, A.h, Cm.h, M.h, PMC_REPS, C.byref(prof)))
+    print(json.dumps({"resid_bytes": prof.resid_bytes, "spmv_bytes": prof.spmv_bytes,
+                      "fwd_bytes": prof.fwd_bytes, "bwd_bytes": prof.bwd_bytes,
+                      "rounds": int(prof.fwd_launches)}), flush=True)
+
+
+def pmc_traffic(args):
+    """HBM bytes per launch from rocprofv3 counters, one pass per counter (FETCH_SIZE and
+    WRITE_SIZE do not fit one TCC pass).  Corrections per MI355X_MICROARCH.md (HBM section):
+    counters are in KiB; FETCH_SIZE counts 128-B read requests at 64 B, so it is doubled.
+    Returns None when rocprofv3 is unavailable or a pass fails (traffic is then reported null)."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None
+    out = {}
+    reps = PMC_REPS
+    with tempfile.TemporaryDirectory(prefix="cpk_pmc_") as tmp:
+        counts = {}
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, ctr)
+            cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+                   sys.executable, os.path.abspath(__file__), "--pmc-probe", "--size", str(args.size)]
+            try:
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+            except subprocess.TimeoutExpired:
+                return None
+            if r.returncode != 0:
+                return {"error": f"rocprofv3 {ctr} pass exited {r.returncode}"}
+            probe = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+            files = [os.path.join(dp, f) for dp, _, fs in os.walk(d) for f in fs if f.endswith("counter_collection.csv")]
+            if not files:
+                return {"error": f"no counter file from the {ctr} pass"}
+            rows = sorted(csv.DictReader(open(files[0])), key=lambda q: int(q["Dispatch_Id"]))
+            counts[ctr] = rows
+        kib = 1024.0
+
+        def per_launch(name_pred, sel):
+            f = [float(q["Counter_Value"]) for q in counts["FETCH_SIZE"] if name_pred(q["Kernel_Name"])]
+            w = [float(q["Counter_Value"]) for q in counts["WRITE_SIZE"] if name_pred(q["Kernel_Name"])]
+            f, w = sel(f), sel(w)
+            if not f or len(f) != len(w):
+                return None
+            fb, wb = 2.0 * kib * sum(f) / len(f), kib * sum(w) / len(w)
+            return {"fetch": round(fb), "write": round(wb), "bytes": round(fb + wb), "launches": len(f)}
+
+        spmv = lambda nm: nm.split("<")[0].split("(")[0].strip().endswith("spmv_stream")  # noqa: E731
+        R = probe["rounds"]
+        out["resid"] = per_launch(spmv, lambda v: v[reps + 2:2 * reps + 2])
+        out["spmv"] = per_launch(spmv, lambda v: v[1:reps + 1])
+        # sweeps: (1 + reps) x R launches each; sum the rounds of one sweep
+        sweep = lambda nm: "sptrsv" in nm  # noqa: E731  (round-0 pipe kernel included)
+        for k, lo in (("fwd", R), ("bwd", R * (reps + 1) + R)):
+            pl = per_launch(sweep, lambda v, lo=lo: v[lo:lo + R * reps])
+            if pl:
+                pl = {kk: (vv * R if kk != "launches" else vv // R) for kk, vv in pl.items()}
+            out[k] = pl
+        for k in ("resid", "spmv", "fwd", "bwd"):
+            if out.get(k):
+                out[k]["algorithmic"] = probe[k + "_bytes"]
+                out[k]["ratio"] = round(out[k]["bytes"] / probe[k + "_bytes"], 3)
+        out["method"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over the S10 kernel "
+                         "profile; FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B), KiB -> bytes")
+    return out
 
 
 if __name__ == "__main__":

@@ -109,6 +109,7 @@ size_t sweep_lds_bytes(int R, int CAP);
 // CPK_SWEEP="R0,CAP0,T0,R1,CAP1,T1": round 0 / upper rounds.
 struct SweepConfig {
     int rows[2] = {192, 2048}, cap[2] = {576, 8192}, threads[2] = {64, 512};
+    int sub0 = 0;  // round-0 subtree cap (0: cap[0])
 };
 SweepConfig sweep_config();
 

@@ -81,7 +81,8 @@ Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int /*nthrea
     return f;
 }
 
-Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1) {
+Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1, int64_t SUB0) {
+    if (SUB0 <= 0 || SUB0 > CAP0) SUB0 = CAP0;
     const int64_t N = f.N;
     Schedule s;
     s.N = N;
@@ -131,7 +132,8 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     while (!alive.empty()) {
         for (int32_t v : alive) sz[v] = 0;
         const std::vector<int64_t> &wt = round == 0 ? wt0 : wt1;
-        const int64_t CAP = capof(round);
+        // round 0 peels subtrees of weight <= SUB0 and packs several of them per block
+        const int64_t CAP = round == 0 ? SUB0 : capof(round);
         for (int32_t v : alive) {  // ascending: children before parents
             sz[v] += wt[v];
             if (f.parent[v] >= 0 && is_alive[f.parent[v]]) sz[f.parent[v]] += sz[v];

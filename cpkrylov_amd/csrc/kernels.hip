@@ -520,6 +520,8 @@ static bool pipe_round0(Ctx &c, const DFactor &F, bool bwd, bool add, const doub
     return pipe_round<128, 2, 6>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
            pipe_round<64, 3, 9>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
            pipe_round<64, 4, 12>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
+           pipe_round<64, 6, 18>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
+           pipe_round<64, 8, 24>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
            pipe_round<128, 1, 4>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
            pipe_round<256, 1, 3>(c, F, bwd, add, xin, neg_from, w, out, run, active);
 }

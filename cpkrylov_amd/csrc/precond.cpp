@@ -22,15 +22,17 @@ namespace cpk {
 SweepConfig sweep_config() {
     SweepConfig cfg;
     if (const char *e = getenv("CPK_SWEEP")) {
-        int v[6] = {0, 0, 0, 0, 0, 0};
-        const int got = sscanf(e, "%d,%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5]);
+        int v[7] = {0, 0, 0, 0, 0, 0, 0};
+        const int got = sscanf(e, "%d,%d,%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5], &v[6]);
         if (got == 3) v[3] = v[0], v[4] = v[1], v[5] = v[2];
         auto ok = [](int r, int c, int t) {
             return r > 0 && r <= 16384 && c > 0 && c <= 16384 && (t == 64 || t == 128 || t == 256 || t == 512) &&
                    sweep_lds_bytes(r, c) <= 160 * 1024;
         };
-        if ((got == 3 || got == 6) && ok(v[0], v[1], v[2]) && ok(v[3], v[4], v[5]))
+        if ((got == 3 || got == 6 || got == 7) && ok(v[0], v[1], v[2]) && ok(v[3], v[4], v[5])) {
             for (int i = 0; i < 2; i++) cfg.rows[i] = v[3 * i], cfg.cap[i] = v[3 * i + 1], cfg.threads[i] = v[3 * i + 2];
+            cfg.sub0 = got == 7 ? v[6] : 0;
+        }
     }
     return cfg;
 }
@@ -43,7 +45,7 @@ Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22) {
     std::vector<int32_t> perm = order_kp(an.Kp, an.n, &an.ordering);
     Factor f0 = ldl_factor(an.Kp, perm, 1);
     an.sweep = sweep_config();
-    an.S = build_schedule(f0, an.sweep.rows[0], an.sweep.cap[0], an.sweep.rows[1], an.sweep.cap[1]);
+    an.S = build_schedule(f0, an.sweep.rows[0], an.sweep.cap[0], an.sweep.rows[1], an.sweep.cap[1], an.sweep.sub0);
     an.F = relabel(f0, an.S);
     an.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return an;
