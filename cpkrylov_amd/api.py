@@ -233,16 +233,50 @@ def analyze(A, B, Cm):
         check(lib.cpk_analysis_export(h, Lp.ctypes.data_as(_P(C.c_int64)), Li.ctypes.data_as(_P(C.c_int32)),
                                       _dptr(Lx), _dptr(D), perm.ctypes.data_as(_P(C.c_int32))))
         nl = C.c_int64()
-        check(lib.cpk_analysis_schedule(h, C.byref(nl), None, None, None))
+        check(lib.cpk_analysis_schedule(h, C.byref(nl), None, None, None, None))
         rp = np.empty(info["nrounds"] + 1, np.int64)
         bl = np.empty(info["nblocks"] + 1, np.int64)
         lr = np.empty(nl.value + 1, np.int64)
+        order = np.empty(N, np.int32)
         check(lib.cpk_analysis_schedule(h, None, rp.ctypes.data_as(_P(C.c_int64)), bl.ctypes.data_as(_P(C.c_int64)),
-                                        lr.ctypes.data_as(_P(C.c_int64))))
+                                        lr.ctypes.data_as(_P(C.c_int64)), order.ctypes.data_as(_P(C.c_int32))))
     finally:
         lib.cpk_analysis_destroy(h)
     L = sp.csc_matrix((Lx[:nnz], Li[:nnz], Lp), shape=(N, N))
-    return dict(info=info, L=L, D=D, perm=perm, round_ptr=rp, blk_lvl=bl, lvl_row=lr)
+    return dict(info=info, L=L, D=D, perm=perm, round_ptr=rp, blk_lvl=bl, lvl_row=lr, order=order)
+
+
+_PLAN_F64 = {"fsub_Lx", "fsub_D", "extra_val", "tf_val", "tb_val", "DT", "kp_val", "ac_val", "ab_val"}
+_PLAN_NAMES = ("sizes", "dofs", "node_rank", "T", "fsub_Lp", "fsub_Li", "fsub_Lx", "fsub_D", "fsub_perm",
+               "fsub_parent", "fsub_key", "extra_ptr", "extra_col", "extra_key", "extra_val", "tf_ptr", "tf_col",
+               "tf_val", "tf_src", "tb_ptr", "tb_col", "tb_val", "DT", "tlev_ptr", "tlev_rows", "tsend", "tdof") + \
+    tuple(f"{k}_{a}" for k in ("kp", "ac", "ab") for a in ("ptr", "col", "val", "send"))
+
+
+def dist_plan(G, B, Cneg, A, Cop, nranks, rank):
+    """Host-only row-block plan of `rank` for opLDL2(G, B, Cneg) and the
+    Krylov operator blocks A, Cop: a dict of numpy arrays (see cpk_plan_array in cpk.h)."""
+    mats = [Matrix(M, host_only=True) for M in (G, B, Cneg, A, Cop)]
+    h = C.c_void_p()
+    check(lib.cpk_analyze(mats[0].h, mats[1].h, mats[2].h, C.byref(h)))
+    p = C.c_void_p()
+    try:
+        check(lib.cpk_analysis_plan(h, mats[3].h, mats[4].h, int(nranks), int(rank), C.byref(p)))
+    finally:
+        lib.cpk_analysis_destroy(h)
+    out = {}
+    try:
+        for nm in _PLAN_NAMES:
+            cnt = C.c_int64()
+            check(lib.cpk_plan_array(p, nm.encode(), C.byref(cnt), None))
+            arr = np.empty(cnt.value, np.float64 if nm in _PLAN_F64 else np.int64)
+            check(lib.cpk_plan_array(p, nm.encode(), C.byref(cnt), arr.ctypes.data_as(C.c_void_p)))
+            out[nm] = arr
+    finally:
+        lib.cpk_plan_destroy(p)
+    keys = ("P", "rank", "n", "m", "N", "n_loc", "m_loc", "N_loc", "nsub", "nT", "kt", "kp_kmax", "ac_kmax", "ab_kmax")
+    out.update({k: int(v) for k, v in zip(keys, out["sizes"])})
+    return out
 
 
 # ---- solvers ----------------------------------------------------------------------------------

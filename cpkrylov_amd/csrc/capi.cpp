@@ -13,6 +13,7 @@
 
 #include "cpk.h"
 #include "dev.hpp"
+#include "dist.hpp"
 #include "solvers.hpp"
 
 using namespace cpk;
@@ -49,6 +50,14 @@ struct cpk_mat_s {
 
 struct cpk_analysis_s {
     Analysis an;
+};
+
+struct cpk_plan_s {
+    TreeSplit ts;
+    DofMap dm;
+    RankPlan rp;
+    DistCsr kp, ac, ab;
+    int64_t n = 0, m = 0;
 };
 
 struct cpk_pc_s {
@@ -411,7 +420,7 @@ int cpk_analysis_get_info(cpk_analysis a, cpk_pc_info *info) {
     const Analysis &an = a->an;
     info->n = an.n, info->m = an.m, info->N = an.N;
     info->nnz_kp = an.Kp.nnz();
-    info->nnz_l = (int64_t)an.F.Li.size();
+    info->nnz_l = (int64_t)an.F0.Li.size();
     info->nblocks = (int64_t)an.S.blk_row.size() - 1;
     info->nrounds = (int64_t)an.S.round_ptr.size() - 1;
     info->max_block_levels = an.S.max_levels;
@@ -423,7 +432,7 @@ int cpk_analysis_get_info(cpk_analysis a, cpk_pc_info *info) {
 int cpk_analysis_export(cpk_analysis a, int64_t *Lcolptr, int32_t *Lrowind, double *Lval, double *D, int32_t *perm) {
     API_BEGIN
     need(a, "NULL argument");
-    const Factor &f = a->an.F;
+    const Factor &f = a->an.F0;
     if (Lcolptr) std::memcpy(Lcolptr, f.Lp.data(), f.Lp.size() * sizeof(int64_t));
     if (Lrowind) std::memcpy(Lrowind, f.Li.data(), f.Li.size() * sizeof(int32_t));
     if (Lval) std::memcpy(Lval, f.Lx.data(), f.Lx.size() * sizeof(double));
@@ -432,14 +441,104 @@ int cpk_analysis_export(cpk_analysis a, int64_t *Lcolptr, int32_t *Lrowind, doub
     API_END
 }
 
-int cpk_analysis_schedule(cpk_analysis a, int64_t *nlevels, int64_t *round_ptr, int64_t *blk_lvl, int64_t *lvl_row) {
+int cpk_analysis_schedule(cpk_analysis a, int64_t *nlevels, int64_t *round_ptr, int64_t *blk_lvl, int64_t *lvl_row,
+                          int32_t *order) {
     API_BEGIN
     need(a, "NULL argument");
     const Schedule &s = a->an.S;
+    if (order) std::memcpy(order, s.order.data(), s.order.size() * sizeof(int32_t));
     if (nlevels) *nlevels = (int64_t)s.lvl_row.size() - 1;
     if (round_ptr) std::memcpy(round_ptr, s.round_ptr.data(), s.round_ptr.size() * sizeof(int64_t));
     if (blk_lvl) std::memcpy(blk_lvl, s.blk_lvl.data(), s.blk_lvl.size() * sizeof(int64_t));
     if (lvl_row) std::memcpy(lvl_row, s.lvl_row.data(), s.lvl_row.size() * sizeof(int64_t));
+    API_END
+}
+
+int cpk_analysis_plan(cpk_analysis a, cpk_mat A, cpk_mat C, int nranks, int rank, cpk_plan *out) {
+    API_BEGIN
+    need(a && A && C && out, "NULL argument");
+    need(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / nranks");
+    const Analysis &an = a->an;
+    need(A->h.nrows == an.n && A->h.ncols == an.n && C->h.nrows == an.m && C->h.ncols == an.m,
+         "A and C must match the analysis' n and m");
+    auto p = std::make_unique<cpk_plan_s>();
+    p->n = an.n, p->m = an.m;
+    p->ts = split_tree(an.F0, nranks);
+    p->dm = make_dofmap(an.F0, p->ts, an.n);
+    p->rp = make_rank_plan(an.F0, p->ts, p->dm, rank);
+    p->kp = dist_csr(an.Kp, p->dm, rank, false);
+    p->ac = dist_csr(blkdiag(A->h, C->h), p->dm, rank, false);
+    p->ab = dist_csr(hstack_ab(A->h, an.Kp, an.n), p->dm, rank, true);
+    *out = p.release();
+    API_END
+}
+
+int cpk_plan_destroy(cpk_plan p) {
+    API_BEGIN
+    delete p;
+    API_END
+}
+
+int cpk_plan_array(cpk_plan p, const char *name, int64_t *count, void *out) {
+    API_BEGIN
+    need(p && name && count, "NULL argument");
+    const RankPlan &r = p->rp;
+    const std::string nm(name);
+    std::vector<int64_t> iv;
+    std::vector<double> dv;
+    bool isd = false;
+    auto I = [&](const auto &v) { iv.assign(v.begin(), v.end()); };
+    auto Dv = [&](const std::vector<double> &v) { dv = v, isd = true; };
+    const DistCsr *dc = nm.rfind("kp_", 0) == 0 ? &p->kp : nm.rfind("ac_", 0) == 0 ? &p->ac : nm.rfind("ab_", 0) == 0 ? &p->ab : nullptr;
+    const std::string sub = dc ? nm.substr(3) : nm;
+    if (dc) {
+        if (sub == "ptr") I(dc->a.ptr);
+        else if (sub == "col") I(dc->a.ind);
+        else if (sub == "val") Dv(dc->a.val);
+        else if (sub == "send") I(dc->send);
+        else throw Error(CPK_ERR_ARGS, "unknown plan array " + nm);
+    } else if (nm == "sizes") {
+        const int64_t nl = p->dm.n_loc[r.rank], ml = p->dm.m_loc[r.rank];
+        iv = {r.P, r.rank, p->n, p->m, p->n + p->m, nl, ml, nl + ml, r.nsub, r.nT, r.kt, p->kp.kmax, p->ac.kmax, p->ab.kmax};
+    } else if (nm == "dofs") I(p->dm.dofs(r.rank));
+    else if (nm == "node_rank") I(p->ts.node_rank);
+    else if (nm == "T") I(p->ts.T);
+    else if (nm == "fsub_Lp") I(r.Fsub.Lp);
+    else if (nm == "fsub_Li") I(r.Fsub.Li);
+    else if (nm == "fsub_Lx") Dv(r.Fsub.Lx);
+    else if (nm == "fsub_D") Dv(r.Fsub.D);
+    else if (nm == "fsub_perm") I(r.Fsub.perm);
+    else if (nm == "fsub_parent") I(r.Fsub.parent);
+    else if (nm == "fsub_key") I(r.key);
+    else if (nm == "extra_ptr" || nm == "extra_col" || nm == "extra_key" || nm == "extra_val") {
+        std::vector<int64_t> ptr{0}, col, key;
+        std::vector<double> val;
+        for (const auto &e : r.extra) {
+            for (const BwdExtra &x : e) col.push_back(x.col), key.push_back(x.key), val.push_back(x.val);
+            ptr.push_back((int64_t)col.size());
+        }
+        if (nm == "extra_ptr") iv = ptr;
+        else if (nm == "extra_col") iv = col;
+        else if (nm == "extra_key") iv = key;
+        else dv = val, isd = true;
+    } else if (nm == "tf_ptr") I(r.tf_ptr);
+    else if (nm == "tf_col") I(r.tf_col);
+    else if (nm == "tf_val") Dv(r.tf_val);
+    else if (nm == "tf_src") I(r.tf_src);
+    else if (nm == "tb_ptr") I(r.tb_ptr);
+    else if (nm == "tb_col") I(r.tb_col);
+    else if (nm == "tb_val") Dv(r.tb_val);
+    else if (nm == "DT") Dv(r.DT);
+    else if (nm == "tlev_ptr") I(r.tlev_ptr);
+    else if (nm == "tlev_rows") I(r.tlev_rows);
+    else if (nm == "tsend") I(r.tsend);
+    else if (nm == "tdof") I(r.tdof);
+    else throw Error(CPK_ERR_ARGS, "unknown plan array " + nm);
+    *count = isd ? (int64_t)dv.size() : (int64_t)iv.size();
+    if (out) {
+        if (isd) std::memcpy(out, dv.data(), dv.size() * sizeof(double));
+        else std::memcpy(out, iv.data(), iv.size() * sizeof(int64_t));
+    }
     API_END
 }
 

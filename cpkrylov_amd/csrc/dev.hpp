@@ -102,7 +102,14 @@ struct DFactor {
                perm.bytes() + blk_lvl.bytes() + lvl_row.bytes() + meta.bytes();
     }
 };
-void make_dfactor(const Factor &f, const Schedule &s, DFactor &d);
+// a backward-sweep entry of row q referring to a row outside the factor (col >= N)
+struct BwdExtra {
+    int32_t col;
+    int64_t key;
+    double val;
+};
+void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vector<int64_t> *key = nullptr,
+                  const std::vector<std::vector<BwdExtra>> *extra = nullptr);
 size_t sweep_lds_bytes(int R, int CAP);
 // Sweep configuration: rows and entries staged per block, threads per block.
 // CPK_SWEEP="rows,cap,threads" overrides the default.
@@ -140,7 +147,8 @@ void launch_set_concat(Ctx &c, double *dst, const double *a, int64_t na, int64_t
 struct Analysis {
     int64_t n = 0, m = 0, N = 0;
     HCsr Kp;
-    Factor F;  // relabelled to the schedule order
+    Factor F0;  // the factor as exported: P'*Kp*P = L*D*L' in pivot order (the reference's view)
+    Factor F;   // F0 relabelled to the schedule order (S.order[q] = F0 index of row q)
     Schedule S;
     int ordering = 0;
     double seconds = 0;
@@ -152,7 +160,7 @@ struct Precond {
     Ctx *ctx = nullptr;
     int64_t n = 0, m = 0, N = 0;
     HCsr Kp;             // host copy (divide, export)
-    Factor F;            // relabelled factor (host copy for export)
+    Factor F;            // exported factor (pivot order, pre-relabel); the device copy sums in its order
     Schedule S;
     int ordering = 0;
     DMat dKp;

@@ -46,16 +46,28 @@ void make_dmat(const HCsr &a, DMat &d) {
 }
 
 // ---- factor layout ---------------------------------------------------------------------------
-void make_dfactor(const Factor &f, const Schedule &s, DFactor &d) {
+// Row entries are stored in the accumulation order of the reference solve on the factor the
+// caller exports: forward rows by ascending key of the column, backward rows (columns of L)
+// by descending key of the row.  key[q] is the pre-relabel index of relabelled row q (so a
+// relabelled factor still sums in the exported factor's order); extra[q] are backward entries
+// of row q that refer to rows outside this factor (distributed separators).
+void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vector<int64_t> *key,
+                  const std::vector<std::vector<BwdExtra>> *extra) {
     const int64_t N = f.N;
+    auto K = [&](int64_t q) { return key ? (*key)[q] : q; };
+    int64_t nextra = 0;
+    if (extra)
+        for (const auto &e : *extra) nextra += (int64_t)e.size();
     d.N = N;
-    d.nnz = (int64_t)f.Li.size();
-    // forward rows: transpose of the CSC (columns ascend, so rows come out with ascending columns)
+    d.nnz = (int64_t)f.Li.size() + nextra;
+    if (d.nnz > (int64_t)INT32_MAX) throw Error(CPK_ERR_UNSUPPORTED, "factor has more than 2^31 entries");
+    // forward rows: transpose of the CSC, then each row ordered by the key of its columns
     std::vector<uint32_t> fptr(N + 1, 0);
     for (int32_t i : f.Li) fptr[i + 1]++;
     for (int64_t i = 0; i < N; i++) fptr[i + 1] += fptr[i];
-    std::vector<int32_t> fcol(d.nnz);
-    std::vector<double> fval(d.nnz);
+    const int64_t nf = (int64_t)f.Li.size();
+    std::vector<int32_t> fcol(nf);
+    std::vector<double> fval(nf);
     {
         std::vector<uint32_t> nx(fptr.begin(), fptr.end() - 1);
         for (int64_t j = 0; j < N; j++)
@@ -64,15 +76,32 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d) {
                 fcol[q] = (int32_t)j;
                 fval[q] = f.Lx[p];
             }
+        if (key) {
+            std::vector<std::pair<int64_t, std::pair<int32_t, double>>> row;
+            for (int64_t i = 0; i < N; i++) {
+                row.clear();
+                for (uint32_t q = fptr[i]; q < fptr[i + 1]; q++) row.push_back({K(fcol[q]), {fcol[q], fval[q]}});
+                std::sort(row.begin(), row.end(), [](auto &x, auto &y) { return x.first < y.first; });
+                for (size_t t = 0; t < row.size(); t++) fcol[fptr[i] + t] = row[t].second.first, fval[fptr[i] + t] = row[t].second.second;
+            }
+        }
     }
-    // backward rows: the CSC columns with row indices in descending order
-    std::vector<uint32_t> bptr(N + 1);
+    // backward rows: L's columns (plus extra entries), keys descending
+    std::vector<uint32_t> bptr(N + 1, 0);
+    for (int64_t j = 0; j < N; j++)
+        bptr[j + 1] = bptr[j] + (uint32_t)(f.Lp[j + 1] - f.Lp[j]) + (uint32_t)(extra ? (*extra)[j].size() : 0);
     std::vector<int32_t> bcol(d.nnz);
     std::vector<double> bval(d.nnz);
-    for (int64_t j = 0; j <= N; j++) bptr[j] = (uint32_t)f.Lp[j];
-    for (int64_t j = 0; j < N; j++) {
-        int64_t a = f.Lp[j], b = f.Lp[j + 1];
-        for (int64_t p = a; p < b; p++) bcol[a + (b - 1 - p)] = f.Li[p], bval[a + (b - 1 - p)] = f.Lx[p];
+    {
+        std::vector<std::pair<int64_t, std::pair<int32_t, double>>> row;
+        for (int64_t j = 0; j < N; j++) {
+            row.clear();
+            for (int64_t p = f.Lp[j]; p < f.Lp[j + 1]; p++) row.push_back({K(f.Li[p]), {f.Li[p], f.Lx[p]}});
+            if (extra)
+                for (const BwdExtra &e : (*extra)[j]) row.push_back({e.key, {e.col, e.val}});
+            std::sort(row.begin(), row.end(), [](auto &x, auto &y) { return x.first > y.first; });
+            for (size_t t = 0; t < row.size(); t++) bcol[bptr[j] + t] = row[t].second.first, bval[bptr[j] + t] = row[t].second.second;
+        }
     }
     d.fptr.upload(fptr);
     d.fcol.upload(fcol);

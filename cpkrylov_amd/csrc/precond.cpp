@@ -47,6 +47,7 @@ Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22) {
     an.sweep = sweep_config();
     an.S = build_schedule(f0, an.sweep.rows[0], an.sweep.cap[0], an.sweep.rows[1], an.sweep.cap[1], an.sweep.sub0);
     an.F = relabel(f0, an.S);
+    an.F0 = std::move(f0);
     an.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return an;
 }
@@ -58,10 +59,14 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
     pc->n = an.n, pc->m = an.m, pc->N = an.N;
     pc->ordering = an.ordering;
     pc->Kp = std::move(an.Kp);
-    pc->F = std::move(an.F);
     pc->S = std::move(an.S);
     make_dmat(pc->Kp, pc->dKp);
-    make_dfactor(pc->F, pc->S, pc->dF);
+    {
+        const std::vector<int64_t> key(pc->S.order.begin(), pc->S.order.end());
+        make_dfactor(an.F, pc->S, pc->dF, &key);
+    }
+    an.F = Factor();
+    pc->F = std::move(an.F0);
     for (int i = 0; i < 2; i++)
         pc->dF.sweep_rows[i] = an.sweep.rows[i], pc->dF.sweep_cap[i] = an.sweep.cap[i],
         pc->dF.sweep_threads[i] = an.sweep.threads[i];

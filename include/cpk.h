@@ -148,9 +148,27 @@ int cpk_analysis_get_info(cpk_analysis an, cpk_pc_info *info);
 int cpk_analysis_export(cpk_analysis an, int64_t *Lcolptr, int32_t *Lrowind, double *Lval, double *D,
                         int32_t *perm);
 /* Sweep schedule: round_ptr[nrounds+1] (blocks per round), blk_lvl[nblocks+1] (levels per
- * block, indices into lvl_row), lvl_row[nlevels+1] (first row of each level; last = N). */
+ * block, indices into lvl_row), lvl_row[nlevels+1] (first position of each level; last = N),
+ * order[N] (order[q] = exported-factor row solved at schedule position q).  Each row sums its
+ * entries in the exported factor's order: forward by ascending column, backward by
+ * descending row -- the order of the reference's column-oriented solves. */
 int cpk_analysis_schedule(cpk_analysis an, int64_t *nlevels, int64_t *round_ptr, int64_t *blk_lvl,
-                          int64_t *lvl_row);
+                          int64_t *lvl_row, int32_t *order);
+
+/* ---- distributed plan (host-only) --------------------------------- */
+/* The row-block plan of rank `rank` out of `nranks` for the system the analysis was built on
+ * (A: n x n, C: m x m the Krylov operator's blocks).  Every rank computes the same global plan
+ * deterministically; a distributed cpk_pc_create builds exactly this.  Exposed for tests and
+ * inspection: cpk_plan_array(plan, name, &count, out) copies array `name` (values as double
+ * for *_val, fsub_Lx, fsub_D, extra_val, tf_val, tb_val, DT; every other array as int64) into
+ * out (NULL: count only).  Names: sizes [P, rank, n, m, N, n_loc, m_loc, N_loc, nsub, nT, kt,
+ * kp_kmax, ac_kmax, ab_kmax], dofs, node_rank, T, fsub_{Lp,Li,Lx,D,perm,parent,key},
+ * extra_{ptr,col,key,val}, tf_{ptr,col,val,src}, tb_{ptr,col,val}, DT, tlev_{ptr,rows},
+ * tsend, tdof, and {kp,ac,ab}_{ptr,col,val,send} for Kp, blkdiag(A,C) and [A B']. */
+typedef struct cpk_plan_s *cpk_plan;
+int cpk_analysis_plan(cpk_analysis an, cpk_mat A, cpk_mat C, int nranks, int rank, cpk_plan *out);
+int cpk_plan_array(cpk_plan plan, const char *name, int64_t *count, void *out);
+int cpk_plan_destroy(cpk_plan plan);
 
 /* ---- solvers --------------------------------------------------------------------------- */
 /* [x, y, stats, flag] = method(b, A, C, M, opts)   (kernels/cp*.m, e.g. cpminres.m:1).

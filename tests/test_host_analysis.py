@@ -28,7 +28,9 @@ SYSTEMS = _systems()
 
 
 def replay(an, x):
-    L, D, perm = an["L"], an["D"], an["perm"]
+    """Schedule position q solves exported-factor row order[q]; each row sums its entries in the
+    exported factor's order (forward: ascending column, backward: descending row)."""
+    L, D, perm, order = an["L"], an["D"], an["perm"], an["order"]
     rp, bl, lr = an["round_ptr"], an["blk_lvl"], an["lvl_row"]
     N = len(D)
     Lr = L.tocsr()
@@ -39,7 +41,8 @@ def replay(an, x):
     for r in range(len(rp) - 1):
         for b in range(rp[r], rp[r + 1]):
             for lv in range(bl[b], bl[b + 1]):
-                for k in range(lr[lv], lr[lv + 1]):
+                for q in range(lr[lv], lr[lv + 1]):
+                    k = order[q]
                     acc = x[perm[k]]
                     for e in range(Lr.indptr[k], Lr.indptr[k + 1]):
                         assert not np.isnan(w[Lr.indices[e]]), "forward dependency not ready"
@@ -50,7 +53,8 @@ def replay(an, x):
     for r in range(len(rp) - 2, -1, -1):
         for b in range(rp[r], rp[r + 1]):
             for lv in range(bl[b + 1] - 1, bl[b] - 1, -1):
-                for k in range(lr[lv], lr[lv + 1]):
+                for q in range(lr[lv], lr[lv + 1]):
+                    k = order[q]
                     acc = w[k] / D[k]
                     for e in range(Lc.indptr[k + 1] - 1, Lc.indptr[k] - 1, -1):
                         assert done[Lc.indices[e]], "backward dependency not ready"
