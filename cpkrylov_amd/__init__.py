@@ -4,7 +4,7 @@ Drop-in for the hot path of optimizers/cpkrylov: reg_cpkrylov + cp{cg,cglanczos,
 symmlq,gmres,dqgmres} + the opLDL2 preconditioner operator.  See DESIGN.md.
 """
 from ._lib import CpkError, IndefiniteError, LIB_PATH  # noqa: F401  (raises if libcpk.so is missing)
-from .api import (Context, Matrix, SymGivens, analyze, dist_plan, cpcg, cpcglanczos, cpdqgmres, cpgmres,  # noqa: F401
+from .api import (Context, Matrix, SimGroup, SymGivens, analyze, dist_plan, cpcg, cpcglanczos, cpdqgmres, cpgmres,  # noqa: F401
                   cpminres, cpsymmlq, default_context, get_unique_id, opLDL2, reg_cpkrylov)
 
 __all__ = ["reg_cpkrylov", "cpcg", "cpcglanczos", "cpminres", "cpsymmlq", "cpgmres", "cpdqgmres", "opLDL2",

@@ -34,15 +34,18 @@ def _dptr(a):
 class Context:
     """One GPU, one HIP stream (and an RCCL communicator when nranks > 1)."""
 
-    def __init__(self, device=None, rank=0, nranks=1, unique_id=None):
+    def __init__(self, device=None, rank=0, nranks=1, unique_id=None, simgroup=None):
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         h = C.c_void_p()
-        uid = None
-        if unique_id is not None:
-            buf = (C.c_ubyte * 128).from_buffer_copy(bytes(unique_id))
-            uid = C.cast(buf, _P(C.c_ubyte))
-        check(lib.cpk_ctx_create(device, rank, nranks, uid, C.byref(h)))
+        if simgroup is not None:  # ranks as threads on one GPU (tests), see cpk_ctx_create_sim
+            check(lib.cpk_ctx_create_sim(device, simgroup.h, rank, nranks, C.byref(h)))
+        else:
+            uid = None
+            if unique_id is not None:
+                buf = (C.c_ubyte * 128).from_buffer_copy(bytes(unique_id))
+                uid = C.cast(buf, _P(C.c_ubyte))
+            check(lib.cpk_ctx_create(device, rank, nranks, uid, C.byref(h)))
         self.h = h
         self.device, self.rank, self.nranks = device, rank, nranks
 
@@ -59,6 +62,20 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+class SimGroup:
+    """A group of `nranks` simulated ranks sharing one GPU (one thread per rank)."""
+
+    def __init__(self, nranks):
+        h = C.c_void_p()
+        check(lib.cpk_simgroup_create(int(nranks), C.byref(h)))
+        self.h, self.nranks = h, nranks
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib.cpk_simgroup_destroy(self.h)
+            self.h = None
 
 
 _default_ctx = None
@@ -195,6 +212,14 @@ class opLDL2:
             X[:, i] = self * e
             e[i] = 0
         return X
+
+    def local_dofs(self):
+        """Global indices of this rank's local vector entries ([x-part; y-part]) and n_loc."""
+        nl, ml = C.c_int64(), C.c_int64()
+        check(lib.cpk_pc_local_dofs(self.h, C.byref(nl), C.byref(ml), None))
+        d = np.empty(nl.value + ml.value, np.int32)
+        check(lib.cpk_pc_local_dofs(self.h, C.byref(nl), C.byref(ml), d.ctypes.data_as(_P(C.c_int32))))
+        return d, nl.value
 
     def export_factors(self):
         """(L (CSC, strict lower), D, perm) with P'*Kp*P = L*D*L', perm[k] = original index."""

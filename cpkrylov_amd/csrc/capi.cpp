@@ -20,6 +20,14 @@ using namespace cpk;
 
 struct cpk_ctx_s {
     Ctx c;
+    std::unique_ptr<Comm> comm;
+};
+
+struct cpk_simgroup_s {
+    SimGroup *g = nullptr;
+    ~cpk_simgroup_s() {
+        if (g) simgroup_destroy(g);
+    }
 };
 
 struct cpk_mat_s {
@@ -35,6 +43,42 @@ struct cpk_mat_s {
             make_dmat(h, *d);
         }
         return *d;
+    }
+    // distributed rows, keyed by the preconditioner whose dof map they follow
+    std::map<std::pair<uint64_t, const void *>, std::unique_ptr<DMat>> dac;
+    std::map<const void *, std::unique_ptr<DMat>> dax, dbtx;
+    const DMat &krylov_op(cpk_mat_s *C, const Precond &M) {
+        if (!M.dist) return blkdiag_with(C);
+        auto key = std::make_pair(C->gen, (const void *)&M);
+        auto it = dac.find(key);
+        if (it == dac.end()) {
+            auto m = std::make_unique<DMat>();
+            make_dist_dmat(dist_csr(blkdiag(h, C->h), *M.dofmap, ctx->c.rank, false), ctx->c.nranks, *m);
+            it = dac.emplace(key, std::move(m)).first;
+        }
+        return *it->second;
+    }
+    // shift rows of a distributed preconditioner: A*xy0(1:n) and B'*xy0(n+1:N), x-part rows
+    std::pair<const DMat *, const DMat *> shift_ops(const Precond &M) {
+        auto it = dax.find(&M);
+        if (it == dax.end()) {
+            const int64_t n = M.gn, N = M.gN;
+            HCsr a = h, bt;
+            a.ncols = N;
+            bt.nrows = n, bt.ncols = N;
+            bt.ptr.assign(n + 1, 0);
+            for (int64_t i = 0; i < n; i++) {
+                for (int64_t q = M.Kp.ptr[i]; q < M.Kp.ptr[i + 1]; q++)
+                    if (M.Kp.ind[q] >= n) bt.ind.push_back(M.Kp.ind[q]), bt.val.push_back(M.Kp.val[q]);
+                bt.ptr[i + 1] = (int64_t)bt.ind.size();
+            }
+            auto ma = std::make_unique<DMat>(), mb = std::make_unique<DMat>();
+            make_dist_dmat(dist_csr(a, *M.dofmap, ctx->c.rank, true), ctx->c.nranks, *ma);
+            make_dist_dmat(dist_csr(bt, *M.dofmap, ctx->c.rank, true), ctx->c.nranks, *mb);
+            it = dax.emplace(&M, std::move(ma)).first;
+            dbtx[&M] = std::move(mb);
+        }
+        return {it->second.get(), dbtx[&M].get()};
     }
     const DMat &blkdiag_with(cpk_mat_s *C) {
         if (!ctx) throw Error(CPK_ERR_ARGS, "host-only matrix (created with ctx == NULL) used on the device");
@@ -95,6 +139,30 @@ static void h2d(DBuf<T> &d, const T *h, size_t n) {
     if (n) CPK_HIP(hipMemcpy(d.p, h, n * sizeof(T), hipMemcpyHostToDevice));
 }
 
+// ---- distributed host vectors: global on every rank <-> local slices on the device ----------
+static void scatter_global(const Precond &p, const double *h_glob, int64_t len_local, DBuf<double> &d) {
+    const std::vector<int32_t> dofs = p.dofmap->dofs(p.ctx->rank);
+    std::vector<double> loc((size_t)len_local);
+    for (int64_t i = 0; i < len_local; i++) loc[i] = h_glob[dofs[i]];
+    d.alloc((size_t)std::max<int64_t>(len_local, 1));
+    if (len_local) CPK_HIP(hipMemcpy(d.p, loc.data(), len_local * sizeof(double), hipMemcpyHostToDevice));
+}
+
+static void gather_global(Ctx &c, const Precond &p, const double *d_loc, double *h_glob) {
+    const DofMap &dm = *p.dofmap;
+    int64_t mx = 1;
+    for (int r = 0; r < dm.P; r++) mx = std::max<int64_t>(mx, dm.n_loc[r] + dm.m_loc[r]);
+    DBuf<double> snd, rcv;
+    snd.alloc((size_t)mx), rcv.alloc((size_t)(mx * dm.P));
+    CPK_HIP(hipMemsetAsync(snd.p, 0, snd.bytes(), c.stream));
+    if (p.N) CPK_HIP(hipMemcpyAsync(snd.p, d_loc, p.N * sizeof(double), hipMemcpyDeviceToDevice, c.stream));
+    c.comm->allgather(snd.p, rcv.p, (size_t)mx, c.stream);
+    std::vector<double> h((size_t)(mx * dm.P));
+    CPK_HIP(hipMemcpyAsync(h.data(), rcv.p, rcv.bytes(), hipMemcpyDeviceToHost, c.stream));
+    CPK_HIP(hipStreamSynchronize(c.stream));
+    for (int64_t g = 0; g < dm.N; g++) h_glob[g] = h[(size_t)dm.owner[g] * mx + dm.lidx[g]];
+}
+
 extern "C" {
 
 const char *cpk_last_error(void) { return g_err.c_str(); }
@@ -103,16 +171,11 @@ int cpk_abi_version(void) { return CPK_ABI_VERSION; }
 int cpk_get_unique_id(unsigned char id[128]) {
     API_BEGIN
     need(id != nullptr, "id is NULL");
-    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
-    ncclUniqueId u;
-    if (ncclGetUniqueId(&u) != ncclSuccess) throw Error(CPK_ERR_RCCL, "ncclGetUniqueId failed");
-    std::memcpy(id, &u, 128);
+    rccl_unique_id(id);
     API_END
 }
 
-int cpk_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id, cpk_ctx *out) {
-    API_BEGIN
-    need(out != nullptr, "out is NULL");
+static std::unique_ptr<cpk_ctx_s> ctx_base(int device, int rank, int nranks) {
     need(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
     auto ctx = std::make_unique<cpk_ctx_s>();
     Ctx &c = ctx->c;
@@ -123,14 +186,44 @@ int cpk_ctx_create(int device, int rank, int nranks, const unsigned char *unique
     CPK_HIP(hipEventCreate(&c.ev0));
     CPK_HIP(hipEventCreate(&c.ev1));
     c.ensure_partials(4096);
+    c.red.alloc(64);
+    return ctx;
+}
+
+int cpk_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id, cpk_ctx *out) {
+    API_BEGIN
+    need(out != nullptr, "out is NULL");
+    auto ctx = ctx_base(device, rank, nranks);
     if (nranks > 1) {
         need(unique_id != nullptr, "unique_id required when nranks > 1");
-        ncclUniqueId u;
-        std::memcpy(&u, unique_id, 128);
-        ncclComm_t comm;
-        if (ncclCommInitRank(&comm, nranks, u, rank) != ncclSuccess) throw Error(CPK_ERR_RCCL, "ncclCommInitRank failed");
-        c.comm = comm;
+        ctx->comm.reset(make_rccl_comm(nranks, rank, unique_id));
+        ctx->c.comm = ctx->comm.get();
     }
+    *out = ctx.release();
+    API_END
+}
+
+int cpk_simgroup_create(int nranks, cpk_simgroup *out) {
+    API_BEGIN
+    need(out && nranks >= 1, "bad argument");
+    auto g = std::make_unique<cpk_simgroup_s>();
+    g->g = simgroup_create(nranks);
+    *out = g.release();
+    API_END
+}
+
+int cpk_simgroup_destroy(cpk_simgroup g) {
+    API_BEGIN
+    delete g;
+    API_END
+}
+
+int cpk_ctx_create_sim(int device, cpk_simgroup group, int rank, int nranks, cpk_ctx *out) {
+    API_BEGIN
+    need(out && group, "NULL argument");
+    auto ctx = ctx_base(device, rank, nranks);
+    ctx->comm.reset(make_sim_comm(group->g, rank));
+    ctx->c.comm = ctx->comm.get();
     *out = ctx.release();
     API_END
 }
@@ -140,9 +233,11 @@ int cpk_ctx_destroy(cpk_ctx ctx) {
     if (!ctx) return CPK_OK;
     Ctx &c = ctx->c;
     (void)hipStreamSynchronize(c.stream);
-    if (c.comm) ncclCommDestroy((ncclComm_t)c.comm);
+    c.comm = nullptr;
+    ctx->comm.reset();
     c.partials.release();
     c.counter.release();
+    c.red.release();
     (void)hipEventDestroy(c.ev0);
     (void)hipEventDestroy(c.ev1);
     (void)hipStreamDestroy(c.stream);
@@ -206,7 +301,8 @@ int cpk_pc_create(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptim
     need(ctx && A11 && B && C22 && out, "opLDL2: Invalid number of arguments.");
     auto pc = std::make_unique<cpk_pc_s>();
     pc->ctx = ctx;
-    pc->p.reset(precond_create(ctx->c, A11->h, B->h, C22->h));
+    if (ctx->c.dist()) pc->p.reset(precond_create_dist(ctx->c, analyze(A11->h, B->h, C22->h)));
+    else pc->p.reset(precond_create(ctx->c, A11->h, B->h, C22->h));
     if (ptime) *ptime = pc->p->ptime;
     *out = pc.release();
     API_END
@@ -252,11 +348,16 @@ int cpk_pc_apply(cpk_pc M, const double *x, double *y) {
     Precond &p = *M->p;
     Ctx &c = M->ctx->c;
     DBuf<double> dx, dy;
-    h2d(dx, x, (size_t)p.N);
-    dy.alloc((size_t)p.N);
+    if (p.dist) scatter_global(p, x, p.N, dx);
+    else h2d(dx, x, (size_t)p.N);
+    dy.alloc((size_t)std::max<int64_t>(p.N, 1));
     p.apply(dx.p, p.N, dy.p, nullptr);
-    CPK_HIP(hipMemcpyAsync(y, dy.p, p.N * sizeof(double), hipMemcpyDeviceToHost, c.stream));
-    CPK_HIP(hipStreamSynchronize(c.stream));
+    if (p.dist) {
+        gather_global(c, p, dy.p, y);
+    } else {
+        CPK_HIP(hipMemcpyAsync(y, dy.p, p.N * sizeof(double), hipMemcpyDeviceToHost, c.stream));
+        CPK_HIP(hipStreamSynchronize(c.stream));
+    }
     API_END
 }
 
@@ -273,11 +374,16 @@ int cpk_pc_divide(cpk_pc M, const double *b, double *x) {
     Precond &p = *M->p;
     Ctx &c = M->ctx->c;
     DBuf<double> db, dx;
-    h2d(db, b, (size_t)p.N);
-    dx.alloc((size_t)p.N);
+    if (p.dist) scatter_global(p, b, p.N, db);
+    else h2d(db, b, (size_t)p.N);
+    dx.alloc((size_t)std::max<int64_t>(p.N, 1));
     launch_spmv(c, p.dKp, db.p, dx.p, nullptr);
-    CPK_HIP(hipMemcpyAsync(x, dx.p, p.N * sizeof(double), hipMemcpyDeviceToHost, c.stream));
-    CPK_HIP(hipStreamSynchronize(c.stream));
+    if (p.dist) {
+        gather_global(c, p, dx.p, x);
+    } else {
+        CPK_HIP(hipMemcpyAsync(x, dx.p, p.N * sizeof(double), hipMemcpyDeviceToHost, c.stream));
+        CPK_HIP(hipStreamSynchronize(c.stream));
+    }
     API_END
 }
 
@@ -285,7 +391,7 @@ int cpk_pc_get_info(cpk_pc M, cpk_pc_info *info) {
     API_BEGIN
     need(M && info, "NULL argument");
     const Precond &p = *M->p;
-    info->n = p.n, info->m = p.m, info->N = p.N;
+    info->n = p.gn, info->m = p.gm, info->N = p.gN;
     info->nnz_kp = p.Kp.nnz();
     info->nnz_l = (int64_t)p.F.Li.size();
     info->nblocks = (int64_t)p.S.blk_row.size() - 1;
@@ -311,15 +417,21 @@ int cpk_pc_export(cpk_pc M, int64_t *Lcolptr, int32_t *Lrowind, double *Lval, do
 static void check_method_dims(cpk_mat A, cpk_mat C, cpk_pc M) {
     need(A && C && M, "NULL argument");
     if (A->h.nrows != A->h.ncols || C->h.nrows != C->h.ncols) throw Error(CPK_ERR_DIM, "A and C must be square");
-    if (A->h.nrows != M->p->n || C->h.nrows != M->p->m) throw Error(CPK_ERR_DIM, "A, C and M dimensions disagree");
+    if (A->h.nrows != M->p->gn || C->h.nrows != M->p->gm) throw Error(CPK_ERR_DIM, "A, C and M dimensions disagree");
+}
+
+static void check_dist_method(const Ctx &c, int method) {
+    if (c.dist() && (method == CPK_GMRES || method == CPK_DQGMRES))
+        throw Error(CPK_ERR_UNSUPPORTED, "cpgmres/cpdqgmres are single-GPU in this version (DESIGN.md section 7)");
 }
 
 int cpk_method_solve_device(cpk_ctx ctx, int method, const double *d_b, cpk_mat A, cpk_mat C, cpk_pc M,
                             const cpk_opts *opts, double *d_xy, cpk_stats *stats) {
     API_BEGIN
-    need(ctx && d_xy && (d_b || !A->h.nrows), "NULL argument");
+    need(ctx && A && M && (d_xy || !M->p->N) && (d_b || !M->p->n), "NULL argument");
     check_method_dims(A, C, M);
-    const DMat &AC = A->blkdiag_with(C);
+    check_dist_method(ctx->c, method);
+    const DMat &AC = A->krylov_op(C, *M->p);
     method_solve_device(ctx->c, method, d_b, AC, *M->p, opts, d_xy, stats);
     API_END
 }
@@ -327,29 +439,55 @@ int cpk_method_solve_device(cpk_ctx ctx, int method, const double *d_b, cpk_mat 
 int cpk_method_solve(cpk_ctx ctx, int method, const double *b, cpk_mat A, cpk_mat C, cpk_pc M, const cpk_opts *opts,
                      double *x, double *y, cpk_stats *stats) {
     API_BEGIN
-    need(ctx && b && x && (y || !C->h.nrows), "NULL argument");
+    need(ctx && b && x && A && C && M && (y || !C->h.nrows), "NULL argument");
     check_method_dims(A, C, M);
+    check_dist_method(ctx->c, method);
     Ctx &c = ctx->c;
-    const int64_t n = M->p->n, m = M->p->m, N = n + m;
-    const DMat &AC = A->blkdiag_with(C);
+    Precond &p = *M->p;
+    const int64_t n = p.n, m = p.m, N = n + m;
+    const DMat &AC = A->krylov_op(C, p);
     DBuf<double> db, dxy;
-    h2d(db, b, (size_t)n);
-    dxy.alloc((size_t)N);
+    if (p.dist) scatter_global(p, b, n, db);
+    else h2d(db, b, (size_t)n);
+    dxy.alloc((size_t)std::max<int64_t>(N, 1));
     auto t0 = std::chrono::steady_clock::now();
-    method_solve_device(c, method, db.p, AC, *M->p, opts, dxy.p, stats);
-    CPK_HIP(hipMemcpy(x, dxy.p, n * sizeof(double), hipMemcpyDeviceToHost));
-    if (m) CPK_HIP(hipMemcpy(y, dxy.p + n, m * sizeof(double), hipMemcpyDeviceToHost));
+    method_solve_device(c, method, db.p, AC, p, opts, dxy.p, stats);
+    if (p.dist) {
+        std::vector<double> g((size_t)p.gN);
+        gather_global(c, p, dxy.p, g.data());
+        std::memcpy(x, g.data(), p.gn * sizeof(double));
+        if (p.gm) std::memcpy(y, g.data() + p.gn, p.gm * sizeof(double));
+    } else {
+        CPK_HIP(hipMemcpy(x, dxy.p, n * sizeof(double), hipMemcpyDeviceToHost));
+        if (m) CPK_HIP(hipMemcpy(y, dxy.p + n, m * sizeof(double), hipMemcpyDeviceToHost));
+    }
     if (stats) stats->stime = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     API_END
+}
+
+// the shift's two products: 1 GPU reads rows < n of blkdiag(A, C) and of Kp (columns >= n);
+// distributed mode has dedicated x-part row slices of [A 0] and [0 B']
+struct ShiftOps {
+    const DMat *A, *Bt;
+    int64_t bt_colmin;
+};
+static ShiftOps shift_ops(cpk_mat A, cpk_mat C, Precond &p) {
+    if (p.dist) {
+        auto pr = A->shift_ops(p);
+        return {pr.first, pr.second, 0};
+    }
+    return {&A->blkdiag_with(C), &p.dKp, p.n};
 }
 
 int cpk_reg_solve_device(cpk_ctx ctx, int method, const double *d_b, cpk_mat A, cpk_mat B, cpk_mat C, cpk_pc M,
                          const cpk_opts *opts, double *d_x, cpk_stats *stats) {
     API_BEGIN
-    need(ctx && d_b && d_x && B, "NULL argument");
+    need(ctx && A && M && B && ((d_b && d_x) || !M->p->N), "NULL argument");
     check_method_dims(A, C, M);
-    const DMat &AC = A->blkdiag_with(C);
-    reg_solve_device(ctx->c, method, d_b, AC, M->p->dKp, *M->p, opts, d_x, stats);
+    check_dist_method(ctx->c, method);
+    const DMat &AC = A->krylov_op(C, *M->p);
+    const ShiftOps so = shift_ops(A, C, *M->p);
+    reg_solve_device(ctx->c, method, d_b, AC, *so.A, *so.Bt, so.bt_colmin, *M->p, opts, d_x, stats);
     if (stats) stats->ptime = M->p->ptime;
     API_END
 }
@@ -357,10 +495,10 @@ int cpk_reg_solve_device(cpk_ctx ctx, int method, const double *d_b, cpk_mat A, 
 int cpk_reg_shift_device(cpk_ctx ctx, const double *d_b, cpk_mat A, cpk_mat B, cpk_mat C, cpk_pc M, double *d_b1,
                          double *d_xy0, int *shifted) {
     API_BEGIN
-    need(ctx && d_b && d_b1 && d_xy0 && B, "NULL argument");
+    need(ctx && A && M && B && ((d_b && d_b1 && d_xy0) || !M->p->N), "NULL argument");
     check_method_dims(A, C, M);
-    const DMat &AC = A->blkdiag_with(C);
-    int s = reg_shift_device(ctx->c, d_b, AC, M->p->dKp, *M->p, d_b1, d_xy0);
+    const ShiftOps so = shift_ops(A, C, *M->p);
+    int s = reg_shift_device(ctx->c, d_b, *so.A, *so.Bt, so.bt_colmin, *M->p, d_b1, d_xy0);
     if (shifted) *shifted = s;
     API_END
 }
@@ -369,7 +507,24 @@ int cpk_profile_kernels(cpk_ctx ctx, cpk_mat A, cpk_mat C, cpk_pc M, int reps, c
     API_BEGIN
     need(ctx && out, "NULL argument");
     check_method_dims(A, C, M);
-    profile_kernels(ctx->c, A->blkdiag_with(C), *M->p, reps, out);
+    profile_kernels(ctx->c, A->krylov_op(C, *M->p), *M->p, reps, out);
+    API_END
+}
+
+int cpk_pc_local_dofs(cpk_pc M, int64_t *n_loc, int64_t *m_loc, int32_t *dofs) {
+    API_BEGIN
+    need(M, "NULL argument");
+    const Precond &p = *M->p;
+    if (n_loc) *n_loc = p.n;
+    if (m_loc) *m_loc = p.m;
+    if (dofs) {
+        if (p.dist) {
+            const std::vector<int32_t> d = p.dofmap->dofs(M->ctx->c.rank);
+            std::memcpy(dofs, d.data(), d.size() * sizeof(int32_t));
+        } else {
+            for (int64_t i = 0; i < p.N; i++) dofs[i] = (int32_t)i;
+        }
+    }
     API_END
 }
 
@@ -382,18 +537,24 @@ int cpk_reg_solve(cpk_ctx ctx, int method, const double *b, cpk_mat A, cpk_mat B
     // M = opLDL2(G, B, -C)   (reg_cpkrylov.m:128-132)
     HCsr negC = C->h;
     for (auto &v : negC.val) v = -v;
+    check_dist_method(c, method);
     auto pc = std::make_unique<cpk_pc_s>();
     pc->ctx = ctx;
-    pc->p.reset(precond_create(c, G->h, B->h, negC));
-    apply_props(*pc->p, opts);  // reg_cpkrylov.m:135-148
+    if (c.dist()) pc->p.reset(precond_create_dist(c, analyze(G->h, B->h, negC)));
+    else pc->p.reset(precond_create(c, G->h, B->h, negC));
+    Precond &p = *pc->p;
+    apply_props(p, opts);  // reg_cpkrylov.m:135-148
     check_method_dims(A, C, pc.get());
-    const int64_t N = pc->p->N;
-    const DMat &AC = A->blkdiag_with(C);
+    const int64_t N = p.N;
+    const DMat &AC = A->krylov_op(C, p);
+    const ShiftOps so = shift_ops(A, C, p);
     DBuf<double> db, dx;
-    h2d(db, b, (size_t)N);
-    dx.alloc((size_t)N);
-    reg_solve_device(c, method, db.p, AC, pc->p->dKp, *pc->p, opts, dx.p, stats);
-    CPK_HIP(hipMemcpy(x, dx.p, N * sizeof(double), hipMemcpyDeviceToHost));
+    if (p.dist) scatter_global(p, b, N, db);
+    else h2d(db, b, (size_t)N);
+    dx.alloc((size_t)std::max<int64_t>(N, 1));
+    reg_solve_device(c, method, db.p, AC, *so.A, *so.Bt, so.bt_colmin, p, opts, dx.p, stats);
+    if (p.dist) gather_global(c, p, dx.p, x);
+    else CPK_HIP(hipMemcpy(x, dx.p, N * sizeof(double), hipMemcpyDeviceToHost));
     if (stats) stats->ptime = pc->p->ptime;
     if (M_out) *M_out = pc.release();
     API_END

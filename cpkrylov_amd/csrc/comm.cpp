@@ -1,0 +1,126 @@
+// comm.cpp -- collectives of the distributed solve.
+//
+// RcclComm: RCCL over xGMI, one process per GPU (production; graph-capturable).
+// SimComm:  P ranks as host threads of one process sharing one GPU, exchanging through a
+//           shared HBM buffer with host barriers.  It exists so the multi-rank device path
+//           can be exercised on a one-GPU box (RCCL refuses two ranks on one device); it is
+//           not capturable and not a performance path.
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "dev.hpp"
+
+namespace cpk {
+
+namespace {
+
+void nccl_check(ncclResult_t r, const char *what) {
+    if (r != ncclSuccess) throw Error(CPK_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+struct RcclComm : Comm {
+    ncclComm_t c = nullptr;
+    ~RcclComm() override {
+        if (c) ncclCommDestroy(c);
+    }
+    void allreduce_sum(double *buf, size_t n, hipStream_t s) override {
+        nccl_check(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c, s), "ncclAllReduce");
+    }
+    void allgather(const double *send, double *recv, size_t n, hipStream_t s) override {
+        nccl_check(ncclAllGather(send, recv, n, ncclDouble, c, s), "ncclAllGather");
+    }
+    bool capturable() const override {
+        const char *e = getenv("CPK_DIST_GRAPH");
+        return !e || atoi(e) != 0;
+    }
+};
+
+}  // namespace
+
+Comm *make_rccl_comm(int nranks, int rank, const unsigned char *uid) {
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId u;
+    std::memcpy(&u, uid, 128);
+    auto *rc = new RcclComm();
+    const ncclResult_t r = ncclCommInitRank(&rc->c, nranks, u, rank);
+    if (r != ncclSuccess) {
+        delete rc;
+        nccl_check(r, "ncclCommInitRank");
+    }
+    return rc;
+}
+
+void rccl_unique_id(unsigned char *uid) {
+    ncclUniqueId u;
+    nccl_check(ncclGetUniqueId(&u), "ncclGetUniqueId");
+    std::memcpy(uid, &u, 128);
+}
+
+// ---- simulated group --------------------------------------------------------------------------
+struct SimGroup {
+    int P;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    DBuf<double> shared;
+    static constexpr size_t kCap = size_t(16) << 20;  // doubles
+    explicit SimGroup(int p) : P(p) {}
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t g = gen;
+        if (++arrived == P) {
+            arrived = 0, gen++;
+            cv.notify_all();
+            return;
+        }
+        if (!cv.wait_for(lk, std::chrono::seconds(300), [&] { return gen != g; }))
+            throw Error(CPK_ERR_RCCL, "simulated collective: a rank did not arrive within 300 s");
+    }
+};
+
+namespace {
+struct SimComm : Comm {
+    SimGroup *g;
+    int rank;
+    SimComm(SimGroup *gg, int r) : g(gg), rank(r) {}
+    void check(size_t n) const {
+        if (n * (size_t)g->P > SimGroup::kCap) throw Error(CPK_ERR_UNSUPPORTED, "simulated collective too large");
+    }
+    void allreduce_sum(double *buf, size_t n, hipStream_t s) override {
+        check(n);
+        CPK_HIP(hipMemcpyAsync(g->shared.p + rank * n, buf, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+        CPK_HIP(hipStreamSynchronize(s));
+        g->barrier();
+        launch_sum_slots(s, g->shared.p, g->P, n, buf);
+        CPK_HIP(hipStreamSynchronize(s));
+        g->barrier();
+    }
+    void allgather(const double *send, double *recv, size_t n, hipStream_t s) override {
+        check(n);
+        if (n) CPK_HIP(hipMemcpyAsync(g->shared.p + rank * n, send, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+        CPK_HIP(hipStreamSynchronize(s));
+        g->barrier();
+        if (n) CPK_HIP(hipMemcpyAsync(recv, g->shared.p, n * g->P * sizeof(double), hipMemcpyDeviceToDevice, s));
+        CPK_HIP(hipStreamSynchronize(s));
+        g->barrier();
+    }
+    bool capturable() const override { return false; }
+};
+}  // namespace
+
+SimGroup *simgroup_create(int nranks) {
+    auto *g = new SimGroup(nranks);
+    g->shared.alloc(SimGroup::kCap);
+    return g;
+}
+void simgroup_destroy(SimGroup *g) { delete g; }
+Comm *make_sim_comm(SimGroup *g, int rank) { return new SimComm(g, rank); }
+
+}  // namespace cpk

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -55,14 +56,25 @@ struct DBuf {
     size_t bytes() const { return n * sizeof(T); }
 };
 
-// Execution context: one GPU, one stream, reduction workspace (and RCCL when nranks > 1).
+// Collectives of a distributed context, enqueued on the context stream.  RCCL over xGMI in
+// production; SimComm runs several ranks as threads sharing one GPU (tests on a 1-GPU box).
+struct Comm {
+    virtual ~Comm() = default;
+    virtual void allreduce_sum(double *buf, size_t n, hipStream_t s) = 0;
+    virtual void allgather(const double *send, double *recv, size_t n, hipStream_t s) = 0;
+    virtual bool capturable() const = 0;  // may be captured into a hipGraph
+};
+
+// Execution context: one GPU, one stream, reduction workspace (and a Comm when nranks > 1).
 struct Ctx {
     int device = 0, rank = 0, nranks = 1;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     DBuf<double> partials;   // per-workgroup partial sums of the grid reductions
     DBuf<unsigned> counter;  // arrival tickets
-    void *comm = nullptr;    // ncclComm_t
+    DBuf<double> red;        // distributed mode: local sums awaiting the allreduce
+    Comm *comm = nullptr;    // owned by the C-ABI context object
+    bool dist() const { return nranks > 1 && comm != nullptr; }
     void ensure_partials(size_t count);
 };
 
@@ -76,9 +88,18 @@ struct DMat {
     DBuf<double> val;
     DBuf<int32_t> blk;  // row-block boundaries [nblk + 1]
     bool is_diag = false;
+    // distributed rows (DistCsr): columns >= nloc read the allgathered halo buffer
+    int64_t nloc = -1, kmax = 0, nsend = 0;
+    DBuf<int32_t> send;         // local indices published to the other ranks
+    DBuf<double> sbuf, rbuf;    // halo payload [kmax], allgathered halo [nranks * kmax]
+    bool halo() const { return nloc >= 0; }
     size_t bytes() const { return ptr.bytes() + col.bytes() + val.bytes() + blk.bytes(); }
 };
 void make_dmat(const HCsr &a, DMat &d);
+struct DistCsr;
+void make_dist_dmat(const DistCsr &a, int nranks, DMat &d);
+// allgather the halo of x (local vector) into A.rbuf
+void launch_halo(Ctx &c, const DMat &A, const double *x);
 
 // HBM-resident factor + sweep schedule (rows in schedule order).
 struct DFactor {
@@ -142,6 +163,20 @@ void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
 // small vector helpers
 void launch_set_concat(Ctx &c, double *dst, const double *a, int64_t na, int64_t nb);  // dst = [a; 0]
 
+// ---- distributed mode (comm.cpp, kernels.hip) --------------------------------------------
+Comm *make_rccl_comm(int nranks, int rank, const unsigned char *uid);
+void rccl_unique_id(unsigned char *uid);
+struct SimGroup;
+SimGroup *simgroup_create(int nranks);
+void simgroup_destroy(SimGroup *g);
+Comm *make_sim_comm(SimGroup *g, int rank);
+void launch_sum_slots(hipStream_t s, const double *slots, int P, size_t n, double *out);
+struct DSep;
+// pack this rank's separator payload (w rows read by T, rank 0: +-x at the T dofs), allgather
+void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x, int64_t neg_from);
+// redundant separator solve into wT (= w + nsub); rank 0 writes (add: accumulates) y at the T dofs
+void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active);
+
 // ---- preconditioner (precond.cpp) --------------------------------------------------------
 // Host analysis of opLDL2's constructor: Kp assembly, ordering, LDL', sweep schedule.
 struct Analysis {
@@ -156,9 +191,22 @@ struct Analysis {
 };
 Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22);
 
+// The separator solve of a distributed preconditioner, device copy.
+struct DSep {
+    int64_t nT = 0, kt = 0, nlev = 0, nsend = 0, ntdof = 0;
+    DBuf<int32_t> tf_ptr, tf_col, tf_src, tb_ptr, tb_col, lev_ptr, lev_rows, send, tdof;
+    DBuf<double> tf_val, tb_val, DT, sbuf, rbuf;
+};
+struct DofMap;
+
 struct Precond {
     Ctx *ctx = nullptr;
-    int64_t n = 0, m = 0, N = 0;
+    int64_t n = 0, m = 0, N = 0;   // local sizes (= global ones on one GPU)
+    int64_t gn = 0, gm = 0, gN = 0;  // global sizes
+    bool dist = false;
+    int64_t nsub = 0;              // distributed: subtree rows of this rank (w holds nsub + nT)
+    DSep sep;
+    std::shared_ptr<DofMap> dofmap;
     HCsr Kp;             // host copy (divide, export)
     Factor F;            // exported factor (pivot order, pre-relabel); the device copy sums in its order
     Schedule S;
@@ -172,10 +220,13 @@ struct Precond {
     double ptime = 0;
     // y = M*x  (opLDL2.multiply); all pointers on the device, enqueued on ctx->stream
     void apply(const double *x, int64_t neg_from, double *y, const int *run);
+    void ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run, const int *act);
     // algorithmic HBM bytes of one apply
     double apply_bytes() const;
 };
 Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22);
 Precond *precond_create(Ctx &c, Analysis &&an);
+// distributed preconditioner of rank c.rank out of c.nranks
+Precond *precond_create_dist(Ctx &c, Analysis &&an);
 
 }  // namespace cpk

@@ -20,6 +20,8 @@ constexpr int kBlock = 256;  // threads per workgroup of the streaming kernels
 struct RedBuf {
     double *partials;   // [grid][NV]
     unsigned *counter;  // zero between launches (the last workgroup resets it)
+    double *defer = nullptr;  // distributed mode: the last workgroup stores the local sums here
+                              // instead of running the epilogue (it runs after the allreduce)
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -83,8 +85,11 @@ __device__ __forceinline__ bool grid_sum(double (&v)[NV], RedBuf rb, double (&to
 #pragma unroll
         for (int j = 0; j < NV; j++) tot[j] = acc[j];
         __hip_atomic_store(rb.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (rb.defer)
+#pragma unroll
+            for (int j = 0; j < NV; j++) rb.defer[j] = acc[j];
     }
-    return true;
+    return rb.defer == nullptr;
 }
 
 // Predicate shared by every solver-loop kernel: run only while the iteration is live.

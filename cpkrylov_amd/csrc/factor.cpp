@@ -81,7 +81,8 @@ Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int /*nthrea
     return f;
 }
 
-Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1, int64_t SUB0) {
+Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1, int64_t SUB0,
+                        const std::vector<int64_t> *extra_bwd) {
     if (SUB0 <= 0 || SUB0 > CAP0) SUB0 = CAP0;
     const int64_t N = f.N;
     Schedule s;
@@ -96,7 +97,7 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
         std::vector<int64_t> fl(N, 0);
         for (int32_t i : f.Li) fl[i]++;
         for (int64_t v = 0; v < N; v++) {
-            ent[v] = std::max(fl[v], f.Lp[v + 1] - f.Lp[v]);
+            ent[v] = std::max(fl[v], f.Lp[v + 1] - f.Lp[v] + (extra_bwd ? (*extra_bwd)[v] : 0));
             wt0[v] = std::max(u0, ent[v]);
             wt1[v] = std::max(u1, ent[v]);
         }

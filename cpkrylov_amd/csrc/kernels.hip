@@ -10,6 +10,7 @@
 
 #include "dev.hpp"
 #include "devutil.hpp"
+#include "dist.hpp"
 #include "spmv.hpp"
 
 namespace cpk {
@@ -36,7 +37,7 @@ void make_dmat(const HCsr &a, DMat &d) {
             r0 = r;
         }
     }
-    if (a.nrows > 0) blk.push_back((int32_t)a.nrows);
+    blk.push_back((int32_t)a.nrows);  // an empty matrix keeps one (empty) block: every launch has a grid
     d.nblk = (int64_t)blk.size() - 1;
     d.ptr.upload(ptr);
     d.col.upload(a.ind);
@@ -186,38 +187,180 @@ struct EpiResidNorm {
 
 static inline int grid_of(const DMat &A) { return (int)A.nblk; }
 
-void launch_spmv(Ctx &c, const DMat &A, const double *x, double *y, const int *run) {
-    if (!A.nblk) return;
-    EpiStore e{y, run};
-    hipLaunchKernelGGL(spmv_stream<EpiStore>, dim3(grid_of(A)), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
-                       A.val.p, A.blk.p, x, (int64_t)0, e);
+template <class Epi>
+static void spmv_launch(Ctx &c, const DMat &A, const double *x, int64_t col_min, const Epi &e) {
+    if (A.halo())
+        hipLaunchKernelGGL((spmv_stream<Epi, true>), dim3(grid_of(A)), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
+                           A.val.p, A.blk.p, x, col_min, e, (const double *)A.rbuf.p, A.nloc);
+    else
+        hipLaunchKernelGGL((spmv_stream<Epi, false>), dim3(grid_of(A)), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
+                           A.val.p, A.blk.p, x, col_min, e, (const double *)nullptr, (int64_t)0);
     CPK_HIP(hipGetLastError());
 }
 
-void launch_spmv_colmask(Ctx &c, const DMat &A, int64_t col_min, const double *x, double *y, const int *run) {
-    if (!A.nblk) return;
-    EpiStore e{y, run};
-    hipLaunchKernelGGL(spmv_stream<EpiStore>, dim3(grid_of(A)), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
-                       A.val.p, A.blk.p, x, col_min, e);
+// ---- distributed halo ----------------------------------------------------
+__global__ void gather_kernel(const double *__restrict__ x, const int32_t *__restrict__ idx, int64_t n,
+                              double *__restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = x[idx[i]];
+}
+
+static void launch_gather(Ctx &c, const double *x, const int32_t *idx, int64_t n, double *out) {
+    if (n <= 0) return;
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(256), 0, c.stream, x, idx, n, out);
     CPK_HIP(hipGetLastError());
+}
+
+void launch_halo(Ctx &c, const DMat &A, const double *x) {
+    if (!A.halo() || A.kmax == 0) return;
+    launch_gather(c, x, A.send.p, A.nsend, A.sbuf.p);
+    c.comm->allgather(A.sbuf.p, A.rbuf.p, (size_t)A.kmax, c.stream);
+}
+
+void make_dist_dmat(const DistCsr &a, int nranks, DMat &d) {
+    make_dmat(a.a, d);
+    d.nloc = a.nloc, d.kmax = a.kmax, d.nsend = (int64_t)a.send.size();
+    d.send.upload(a.send);
+    d.sbuf.alloc((size_t)std::max<int64_t>(a.kmax, 1));
+    d.rbuf.alloc((size_t)std::max<int64_t>(a.kmax * nranks, 1));
+    CPK_HIP(hipMemset(d.rbuf.p, 0, d.rbuf.bytes()));
+}
+
+__global__ void sum_slots_kernel(const double *__restrict__ slots, int P, int64_t n, double *__restrict__ out) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+        double s = slots[j];
+        for (int q = 1; q < P; q++) s += slots[(int64_t)q * n + j];
+        out[j] = s;
+    }
+}
+void launch_sum_slots(hipStream_t st, const double *slots, int P, size_t n, double *out) {
+    if (!n) return;
+    const int grid = (int)std::min<size_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(sum_slots_kernel, dim3(grid), dim3(256), 0, st, slots, P, (int64_t)n, out);
+    CPK_HIP(hipGetLastError());
+}
+
+void launch_spmv(Ctx &c, const DMat &A, const double *x, double *y, const int *run) {
+    launch_halo(c, A, x);
+    if (!A.nblk) return;
+    spmv_launch(c, A, x, 0, EpiStore{y, run});
+}
+
+void launch_spmv_colmask(Ctx &c, const DMat &A, int64_t col_min, const double *x, double *y, const int *run) {
+    launch_halo(c, A, x);
+    if (!A.nblk) return;
+    spmv_launch(c, A, x, col_min, EpiStore{y, run});
 }
 
 void launch_spmv_resid(Ctx &c, const DMat &A, const double *xin, int64_t neg_from, const double *y, double *r,
                        const int *run, const int *active) {
+    launch_halo(c, A, y);
     if (!A.nblk) return;
-    EpiResid e{xin, neg_from, r, run, active};
-    hipLaunchKernelGGL(spmv_stream<EpiResid>, dim3(grid_of(A)), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
-                       A.val.p, A.blk.p, y, (int64_t)0, e);
-    CPK_HIP(hipGetLastError());
+    spmv_launch(c, A, y, 0, EpiResid{xin, neg_from, r, run, active});
+}
+
+// the refinement predicate from the allreduced (|r|^2, |x|^2) (distributed mode)
+__global__ void resid_norm_fin_kernel(const double *tot, double tol, int *active_out, const int *run,
+                                      const int *active) {
+    if (threadIdx.x || blockIdx.x || skip(run, active)) return;
+    *active_out = (sqrt(tot[0]) >= tol * sqrt(tot[1])) ? 1 : 0;
 }
 
 void launch_spmv_resid_norm(Ctx &c, const DMat &A, const double *xin, int64_t neg_from, const double *y, double *r,
                             double tol, int *active_out, const int *run, const int *active) {
-    if (!A.nblk) return;
-    c.ensure_partials((size_t)A.nblk * 2);
-    EpiResidNorm e{xin, neg_from, r, tol, active_out, RedBuf{c.partials.p, c.counter.p}, run, active};
-    hipLaunchKernelGGL(spmv_stream<EpiResidNorm>, dim3(grid_of(A)), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
-                       A.val.p, A.blk.p, y, (int64_t)0, e);
+    launch_halo(c, A, y);
+    const bool dist = c.dist();
+    if (dist) CPK_HIP(hipMemsetAsync(c.red.p, 0, 2 * sizeof(double), c.stream));  // a rank with no rows adds 0
+    if (A.nblk) {
+        c.ensure_partials((size_t)A.nblk * 2);
+        EpiResidNorm e{xin, neg_from, r, tol, active_out, RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr},
+                       run, active};
+        spmv_launch(c, A, y, 0, e);
+    }
+    if (dist) {
+        c.comm->allreduce_sum(c.red.p, 2, c.stream);
+        hipLaunchKernelGGL(resid_norm_fin_kernel, dim3(1), dim3(64), 0, c.stream, (const double *)c.red.p, tol,
+                           active_out, run, active);
+        CPK_HIP(hipGetLastError());
+    }
+}
+
+// ---- separator solve of the distributed apply ----------------------------
+// One workgroup solves the (replicated) separator rows T: forward by levels from the
+// allgathered payload (subtree values of every rank + the T inputs published by rank 0), then
+// backward by levels in reverse, all out of LDS.  Each row subtracts its terms in the exported
+// factor's order, exactly as the single-GPU sweep does.  The results go to w[nsub + t] (read
+// by the local backward sweep as outside-block values) and, on rank 0, to the T dofs of y.
+__global__ __launch_bounds__(256) void tsolve_kernel(
+    int nlev, int nT, const int32_t *__restrict__ lev_ptr, const int32_t *__restrict__ lev_rows,
+    const int32_t *__restrict__ tf_ptr, const int32_t *__restrict__ tf_col, const double *__restrict__ tf_val,
+    const int32_t *__restrict__ tf_src, const int32_t *__restrict__ tb_ptr, const int32_t *__restrict__ tb_col,
+    const double *__restrict__ tb_val, const double *__restrict__ DT, const double *__restrict__ rbuf,
+    const int32_t *__restrict__ tdof, int ntdof, double *wT, double *y, int add, const int *run, const int *active) {
+    extern __shared__ double wt[];
+    if (skip(run, active)) return;
+    const int tid = threadIdx.x;
+    for (int l = 0; l < nlev; l++) {
+        for (int q = lev_ptr[l] + tid; q < lev_ptr[l + 1]; q += blockDim.x) {
+            const int t = lev_rows[q];
+            double acc = rbuf[tf_src[t]];
+            for (int e = tf_ptr[t]; e < tf_ptr[t + 1]; e++) {
+                const int c = tf_col[e];
+                const double xv = c >= 0 ? rbuf[c] : wt[-c - 1];
+                acc -= tf_val[e] * xv;
+            }
+            wt[t] = acc;
+        }
+        __syncthreads();
+    }
+    for (int l = nlev - 1; l >= 0; l--) {
+        for (int q = lev_ptr[l] + tid; q < lev_ptr[l + 1]; q += blockDim.x) {
+            const int t = lev_rows[q];
+            double acc = wt[t] / DT[t];
+            for (int e = tb_ptr[t]; e < tb_ptr[t + 1]; e++) acc -= tb_val[e] * wt[tb_col[e]];
+            wt[t] = acc;
+        }
+        __syncthreads();
+    }
+    for (int t = tid; t < nT; t += blockDim.x) {
+        wT[t] = wt[t];
+        if (t < ntdof) {
+            const int32_t d = tdof[t];
+            y[d] = add ? y[d] + wt[t] : wt[t];
+        }
+    }
+}
+
+// payload: w of this rank's rows that separator rows read, then (rank 0) the T inputs +-x[tdof]
+__global__ void tpack_kernel(const double *__restrict__ w, const int32_t *__restrict__ send, int nsend,
+                             const double *__restrict__ x, int64_t neg_from, const int32_t *__restrict__ tdof,
+                             int ntdof, double *__restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nsend) out[i] = w[send[i]];
+    else if (i < nsend + ntdof) {
+        const int32_t d = tdof[i - nsend];
+        const double v = x[d];
+        out[i] = d >= neg_from ? -v : v;
+    }
+}
+
+void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x, int64_t neg_from) {
+    if (S.kt == 0) return;
+    const int64_t n = S.nsend + S.ntdof;
+    if (n > 0)
+        hipLaunchKernelGGL(tpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c.stream, w, S.send.p,
+                           (int)S.nsend, x, neg_from, S.tdof.p, (int)S.ntdof, S.sbuf.p);
+    CPK_HIP(hipGetLastError());
+    c.comm->allgather(S.sbuf.p, S.rbuf.p, (size_t)S.kt, c.stream);
+}
+
+void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active) {
+    if (S.nT == 0) return;
+    hipLaunchKernelGGL(tsolve_kernel, dim3(1), dim3(256), (size_t)S.nT * sizeof(double), c.stream, (int)S.nlev,
+                       (int)S.nT, S.lev_ptr.p, S.lev_rows.p, S.tf_ptr.p, S.tf_col.p, S.tf_val.p, S.tf_src.p,
+                       S.tb_ptr.p, S.tb_col.p, S.tb_val.p, S.DT.p, S.rbuf.p, S.tdof.p, (int)S.ntdof, wT, y,
+                       add ? 1 : 0, run, active);
     CPK_HIP(hipGetLastError());
 }
 

@@ -16,6 +16,7 @@
 #include <memory>
 
 #include "dev.hpp"
+#include "dist.hpp"
 
 namespace cpk {
 
@@ -57,6 +58,7 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
     auto pc = std::make_unique<Precond>();
     pc->ctx = &c;
     pc->n = an.n, pc->m = an.m, pc->N = an.N;
+    pc->gn = an.n, pc->gm = an.m, pc->gN = an.N;
     pc->ordering = an.ordering;
     pc->Kp = std::move(an.Kp);
     pc->S = std::move(an.S);
@@ -79,31 +81,103 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
     return pc.release();
 }
 
+Precond *precond_create_dist(Ctx &c, Analysis &&an) {
+    auto t0 = std::chrono::steady_clock::now();
+    auto pc = std::make_unique<Precond>();
+    pc->ctx = &c;
+    pc->dist = true;
+    pc->gn = an.n, pc->gm = an.m, pc->gN = an.N;
+    pc->ordering = an.ordering;
+    const TreeSplit ts = split_tree(an.F0, c.nranks);
+    auto dm = std::make_shared<DofMap>(make_dofmap(an.F0, ts, an.n));
+    RankPlan rp = make_rank_plan(an.F0, ts, *dm, c.rank);
+    pc->n = dm->n_loc[c.rank], pc->m = dm->m_loc[c.rank], pc->N = pc->n + pc->m;
+    pc->nsub = rp.nsub;
+    if (rp.nT * (int64_t)sizeof(double) > 64 * 1024)
+        throw Error(CPK_ERR_UNSUPPORTED, "separator set too large for the one-workgroup separator solve");
+    // local sweeps: schedule + relabel of this rank's subtrees, rows summed in exported order
+    std::vector<int64_t> nextra(rp.nsub);
+    for (int64_t j = 0; j < rp.nsub; j++) nextra[j] = (int64_t)rp.extra[j].size();
+    const SweepConfig &sw = an.sweep;
+    Schedule S = build_schedule(rp.Fsub, sw.rows[0], sw.cap[0], sw.rows[1], sw.cap[1], sw.sub0, &nextra);
+    {
+        Factor Fl = relabel(rp.Fsub, S);
+        std::vector<int64_t> key(rp.nsub);
+        std::vector<std::vector<BwdExtra>> extra(rp.nsub);
+        std::vector<int32_t> pos(rp.nsub);
+        for (int64_t q = 0; q < rp.nsub; q++) {
+            key[q] = rp.key[S.order[q]];
+            extra[q] = std::move(rp.extra[S.order[q]]);
+            pos[S.order[q]] = (int32_t)q;
+        }
+        make_dfactor(Fl, S, pc->dF, &key, &extra);
+        std::vector<int32_t> send(rp.tsend.size());
+        for (size_t i = 0; i < send.size(); i++) send[i] = pos[rp.tsend[i]];
+        pc->sep.send.upload(send);
+        pc->sep.nsend = (int64_t)send.size();
+    }
+    for (int i = 0; i < 2; i++)
+        pc->dF.sweep_rows[i] = sw.rows[i], pc->dF.sweep_cap[i] = sw.cap[i], pc->dF.sweep_threads[i] = sw.threads[i];
+    // separator solve
+    DSep &T = pc->sep;
+    T.nT = rp.nT, T.kt = rp.kt, T.nlev = (int64_t)rp.tlev_ptr.size() - 1, T.ntdof = (int64_t)rp.tdof.size();
+    auto i32 = [](const std::vector<int64_t> &v) { return std::vector<int32_t>(v.begin(), v.end()); };
+    T.tf_ptr.upload(i32(rp.tf_ptr)), T.tf_col.upload(rp.tf_col), T.tf_val.upload(rp.tf_val);
+    T.tf_src.upload(rp.tf_src), T.tb_ptr.upload(i32(rp.tb_ptr)), T.tb_col.upload(rp.tb_col);
+    T.tb_val.upload(rp.tb_val), T.DT.upload(rp.DT), T.lev_ptr.upload(rp.tlev_ptr), T.lev_rows.upload(rp.tlev_rows);
+    T.tdof.upload(rp.tdof);
+    T.sbuf.alloc((size_t)std::max<int64_t>(T.kt, 1));
+    T.rbuf.alloc((size_t)std::max<int64_t>(T.kt * c.nranks, 1));
+    // refinement residual rows of Kp with their halo
+    make_dist_dmat(dist_csr(an.Kp, *dm, c.rank, false), c.nranks, pc->dKp);
+    pc->Kp = std::move(an.Kp);
+    pc->S = std::move(S);
+    pc->F = std::move(an.F0);
+    pc->dofmap = dm;
+    an.F = Factor();
+    pc->w.alloc((size_t)std::max<int64_t>(pc->nsub + T.nT, 1));
+    pc->r.alloc((size_t)std::max<int64_t>(pc->N, 1));
+    pc->active.alloc(1);
+    c.ensure_partials(std::max<size_t>(pc->dKp.nblk * 2, 4096));
+    CPK_HIP(hipDeviceSynchronize());
+    pc->ptime = an.seconds + std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return pc.release();
+}
+
 Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22) {
     return precond_create(c, analyze(A11, B, C22));
+}
+
+// y (=|+=) LDL * xin: forward sweep, [distributed: separator exchange + solve], backward sweep
+void Precond::ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run,
+                        const int *act) {
+    Ctx &c = *ctx;
+    launch_sptrsv_fwd(c, dF, xin, neg_from, w.p, run, act);
+    if (dist) {
+        launch_sep_exchange(c, sep, w.p, xin, neg_from);
+        launch_sep_solve(c, sep, w.p + nsub, y, add, run, act);
+    }
+    launch_sptrsv_bwd(c, dF, w.p, y, add, run, act);
 }
 
 void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run) {
     Ctx &c = *ctx;
     // y = op.LDL * x   (opLDL2.m:165-167)
-    launch_sptrsv_fwd(c, dF, x, neg_from, w.p, run, nullptr);
-    launch_sptrsv_bwd(c, dF, w.p, y, false, run, nullptr);
+    ldl_solve(x, neg_from, y, false, run, nullptr);
     if (nitref <= 0) return;
     const int64_t steps = (int64_t)nitref;
     if (force_itref != 0) {
         // every step runs; rNorm/xNorm and the final residual are dead
         for (int64_t s = 0; s < steps; s++) {
             launch_spmv_resid(c, dKp, x, neg_from, y, r.p, run, nullptr);  // r = x - op.A*y
-            launch_sptrsv_fwd(c, dF, r.p, N, w.p, run, nullptr);         // dy = op.LDL*r
-            launch_sptrsv_bwd(c, dF, w.p, y, true, run, nullptr);        // y = y + dy
+            ldl_solve(r.p, N, y, true, run, nullptr);                     // y = y + op.LDL*r
         }
         return;
     }
     // data-dependent refinement: the predicate lives on the device, kernels test it
     launch_spmv_resid_norm(c, dKp, x, neg_from, y, r.p, itref_tol, active.p, run, nullptr);
     for (int64_t s = 0; s < steps; s++) {
-        launch_sptrsv_fwd(c, dF, r.p, N, w.p, run, active.p);
-        launch_sptrsv_bwd(c, dF, w.p, y, true, run, active.p);
+        ldl_solve(r.p, N, y, true, run, active.p);
         if (s + 1 < steps) launch_spmv_resid_norm(c, dKp, x, neg_from, y, r.p, itref_tol, active.p, run, active.p);
     }
 }

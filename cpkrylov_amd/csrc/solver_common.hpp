@@ -105,11 +105,24 @@ template <class F>
 inline void launch_ew(Ctx &c, int64_t N, const F &f) {
     hipLaunchKernelGGL(ew_kernel<F>, dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f);
 }
+// Distributed mode: the reduction kernel leaves its local sums in c.red, RCCL allreduces them
+// and this single-thread kernel runs the epilogue on the global sums (identical on every rank).
+template <class F>
+__global__ void ewred_fin_kernel(F f, const double *tot) {
+    if (threadIdx.x || blockIdx.x) return;
+    if (f.setup()) f.fin(tot);
+}
 template <int NV, class F>
 inline void launch_ewred(Ctx &c, int64_t N, const F &f) {
     c.ensure_partials((size_t)ew_grid(N) * NV);
+    const bool dist = c.dist();
+    if (dist) CPK_HIP(hipMemsetAsync(c.red.p, 0, NV * sizeof(double), c.stream));
     hipLaunchKernelGGL((ewred_kernel<NV, F>), dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f,
-                       RedBuf{c.partials.p, c.counter.p});
+                       RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr});
+    if (dist) {
+        c.comm->allreduce_sum(c.red.p, NV, c.stream);
+        hipLaunchKernelGGL(ewred_fin_kernel<F>, dim3(1), dim3(64), 0, c.stream, f, (const double *)c.red.p);
+    }
 }
 template <class F>
 inline void launch_scalar(Ctx &c, const F &f) {

@@ -46,6 +46,7 @@ struct PolLanczosSpmv {
     int64_t N;
     int slot_shift;  // vk = VQ[(kk + slot_shift) % 3]
     __device__ bool skip(DState *st) { return PolStart::start(st); }
+    __device__ bool ran(DState *st) const { return st->running != 0; }
     __device__ const double *select(DState *st, const double *) {
         const int64_t kk = st->k + 1;
         return VQ + ((kk + slot_shift) % 3) * N;
@@ -81,6 +82,7 @@ struct PolLanczosSpmv {
 struct PolCgSpmv {
     const double *PQ;
     __device__ bool skip(DState *st) { return PolStart::start(st); }
+    __device__ bool ran(DState *st) const { return st->running != 0; }
     __device__ const double *select(DState *, const double *) { return PQ; }
     __device__ void fin(DState *st, const double *tot) {
         const int64_t kk = st->k + 1;
@@ -102,6 +104,7 @@ struct PolArnoldiSpmv {
     int64_t N;
     int64_t ring;  // 0: GMRES (column k-1), >0: DQGMRES ring size mem+1
     __device__ bool skip(DState *st) { return PolStart::start(st); }
+    __device__ bool ran(DState *st) const { return st->running != 0; }
     __device__ const double *select(DState *st, const double *) {
         const int64_t kk = st->k + 1;
         const int64_t pos = ring ? (kk - 1) % ring : (kk - 1);
@@ -114,15 +117,48 @@ struct PolArnoldiSpmv {
 struct PolPlainSpmv {
     const double *X;
     __device__ bool skip(DState *) { return false; }
+    __device__ bool ran(DState *) const { return true; }
     __device__ const double *select(DState *, const double *) { return X; }
     __device__ void fin(DState *st, const double *tot) { st->alpha = tot[0] + tot[1]; }
 };
 
+// distributed mode: publish the halo of the vector the policy selects, then run the epilogue
+// on the allreduced inner products
+template <class P>
+__global__ void krylov_pack_kernel(P pol, DState *st, const int32_t *__restrict__ idx, int64_t n, double *out) {
+    const double *x = pol.select(st, nullptr);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = x[idx[i]];
+}
+template <class P>
+__global__ void krylov_fin_kernel(P pol, DState *st, const double *tot) {
+    if (threadIdx.x || blockIdx.x) return;
+    if (pol.ran(st)) pol.fin(st, tot);
+}
+
 template <class P>
 void launch_krylov_spmv(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n, const P &pol) {
-    EpiKrylov<P> e{st, nullptr, y, n, RedBuf{c.partials.p, c.counter.p}, pol};
-    hipLaunchKernelGGL(spmv_stream<EpiKrylov<P>>, dim3((unsigned)AC.nblk), dim3(kBlock), 0, c.stream, AC.ptr.p,
-                       AC.col.p, AC.val.p, AC.blk.p, (const double *)nullptr, (int64_t)0, e);
+    const bool dist = c.dist();
+    if (AC.halo() && AC.kmax > 0) {
+        if (AC.nsend > 0)
+            hipLaunchKernelGGL(krylov_pack_kernel<P>, dim3((unsigned)std::min<int64_t>((AC.nsend + 255) / 256, 1024)),
+                               dim3(256), 0, c.stream, pol, st, AC.send.p, AC.nsend, AC.sbuf.p);
+        c.comm->allgather(AC.sbuf.p, AC.rbuf.p, (size_t)AC.kmax, c.stream);
+    }
+    if (dist) CPK_HIP(hipMemsetAsync(c.red.p, 0, 2 * sizeof(double), c.stream));
+    EpiKrylov<P> e{st, nullptr, y, n, RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr}, pol};
+    if (AC.halo())
+        hipLaunchKernelGGL((spmv_stream<EpiKrylov<P>, true>), dim3((unsigned)AC.nblk), dim3(kBlock), 0, c.stream,
+                           AC.ptr.p, AC.col.p, AC.val.p, AC.blk.p, (const double *)nullptr, (int64_t)0, e,
+                           (const double *)AC.rbuf.p, AC.nloc);
+    else
+        hipLaunchKernelGGL((spmv_stream<EpiKrylov<P>, false>), dim3((unsigned)AC.nblk), dim3(kBlock), 0, c.stream,
+                           AC.ptr.p, AC.col.p, AC.val.p, AC.blk.p, (const double *)nullptr, (int64_t)0, e,
+                           (const double *)nullptr, (int64_t)0);
+    if (dist) {
+        c.comm->allreduce_sum(c.red.p, 2, c.stream);
+        hipLaunchKernelGGL(krylov_fin_kernel<P>, dim3(1), dim3(64), 0, c.stream, pol, st, (const double *)c.red.p);
+    }
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -952,7 +988,8 @@ struct SolveCore {
 
     SolveCore(Ctx &cc, Precond &MM, const DMat &ACm, int meth, const cpk_opts *o)
         : c(cc), M(MM), AC(ACm), n(MM.n), m(MM.m), N(MM.N), method(meth) {
-        const double itmax_default = (meth == CPK_GMRES || meth == CPK_DQGMRES) ? (double)(n + m) : (double)n;
+        // defaults use the global sizes (size(A,1) in the reference), identical on every rank
+        const double itmax_default = (meth == CPK_GMRES || meth == CPK_DQGMRES) ? (double)(MM.gn + MM.gm) : (double)MM.gn;
         itmax = itmax_default;
         if (o) {
             if (o->has_atol) atol = o->atol;
@@ -964,6 +1001,8 @@ struct SolveCore {
             if (o->has_print) print = o->print != 0;
         }
         if (const char *e = getenv("CPK_NO_GRAPH")) use_graph = atoi(e) == 0;
+        if (c.dist() && !c.comm->capturable()) use_graph = false;
+        if (c.rank != 0) print = false;
         if (const char *e = getenv("CPK_BATCH")) batch = std::max(1, atoi(e));
     }
 
@@ -1431,43 +1470,44 @@ void method_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, 
     }
 }
 
-int reg_shift_device(Ctx &c, const double *d_b, const DMat &AC, const DMat &Kp, Precond &M, double *d_b1,
-                     double *d_xy0) {
+int reg_shift_device(Ctx &c, const double *d_b, const DMat &Arows, const DMat &Btrows, int64_t bt_colmin, Precond &M,
+                     double *d_b1, double *d_xy0) {
     const int64_t n = M.n, m = M.m, N = M.N;
     DBuf<int> flag;
     flag.alloc(1);
     int shift = 0;
-    if (m > 0) {
+    if (M.gm > 0) {  // any(b(n+1:n+m)) over all ranks
         c.ensure_partials((size_t)kEwGrid);
+        CPK_HIP(hipMemsetAsync(flag.p, 0, sizeof(int), c.stream));
         launch_ewred<1>(c, m, AnyNonzero{d_b, n, flag.p});
         CPK_HIP(hipMemcpyAsync(&shift, flag.p, sizeof(int), hipMemcpyDeviceToHost, c.stream));
         CPK_HIP(hipStreamSynchronize(c.stream));
     }
     if (shift) {
         DBuf<double> t1, t2;
-        t1.alloc(N), t2.alloc(N);
+        t1.alloc(std::max<int64_t>(N, 1)), t2.alloc(std::max<int64_t>(N, 1));
         // xy0 = M * [zeros(n,1); b(n+1:n+m)]   (reg_cpkrylov.m:156)
-        CPK_HIP(hipMemsetAsync(t1.p, 0, n * sizeof(double), c.stream));
-        CPK_HIP(hipMemcpyAsync(t1.p + n, d_b + n, m * sizeof(double), hipMemcpyDeviceToDevice, c.stream));
+        if (n) CPK_HIP(hipMemsetAsync(t1.p, 0, n * sizeof(double), c.stream));
+        if (m) CPK_HIP(hipMemcpyAsync(t1.p + n, d_b + n, m * sizeof(double), hipMemcpyDeviceToDevice, c.stream));
         M.apply(t1.p, N, d_xy0, nullptr);
-        launch_spmv(c, AC, d_xy0, t1.p, nullptr);            // rows < n: A*xy0(1:n)
-        launch_spmv_colmask(c, Kp, n, d_xy0, t2.p, nullptr);  // rows < n: B'*xy0(n+1:N)
-        launch_ew(c, n, ShiftRhs{d_b, t1.p, t2.p, d_b1});    // b1 = b(1:n) - A*xy0(1:n) - B'*xy0(n+1:N)
+        launch_spmv(c, Arows, d_xy0, t1.p, nullptr);                     // rows < n: A*xy0(1:n)
+        launch_spmv_colmask(c, Btrows, bt_colmin, d_xy0, t2.p, nullptr);  // rows < n: B'*xy0(n+1:N)
+        launch_ew(c, n, ShiftRhs{d_b, t1.p, t2.p, d_b1});  // b1 = b(1:n) - A*xy0(1:n) - B'*xy0(n+1:N)
         CPK_HIP(hipStreamSynchronize(c.stream));
     } else {
-        CPK_HIP(hipMemcpyAsync(d_b1, d_b, n * sizeof(double), hipMemcpyDeviceToDevice, c.stream));
-        CPK_HIP(hipMemsetAsync(d_xy0, 0, N * sizeof(double), c.stream));
+        if (n) CPK_HIP(hipMemcpyAsync(d_b1, d_b, n * sizeof(double), hipMemcpyDeviceToDevice, c.stream));
+        if (N) CPK_HIP(hipMemsetAsync(d_xy0, 0, N * sizeof(double), c.stream));
     }
     return shift;
 }
 
-void reg_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, const DMat &Kp, Precond &M,
-                      const cpk_opts *opts, double *d_x, cpk_stats *stats) {
+void reg_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, const DMat &Arows, const DMat &Btrows,
+                      int64_t bt_colmin, Precond &M, const cpk_opts *opts, double *d_x, cpk_stats *stats) {
     const int64_t n = M.n, N = M.N;
     auto t0 = std::chrono::steady_clock::now();
     DBuf<double> xy0, b1, dxy;
-    xy0.alloc(N), b1.alloc(std::max<int64_t>(n, 1)), dxy.alloc(N);
-    const int shift = reg_shift_device(c, d_b, AC, Kp, M, b1.p, xy0.p);
+    xy0.alloc(std::max<int64_t>(N, 1)), b1.alloc(std::max<int64_t>(n, 1)), dxy.alloc(std::max<int64_t>(N, 1));
+    const int shift = reg_shift_device(c, d_b, Arows, Btrows, bt_colmin, M, b1.p, xy0.p);
     method_solve_device(c, method, b1.p, AC, M, opts, shift ? dxy.p : d_x, stats);
     if (shift) launch_ew(c, N, Recover{xy0.p, dxy.p, d_x});  // x = [xy0(1:n) + dx; xy0(n+1:N) + dy]
     CPK_HIP(hipStreamSynchronize(c.stream));

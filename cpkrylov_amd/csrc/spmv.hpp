@@ -14,12 +14,14 @@
 
 namespace cpk {
 
-template <class Epi>
+// HALO: distributed rows (DistCsr); column c >= nloc reads the allgathered halo xg[c - nloc].
+template <class Epi, bool HALO = false>
 __global__ __launch_bounds__(kBlock) void spmv_stream(const uint32_t *__restrict__ ptr,
                                                       const int32_t *__restrict__ col,
                                                       const double *__restrict__ val,
                                                       const int32_t *__restrict__ blk,
-                                                      const double *x, int64_t col_min, Epi epi) {
+                                                      const double *x, int64_t col_min, Epi epi,
+                                                      const double *xg, int64_t nloc) {
     __shared__ double prod[kSpmvCap];
     if (epi.skip()) return;
     x = epi.xvec(x);
@@ -29,7 +31,8 @@ __global__ __launch_bounds__(kBlock) void spmv_stream(const uint32_t *__restrict
     if (e1 - e0 <= (uint32_t)kSpmvCap) {
         for (uint32_t e = e0 + tid; e < e1; e += kBlock) {
             const int32_t c = col[e];
-            prod[e - e0] = (c >= col_min) ? val[e] * x[c] : 0.0;
+            const double xv = (!HALO || c < nloc) ? x[c] : xg[c - nloc];
+            prod[e - e0] = (c >= col_min) ? val[e] * xv : 0.0;
         }
         __syncthreads();
         for (int64_t r = r0 + tid; r < r1; r += kBlock) {
@@ -44,7 +47,8 @@ __global__ __launch_bounds__(kBlock) void spmv_stream(const uint32_t *__restrict
             const uint32_t c1 = min(e1, c0 + (uint32_t)kSpmvCap);
             for (uint32_t e = c0 + tid; e < c1; e += kBlock) {
                 const int32_t c = col[e];
-                prod[e - c0] = (c >= col_min) ? val[e] * x[c] : 0.0;
+                const double xv = (!HALO || c < nloc) ? x[c] : xg[c - nloc];
+                prod[e - c0] = (c >= col_min) ? val[e] * xv : 0.0;
             }
             __syncthreads();
             if (tid == 0)

@@ -106,6 +106,14 @@ int cpk_abi_version(void);
 int cpk_get_unique_id(unsigned char id[128]);
 /* device < 0: use the current device.  nranks == 1: no communicator (unique_id may be NULL). */
 int cpk_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id, cpk_ctx *out);
+/* Single-GPU rehearsal of the distributed path: `nranks` ranks as host threads of one process,
+ * all on one device, exchanging through a shared HBM buffer instead of RCCL (RCCL refuses two
+ * ranks on one GPU).  Each thread creates its context with cpk_ctx_create_sim and then makes
+ * the same collective calls as an RCCL rank.  For tests; no hipGraph capture. */
+typedef struct cpk_simgroup_s *cpk_simgroup;
+int cpk_simgroup_create(int nranks, cpk_simgroup *out);
+int cpk_simgroup_destroy(cpk_simgroup g);
+int cpk_ctx_create_sim(int device, cpk_simgroup group, int rank, int nranks, cpk_ctx *out);
 int cpk_ctx_destroy(cpk_ctx ctx);
 int cpk_ctx_synchronize(cpk_ctx ctx);
 
@@ -121,7 +129,11 @@ int cpk_mat_destroy(cpk_mat A);
 /* y = A*x on the device (host vectors in/out); replaces MATLAB sparse mtimes A*v. */
 int cpk_mat_spmv(cpk_mat A, const double *x, double *y);
 
-/* ---- preconditioner: M = opLDL2(A, B, C), Kp = [A B'; B C] (ops/opLDL2.m:60-92) ------ */
+/* ---- preconditioner: M = opLDL2(A, B, C), Kp = [A B'; B C] (ops/opLDL2.m:60-92) ------
+ * Distributed contexts (nranks > 1): every rank passes the same global matrices; the library
+ * partitions rows by the elimination tree.  Host-vector entry points
+ * then take and return GLOBAL vectors on every rank; device-vector entry points take the
+ * rank's LOCAL slice in the order cpk_pc_local_dofs reports ([x-part; y-part]). */
 int cpk_pc_create(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptime, cpk_pc *out);
 int cpk_pc_destroy(cpk_pc M);
 /* M.nitref = ...; M.itref_tol = ...; etc. (opLDL2.m:45-50, 97-115), has_* fields select. */
@@ -134,6 +146,9 @@ int cpk_pc_apply_device(cpk_pc M, const double *d_x, double *d_y);
 /* x = Kp*b (opLDL2.divide, opLDL2.m:193-195). */
 int cpk_pc_divide(cpk_pc M, const double *b, double *x);
 int cpk_pc_get_info(cpk_pc M, cpk_pc_info *info);
+/* Local slice of a (distributed) preconditioner: n_loc x-part and m_loc y-part dofs; dofs[i] =
+ * global index of local entry i (n_loc + m_loc entries).  One GPU: the identity. */
+int cpk_pc_local_dofs(cpk_pc M, int64_t *n_loc, int64_t *m_loc, int32_t *dofs);
 /* Export the factors P'*Kp*P = L*D*L': strict-lower L in CSC (Lcolptr[N+1], Lrowind[nnz_l],
  * Lval[nnz_l]), D[N], perm[N] (perm[k] = original index of pivot k).  Any pointer may be NULL. */
 int cpk_pc_export(cpk_pc M, int64_t *Lcolptr, int32_t *Lrowind, double *Lval, double *D, int32_t *perm);

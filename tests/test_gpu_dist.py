@@ -1,0 +1,150 @@
+"""Distributed path on the GPU, rehearsed on one MI355X: P ranks run as
+threads of this process, each with its own context and stream, exchanging through a shared HBM
+buffer (cpk_ctx_create_sim) instead of RCCL -- RCCL refuses two ranks on one device, so the
+RCCL transport itself is exercised by the 8-GPU bench only.
+
+Parity bar:
+  * M*z of the distributed preconditioner (local sweeps + separator exchange + redundant
+    separator solve + halo'd residual SpMV) equals the oracle's opLDL2 apply bit for bit;
+  * distributed solves match the oracle as the 1-GPU solves do (same niters, histories within
+    the sensitivity band); only the inner products' summation order differs.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import fixtures as F
+from cpkrylov_amd.synthetic import saddle_system
+from oracle import oracle as O
+from sensitivity import band
+
+pytestmark = pytest.mark.gpu
+
+FLOOR = 1e-8
+SAFETY = 10.0
+
+
+def _run_ranks(P, fn):
+    """fn(ctx, rank) on P simulated ranks; returns the list of results."""
+    import cpkrylov_amd as cpk
+    g = cpk.SimGroup(P)
+
+    def one(r):
+        ctx = cpk.Context(device=0, rank=r, nranks=P, simgroup=g)
+        try:
+            return fn(ctx, r)
+        finally:
+            ctx.close()
+
+    with ThreadPoolExecutor(P) as ex:
+        futs = [ex.submit(one, r) for r in range(P)]
+        return [f.result(timeout=600) for f in futs]
+
+
+def _system(name):
+    if name == "synthetic20k":
+        S = saddle_system(N=20000, seed=3)
+        return dict(Q=S["Q"], B=S["B"], C=S["C"], G=S["G"], n=S["n"], m=S["m"], rhs=S["rhs"])
+    return F.load(name)
+
+
+@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("name", ["cvxqp1_m", "synthetic20k"])
+@pytest.mark.parametrize("props", [dict(nitref=0), dict(nitref=1, force_itref=True),
+                                   dict(nitref=3, force_itref=False, itref_tol=1e-8)])
+def test_dist_apply_bitexact(name, P, props):
+    import cpkrylov_amd as cpk
+    S = _system(name)
+    z = np.random.default_rng(5).standard_normal(S["n"] + S["m"])
+
+    def work(ctx, r):
+        M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+        for k, v in props.items():
+            setattr(M, k, v)
+        d, nl = M.local_dofs()
+        return M * z, M.export_factors() if r == 0 else None, d, nl
+
+    res = _run_ranks(P, work)
+    L, D, perm = res[0][1]
+    Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=(L, D, perm))
+    Mo.set(**{k: float(v) for k, v in props.items()})
+    yo = Mo @ z
+    for y, _, _, _ in res:
+        assert np.array_equal(y, yo), np.max(np.abs(y - yo))
+    # ownership: the local slices partition the dofs, x-part first
+    alld = np.concatenate([d for _, _, d, _ in res])
+    assert np.array_equal(np.sort(alld), np.arange(S["n"] + S["m"]))
+    for _, _, d, nl in res:
+        assert np.all(d[:nl] < S["n"]) and np.all(d[nl:] >= S["n"])
+
+
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("method", ["minres", "cg", "cglanczos", "symmlq"])
+def test_dist_reg_cpkrylov_matches_oracle(method, P):
+    import cpkrylov_amd as cpk
+    name = "cvxqp1_m"
+    Pd = F.load(name)
+    opts = dict(F.EXPROG_OPTS)
+    fn = getattr(cpk, "cp" + method)
+
+    def work(ctx, r):
+        x, stats, flag = cpk.reg_cpkrylov(fn, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts, ctx=ctx)
+        perm = stats["M"].export_factors()[2] if r == 0 else None
+        return x, {k: v for k, v in stats.items() if k != "M"}, flag, perm
+
+    res = _run_ranks(P, work)
+    x, stats, flag, perm = res[0]
+    for xr, sr, fr, _ in res[1:]:  # every rank returns the same global answer
+        assert np.array_equal(xr, x) and sr["niters"] == stats["niters"] and fr == flag
+    xo, so = O.reg_cpkrylov(method, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts, perm=perm)
+    assert stats["niters"] == so["niters"]
+    assert flag["solved"] == so["solved"]
+    bd = band(name, method, {}, perm)
+    h0 = stats.get("residHistory", stats.get("cgresidHistory"))[0]
+    for k in [k for k in so if k.endswith("History")]:
+        assert len(stats[k]) == len(so[k]), k
+        dev = np.max(np.abs(stats[k] - so[k])) / h0
+        assert dev <= max(FLOOR, SAFETY * bd[k]), (k, dev, bd[k])
+    dx = np.linalg.norm(x - xo) / np.linalg.norm(xo)
+    assert dx <= max(FLOOR, SAFETY * bd["x"]), (dx, bd["x"])
+
+
+def test_dist_device_vectors_synthetic():
+    """Device-resident local slices (the bench's path): shift + cpminres on 4 ranks agree with
+    the 1-GPU solve of the same system."""
+    import ctypes as C
+
+    import cpkrylov_amd as cpk
+    from cpkrylov_amd import _lib
+    from devbuf import DeviceArray
+    S = saddle_system(N=60000, seed=9)
+    opts = dict(F.EXPROG_OPTS)
+    x1, st1, fl1 = cpk.reg_cpkrylov(cpk.cpminres, S["rhs"], S["Q"], S["B"], S["C"], S["G"], opts)
+
+    def work(ctx, r):
+        A, B, Cm = (cpk.Matrix(S[k], ctx) for k in ("Q", "B", "C"))
+        M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+        M.nitref, M.force_itref = 1, True
+        d, nl = M.local_dofs()
+        b = DeviceArray.of(S["rhs"][d])
+        b1, xy0, xy = DeviceArray(nl), DeviceArray(len(d)), DeviceArray(len(d))
+        sh = C.c_int()
+        _lib.check(_lib.lib.cpk_reg_shift_device(ctx.h, b.p, A.h, B.h, Cm.h, M.h, b1.p, xy0.p, C.byref(sh)))
+        st = _lib.Stats()
+        hist = np.zeros(600)
+        st.hist = hist.ctypes.data_as(C.POINTER(C.c_double))
+        st.hist_cap = 600
+        _lib.check(_lib.lib.cpk_method_solve_device(ctx.h, 2, b1.p, A.h, Cm.h, M.h, C.byref(_lib.make_opts(opts)),
+                                                    xy.p, C.byref(st)))
+        ctx.synchronize()
+        x = xy0.numpy() + xy.numpy()
+        return d, x, int(st.niters), hist[:st.hist_len].copy(), bool(sh.value)
+
+    res = _run_ranks(4, work)
+    x = np.empty(S["n"] + S["m"])
+    for d, xl, it, h, sh in res:
+        x[d] = xl
+        assert sh and it == st1["niters"]
+        assert np.max(np.abs(h - st1["residHistory"])) <= 1e-8 * st1["residHistory"][0]
+    assert np.linalg.norm(x - x1) <= 1e-8 * np.linalg.norm(x1)
