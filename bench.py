@@ -12,8 +12,10 @@ Metric (BASELINE.json): "Krylov iters/sec + SpMV GB/s (% HBM peak), cpminres 10M
             algorithmic bytes per launch / its HIP-event-timed average duration, vs 8 TB/s.
   cpu_baseline  the C restatement (oracle/) of the same solve on one host core, timed on a
             bounded sample of the same workload.
-Multi-GPU (torchrun, one process per GPU): each rank runs an independent replica of the solve
-(replicas only this round) and the line reports the aggregate.
+Multi-GPU (torchrun, one process per GPU): ONE solve of the same S10 system row-block
+partitioned over the ranks (strong scaling): RCCL allreduce for the inner
+products, allgathered halos for the SpMVs and the separator exchange of the distributed LDL'
+sweeps.  value = that solve's iterations / max-over-ranks wall time.
 """
 import argparse
 import ctypes as C
@@ -43,8 +45,24 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-reps", type=int, default=20)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE passes")
+    ap.add_argument("--dist", action="store_true", help="run the distributed path even on one GPU (1-rank RCCL)")
     ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+class _quiet_stdout:
+    """Send fd 1 to stderr while RCCL initialises (it prints a version banner on stdout; the
+    bench's stdout is its one JSON line)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
 
 
 def main():
@@ -59,7 +77,9 @@ def main():
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        with _quiet_stdout():
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.barrier()
     import torch
 
     import cpkrylov_amd as cpk
@@ -69,16 +89,28 @@ def main():
     t_setup = time.perf_counter()
     S = saddle_system(N=args.size)
     n, m, N = S["n"], S["m"], S["N"]
-    ctx = cpk.Context(device=local)
+    # N > 1 (or --dist): one distributed solve over all ranks (strong scaling), RCCL collectives
+    # and halo exchanges inside the solver; every rank holds its row block
+    distributed = world > 1 or args.dist
+    if distributed:
+        uid = [cpk.get_unique_id() if rank == 0 else None]
+        if dist:
+            dist.broadcast_object_list(uid, src=0)
+        with _quiet_stdout():
+            ctx = cpk.Context(device=local, rank=rank, nranks=world, unique_id=uid[0])
+    else:
+        ctx = cpk.Context(device=local)
     A, B, Cm, G = (cpk.Matrix(S[k], ctx) for k in ("Q", "B", "C", "G"))
     M = cpk.opLDL2(G, B, -S["C"], ctx=ctx)
     M.nitref, M.itref_tol = EXPROG_OPTS["nitref"], EXPROG_OPTS["itref_tol"]
     M.residual_update, M.force_itref = EXPROG_OPTS["residual_update"], EXPROG_OPTS["force_itref"]
+    dofs, n_loc = M.local_dofs()
+    N_loc = len(dofs)
     dev = torch.device("cuda", local)
-    b = torch.from_numpy(S["rhs"]).to(dev)
-    b1 = torch.empty(n, dtype=torch.float64, device=dev)
-    xy0 = torch.empty(N, dtype=torch.float64, device=dev)
-    xy = torch.empty(N, dtype=torch.float64, device=dev)
+    b = torch.from_numpy(np.ascontiguousarray(S["rhs"][dofs])).to(dev)
+    b1 = torch.empty(max(n_loc, 1), dtype=torch.float64, device=dev)
+    xy0 = torch.empty(max(N_loc, 1), dtype=torch.float64, device=dev)
+    xy = torch.empty(max(N_loc, 1), dtype=torch.float64, device=dev)
     torch.cuda.synchronize(dev)
     shifted = C.c_int()
     _lib.check(_lib.lib.cpk_reg_shift_device(ctx.h, C.c_void_p(b.data_ptr()), A.h, B.h, Cm.h, M.h,
@@ -120,11 +152,8 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        it = torch.tensor([float(iters)], dtype=torch.float64, device=dev)
-        dist.all_reduce(it, op=dist.ReduceOp.SUM)
-        total_iters = float(it.item())
-    else:
-        total_iters = float(iters)
+    # one solve over all ranks: its iterations are the job's iterations (strong scaling)
+    total_iters = float(iters)
 
     prof = _lib.Profile()
     _lib.check(_lib.lib.cpk_profile_kernels(ctx.h, A.h, Cm.h, M.h, args.profile_reps, C.byref(prof)))
@@ -140,10 +169,10 @@ def main():
 
     cpu = None
     parity = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not distributed:
         cpu, parity = cpu_baseline(S, b1.cpu().numpy(), M, args, hist_gpu, niters_last)
     pmc = None
-    if rank == 0 and world == 1 and not args.no_pmc:
+    if rank == 0 and world == 1 and not args.no_pmc and not distributed:
         pmc = pmc_traffic(args)
         if pmc and "resid" in pmc:
             roofline["traffic"] = pmc["resid"]["bytes"]
@@ -155,17 +184,18 @@ def main():
             "metric": "Krylov iters/sec + SpMV GB/s (% HBM peak), cpminres 10M-dof, 1/2/4/8 GPU",
             "value": round(value, 2), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"S10 synthetic symmetric saddle-point system, cp{args.method} to convergence "
                                    "(cpk_exprog1 options), step = one method call",
                        "N": N, "n": n, "m": m, "nnz_kp": M.info["nnz_kp"], "nnz_l": M.info["nnz_l"],
                        "sweep_launches": M.info["nrounds"], "elim_tree_depth": M.info["depth"],
-                       "parallelism": "single" if world == 1 else f"replicas{world}", "seed": S["seed"]},
-            "iters_per_step": round(total_iters / args.steps / world, 2), "solved": solved,
+                       "parallelism": f"rowblock{world}" if distributed else "single", "seed": S["seed"],
+                       "rows_local_rank0": N_loc},
+            "iters_per_step": round(total_iters / args.steps, 2), "solved": solved,
             "roofline": roofline,
-            "roofline_iteration": {"bytes_per_iter": bytes_per_iter,
-                                   "achieved": round(bytes_per_iter * total_iters / world / dt / 1e9, 1),
-                                   "frac": round(bytes_per_iter * total_iters / world / dt / 1e9 / HBM_PEAK_GBS, 4)},
+            "roofline_iteration": {"bytes_per_iter_rank0": bytes_per_iter,
+                                   "achieved": round(bytes_per_iter * total_iters / dt / 1e9, 1),
+                                   "frac": round(bytes_per_iter * total_iters / dt / 1e9 / HBM_PEAK_GBS, 4)},
             "kernels": kernels,
             "device_loop_ms_per_step": round(loop_ms / args.steps, 3),
             "setup_s": round(setup_s, 2),

@@ -194,7 +194,7 @@ int cpk_ctx_create(int device, int rank, int nranks, const unsigned char *unique
     API_BEGIN
     need(out != nullptr, "out is NULL");
     auto ctx = ctx_base(device, rank, nranks);
-    if (nranks > 1) {
+    if (nranks > 1 || unique_id) {  // a 1-rank communicator runs the distributed path (tests)
         need(unique_id != nullptr, "unique_id required when nranks > 1");
         ctx->comm.reset(make_rccl_comm(nranks, rank, unique_id));
         ctx->c.comm = ctx->comm.get();

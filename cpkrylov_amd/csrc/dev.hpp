@@ -74,7 +74,7 @@ struct Ctx {
     DBuf<unsigned> counter;  // arrival tickets
     DBuf<double> red;        // distributed mode: local sums awaiting the allreduce
     Comm *comm = nullptr;    // owned by the C-ABI context object
-    bool dist() const { return nranks > 1 && comm != nullptr; }
+    bool dist() const { return comm != nullptr; }  // also a 1-rank communicator (tests)
     void ensure_partials(size_t count);
 };
 
@@ -88,6 +88,7 @@ struct DMat {
     DBuf<double> val;
     DBuf<int32_t> blk;  // row-block boundaries [nblk + 1]
     bool is_diag = false;
+    uint64_t gen = 0;   // unique per upload (keys cached solver graphs)
     // distributed rows (DistCsr): columns >= nloc read the allgathered halo buffer
     int64_t nloc = -1, kmax = 0, nsend = 0;
     DBuf<int32_t> send;         // local indices published to the other ranks
@@ -218,6 +219,8 @@ struct Precond {
     // public properties of opLDL2 (opLDL2.m:45-50)
     double nitref = 3, itref_tol = 1.0e-8, force_itref = 0, residual_update = 0;
     double ptime = 0;
+    // cached solvers (workspace + captured iteration graphs), keyed; see solvers.hip
+    std::vector<std::pair<std::string, std::shared_ptr<void>>> solvers;
     // y = M*x  (opLDL2.multiply); all pointers on the device, enqueued on ctx->stream
     void apply(const double *x, int64_t neg_from, double *y, const int *run);
     void ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run, const int *act);

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 #include "dev.hpp"
@@ -25,6 +26,8 @@ void Ctx::ensure_partials(size_t count) {
 
 // ---- device matrix layout -------------------------------------------------------------------
 void make_dmat(const HCsr &a, DMat &d) {
+    static std::atomic<uint64_t> gen{1};
+    d.gen = gen++;
     if (a.nnz() > (int64_t)UINT32_MAX) throw Error(CPK_ERR_UNSUPPORTED, "more than 2^32 nonzeros in one matrix");
     d.nrows = a.nrows, d.ncols = a.ncols, d.nnz = a.nnz();
     std::vector<uint32_t> ptr(a.ptr.begin(), a.ptr.end());

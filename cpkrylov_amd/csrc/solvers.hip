@@ -970,6 +970,9 @@ struct Copy {
 // ==============================================================================================
 // host driver
 // ==============================================================================================
+// A SolveCore is kept by the preconditioner between calls with the same method, operators,
+// vectors and captured properties (solver_key): its workspace and the captured iteration
+// graphs are reused, so a repeated solve costs its kernels plus one state upload.
 struct SolveCore {
     Ctx &c;
     Precond &M;
@@ -985,12 +988,26 @@ struct SolveCore {
     int64_t printed = 0;
     int batch = 16;
     bool use_graph = true;
+    // reused across calls
+    std::vector<DBuf<double>> rings;
+    size_t ring_next = 0;
+    std::vector<std::pair<hipGraph_t, hipGraphExec_t>> graphs;  // one per loop site
 
     SolveCore(Ctx &cc, Precond &MM, const DMat &ACm, int meth, const cpk_opts *o)
         : c(cc), M(MM), AC(ACm), n(MM.n), m(MM.m), N(MM.N), method(meth) {
+        reset(o);
+    }
+    ~SolveCore() {
+        for (auto &g : graphs) {
+            if (g.second) (void)hipGraphExecDestroy(g.second);
+            if (g.first) (void)hipGraphDestroy(g.first);
+        }
+    }
+    // per-call options (they only reach the device through DState, not through captured kernels)
+    void reset(const cpk_opts *o) {
         // defaults use the global sizes (size(A,1) in the reference), identical on every rank
-        const double itmax_default = (meth == CPK_GMRES || meth == CPK_DQGMRES) ? (double)(MM.gn + MM.gm) : (double)MM.gn;
-        itmax = itmax_default;
+        itmax = (method == CPK_GMRES || method == CPK_DQGMRES) ? (double)(M.gn + M.gm) : (double)M.gn;
+        atol = 1e-6, rtol = 1e-6, btol = 0, restart = 50, mem = 50, print = true;
         if (o) {
             if (o->has_atol) atol = o->atol;
             if (o->has_rtol) rtol = o->rtol;
@@ -1000,10 +1017,14 @@ struct SolveCore {
             if (o->has_mem) mem = std::max(1.0, o->mem);  // cpdqgmres.m:116-118
             if (o->has_print) print = o->print != 0;
         }
+        use_graph = true;
         if (const char *e = getenv("CPK_NO_GRAPH")) use_graph = atoi(e) == 0;
         if (c.dist() && !c.comm->capturable()) use_graph = false;
         if (c.rank != 0) print = false;
+        batch = 16;
         if (const char *e = getenv("CPK_BATCH")) batch = std::max(1, atoi(e));
+        printed = 0;
+        ring_next = 0;
     }
 
     double *vec(size_t i) {
@@ -1013,36 +1034,40 @@ struct SolveCore {
         }
         return vecs[i].p;
     }
-    // a fresh contiguous allocation of `count` N-vectors (slot rings)
-    std::vector<DBuf<double>> rings;
+    // the ring_next-th contiguous allocation of `count` N-vectors (slot rings, Arnoldi bases)
     double *ring(size_t count) {
-        rings.emplace_back();
-        rings.back().alloc(count * (size_t)N);
-        return rings.back().p;
+        if (ring_next == rings.size()) rings.emplace_back();
+        DBuf<double> &r = rings[ring_next++];
+        if (r.n != count * (size_t)N) r.alloc(std::max<size_t>(count * (size_t)N, 1));
+        return r.p;
+    }
+    template <class T>
+    static void ensure(DBuf<T> &b, size_t count) {
+        if (b.n != count) b.alloc(count);
     }
 
     void setup_state(int64_t hcap, int64_t maxv) {
-        dst.alloc(1);
+        ensure(dst, 1);
         std::memset(&h, 0, sizeof h);
         h.itmax = (int64_t)std::min(itmax, 9.0e15);
         if (h.itmax < 0) h.itmax = 0;
         h.atol = atol, h.rtol = rtol, h.btol = btol;
         h.hcap = hcap;
-        hist.alloc(hcap);
-        hist2.alloc(hcap);
-        hist3.alloc(hcap);
-        aux.alloc(3 * hcap);
+        ensure(hist, hcap);
+        ensure(hist2, hcap);
+        ensure(hist3, hcap);
+        ensure(aux, 3 * hcap);
         h.hist = hist.p, h.hist2 = hist2.p, h.hist3 = hist3.p, h.aux = aux.p;
         h.restart = (int64_t)restart;
         h.mem = (int64_t)mem;
         if (maxv > 0) {
             const int64_t R = h.restart, Mm = h.mem;
             if (method == CPK_GMRES) {
-                H.alloc((R + 1) * R);
-                cvec.alloc(R), svec.alloc(R), gvec.alloc(R + 1), zvec.alloc(R);
+                ensure(H, (R + 1) * R);
+                ensure(cvec, R), ensure(svec, R), ensure(gvec, R + 1), ensure(zvec, R);
             } else {
-                H.alloc((Mm + 2) * (Mm + 2));
-                cvec.alloc(Mm), svec.alloc(Mm), gvec.alloc(Mm + 1), zvec.alloc(1);
+                ensure(H, (Mm + 2) * (Mm + 2));
+                ensure(cvec, Mm), ensure(svec, Mm), ensure(gvec, Mm + 1), ensure(zvec, 1);
             }
             H.zero(c.stream), cvec.zero(c.stream), svec.zero(c.stream), gvec.zero(c.stream);
             h.H = H.p, h.c = cvec.p, h.s = svec.p, h.g = gvec.p, h.z = zvec.p;
@@ -1059,17 +1084,23 @@ struct SolveCore {
         CPK_HIP(hipStreamSynchronize(c.stream));
     }
 
-    // replay `body` (one iteration) in batches until the device sets `stop`
-    void loop(const std::function<void()> &body, const std::function<void()> &printer) {
+    // replay `body` (one iteration) in batches until the device sets `stop`.  The batch graph of
+    // a loop site is captured once and replayed by later calls with the same key.
+    void loop(const std::function<void()> &body, const std::function<void()> &printer, size_t site = 0) {
         pull();
         if (h.stop) return;
-        hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
         if (use_graph) {
-            CPK_HIP(hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
-            for (int b = 0; b < batch; b++) body();
-            CPK_HIP(hipStreamEndCapture(c.stream, &graph));
-            CPK_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+            if (graphs.size() <= site) graphs.resize(site + 1, {nullptr, nullptr});
+            if (!graphs[site].second) {
+                hipGraph_t graph = nullptr;
+                CPK_HIP(hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
+                for (int b = 0; b < batch; b++) body();
+                CPK_HIP(hipStreamEndCapture(c.stream, &graph));
+                graphs[site].first = graph;
+                CPK_HIP(hipGraphInstantiate(&graphs[site].second, graph, nullptr, nullptr, 0));
+            }
+            exec = graphs[site].second;
         }
         const int64_t guard = h.k + (int64_t)std::min(itmax, 4.0e9) + 2 * batch + 2;
         for (;;) {
@@ -1079,14 +1110,7 @@ struct SolveCore {
             pull();
             if (print && printer) printer();
             if (h.stop) break;
-            if (h.k > guard) {
-                if (exec) (void)hipGraphExecDestroy(exec), (void)hipGraphDestroy(graph);
-                throw Error(CPK_ERR_HIP, "solver loop did not terminate");
-            }
-        }
-        if (exec) {
-            CPK_HIP(hipGraphExecDestroy(exec));
-            CPK_HIP(hipGraphDestroy(graph));
+            if (h.k > guard) throw Error(CPK_ERR_HIP, "solver loop did not terminate");
         }
     }
 
@@ -1342,9 +1366,7 @@ void SolveCore::gmres(const double *b, double *xy, cpk_stats *stats) {
     const int64_t hcap = (int64_t)(std::ceil(std::min(itmax, 1.0e8) / (double)R) * R) + 4;
     setup_state(hcap, R);
     DState *st = dst.p;
-    DBuf<double> Vb;
-    Vb.alloc((size_t)(R + 1) * N);
-    double *V = Vb.p;
+    double *V = ring((size_t)(R + 1));
     double *UT = vec(0), *Wv = vec(1), *TMP = vec(2);
     CPK_HIP(hipMemsetAsync(xy, 0, N * sizeof(double), c.stream));
     const double outermax = std::ceil(itmax / (double)R);
@@ -1409,10 +1431,7 @@ void SolveCore::dqgmres(const double *b, double *xy, cpk_stats *stats) {
     const int64_t hcap = (int64_t)std::min(itmax, 1.0e8) + 4;
     setup_state(hcap, Mm);
     DState *st = dst.p;
-    DBuf<double> Vb, PVb;
-    Vb.alloc((size_t)M1 * N);
-    PVb.alloc((size_t)M1 * N);
-    double *V = Vb.p, *PV = PVb.p;
+    double *V = ring((size_t)M1), *PV = ring((size_t)M1);
     double *UT = vec(0), *Wv = vec(1);
     CPK_HIP(hipMemsetAsync(xy, 0, N * sizeof(double), c.stream));
     if (print) printf("\n**** Constraint-preconditioned version of DQGMRES - mem = %lld ****\n\n", (long long)Mm);
@@ -1447,11 +1466,40 @@ void SolveCore::dqgmres(const double *b, double *xy, cpk_stats *stats) {
 }
 
 // ==============================================================================================
+// The cached solver of (method, operators, vectors, captured properties); see SolveCore.
+static std::string solver_key(const Ctx &c, const Precond &M, const DMat &AC, int method, const cpk_opts *o,
+                              const double *d_b, const double *d_xy) {
+    char buf[512];
+    const double restart = o && o->has_restart ? o->restart : 50, mem = o && o->has_mem ? o->mem : 50;
+    const double itmax = o && o->has_itmax ? o->itmax : -1;
+    snprintf(buf, sizeof buf, "%d|%llu|%p|%p|%p|%p|%.17g|%.17g|%.17g|%.17g|%.17g|%.17g|%s|%s", method,
+             (unsigned long long)AC.gen, (const void *)d_b, (const void *)d_xy, (const void *)c.partials.p,
+             (const void *)c.counter.p, M.nitref, M.force_itref, M.itref_tol, restart, mem,
+             method == CPK_DQGMRES ? itmax : 0.0, getenv("CPK_BATCH") ? getenv("CPK_BATCH") : "",
+             getenv("CPK_NO_GRAPH") ? getenv("CPK_NO_GRAPH") : "");
+    return buf;
+}
+
+static SolveCore &solver_for(Ctx &c, Precond &M, const DMat &AC, int method, const cpk_opts *opts,
+                             const double *d_b = nullptr, const double *d_xy = nullptr) {
+    const std::string key = solver_key(c, M, AC, method, opts, d_b, d_xy);
+    for (auto &e : M.solvers)
+        if (e.first == key) {
+            auto *s = static_cast<SolveCore *>(e.second.get());
+            s->reset(opts);
+            return *s;
+        }
+    if (M.solvers.size() >= 4) M.solvers.erase(M.solvers.begin());  // bounded: oldest out
+    std::shared_ptr<void> sp(new SolveCore(c, M, AC, method, opts));
+    M.solvers.emplace_back(key, sp);
+    return *static_cast<SolveCore *>(sp.get());
+}
+
 void method_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, Precond &M, const cpk_opts *opts,
                          double *d_xy, cpk_stats *stats) {
     if (method < CPK_CG || method > CPK_DQGMRES) throw Error(CPK_ERR_ARGS, "unknown method");
     CPK_HIP(hipEventRecord(c.ev0, c.stream));
-    SolveCore s(c, M, AC, method, opts);
+    SolveCore &s = solver_for(c, M, AC, method, opts, d_b, d_xy);
     switch (method) {
     case CPK_MINRES: s.minres_like(0, d_b, d_xy, stats); break;
     case CPK_CGLANCZOS: s.minres_like(1, d_b, d_xy, stats); break;

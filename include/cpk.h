@@ -104,7 +104,8 @@ int cpk_abi_version(void);
 /* ---- context: device, streams, RCCL communicator ------------------------------------- */
 /* Fill `id` (128 bytes) with an RCCL unique id on rank 0; broadcast it to the other ranks. */
 int cpk_get_unique_id(unsigned char id[128]);
-/* device < 0: use the current device.  nranks == 1: no communicator (unique_id may be NULL). */
+/* device < 0: use the current device.  nranks == 1 and unique_id == NULL: no communicator.
+ * With a unique_id the context runs the distributed path even for nranks == 1. */
 int cpk_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id, cpk_ctx *out);
 /* Single-GPU rehearsal of the distributed path: `nranks` ranks as host threads of one process,
  * all on one device, exchanging through a shared HBM buffer instead of RCCL (RCCL refuses two

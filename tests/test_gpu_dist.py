@@ -148,3 +148,23 @@ def test_dist_device_vectors_synthetic():
         assert sh and it == st1["niters"]
         assert np.max(np.abs(h - st1["residHistory"])) <= 1e-8 * st1["residHistory"][0]
     assert np.linalg.norm(x - x1) <= 1e-8 * np.linalg.norm(x1)
+
+
+def test_rccl_one_rank_graph_capture():
+    """The RCCL transport and hipGraph capture of its collectives, on the one GPU available:
+    a 1-rank communicator runs the distributed path (allreduce epilogues captured in the
+    iteration graph).  With one rank every sum is the local one, so the answer is bit-identical
+    to the single-GPU path."""
+    import cpkrylov_amd as cpk
+    Pd = F.load("cvxqp1_m")
+    opts = dict(F.EXPROG_OPTS)
+    x1, s1, f1 = cpk.reg_cpkrylov(cpk.cpminres, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts)
+    ctx = cpk.Context(device=0, rank=0, nranks=1, unique_id=cpk.get_unique_id())
+    try:
+        x2, s2, f2 = cpk.reg_cpkrylov(cpk.cpminres, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts, ctx=ctx)
+        assert s2["niters"] == s1["niters"] and f2 == f1
+        assert np.array_equal(s2["residHistory"], s1["residHistory"])
+        assert np.array_equal(x2, x1)
+        del s2
+    finally:
+        ctx.close()
