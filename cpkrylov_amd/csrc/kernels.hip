@@ -141,7 +141,8 @@ struct EpiStore {
     const int *run;
     __device__ bool skip() const { return run && *run == 0; }
     __device__ const double *xvec(const double *x) const { return x; }
-    __device__ void row(int64_t r, double acc) { y[r] = acc; }
+    __device__ double pre(int64_t) const { return 0.0; }
+    __device__ void row(int64_t r, double acc, double) { y[r] = acc; }
     __device__ void finish() {}
 };
 struct EpiResid {
@@ -151,8 +152,8 @@ struct EpiResid {
     const int *run, *active;
     __device__ bool skip() const { return cpk::skip(run, active); }
     __device__ const double *xvec(const double *x) const { return x; }
-    __device__ void row(int64_t i, double acc) {
-        double xi = xin[i];
+    __device__ double pre(int64_t i) const { return xin[i]; }
+    __device__ void row(int64_t i, double acc, double xi) {
         if (i >= neg_from) xi = -xi;
         r[i] = xi - acc;
     }
@@ -169,8 +170,8 @@ struct EpiResidNorm {
     double rr = 0.0, xx = 0.0;
     __device__ bool skip() const { return cpk::skip(run, active); }
     __device__ const double *xvec(const double *x) const { return x; }
-    __device__ void row(int64_t i, double acc) {
-        double xi = xin[i];
+    __device__ double pre(int64_t i) const { return xin[i]; }
+    __device__ void row(int64_t i, double acc, double xi) {
         if (i >= neg_from) xi = -xi;
         double ri = xi - acc;
         r[i] = ri;
@@ -191,13 +192,14 @@ struct EpiResidNorm {
 static inline int grid_of(const DMat &A) { return (int)A.nblk; }
 
 template <class Epi>
-static void spmv_launch(Ctx &c, const DMat &A, const double *x, int64_t col_min, const Epi &e) {
+static void spmv_launch(Ctx &c, const DMat &A, const double *x, int64_t col_min, const Epi &e, bool reduces = false) {
+    const unsigned grid = spmv_grid(A.nblk, reduces);
     if (A.halo())
-        hipLaunchKernelGGL((spmv_stream<Epi, true>), dim3(grid_of(A)), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
-                           A.val.p, A.blk.p, x, col_min, e, (const double *)A.rbuf.p, A.nloc);
+        hipLaunchKernelGGL((spmv_stream<Epi, true>), dim3(grid), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
+                           A.val.p, A.blk.p, A.nblk, x, col_min, e, (const double *)A.rbuf.p, A.nloc);
     else
-        hipLaunchKernelGGL((spmv_stream<Epi, false>), dim3(grid_of(A)), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
-                           A.val.p, A.blk.p, x, col_min, e, (const double *)nullptr, (int64_t)0);
+        hipLaunchKernelGGL((spmv_stream<Epi, false>), dim3(grid), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
+                           A.val.p, A.blk.p, A.nblk, x, col_min, e, (const double *)nullptr, (int64_t)0);
     CPK_HIP(hipGetLastError());
 }
 
@@ -279,7 +281,7 @@ void launch_spmv_resid_norm(Ctx &c, const DMat &A, const double *xin, int64_t ne
         c.ensure_partials((size_t)A.nblk * 2);
         EpiResidNorm e{xin, neg_from, r, tol, active_out, RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr},
                        run, active};
-        spmv_launch(c, A, y, 0, e);
+        spmv_launch(c, A, y, 0, e, true);
     }
     if (dist) {
         c.comm->allreduce_sum(c.red.p, 2, c.stream);
@@ -380,20 +382,40 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
 // contiguously.  Each row still subtracts its terms in the reference's order, one rounding per
 // product and per subtraction, so the result is bit-identical to the direct path.
 // LDS image of a staged block (dynamic shared memory, sized per launch):
-//   double w[R] | double v[CAP + 4] | int16 c[CAP + 4] | int16 p[R + 1] | int16 lv[R + 1]
+//   double w[R] | double v[CAP + 4] | int16 c[CAP + 4] | int16 p[R + 1] | int16 lv[R + 1] | int16 ps[R + 1]
 struct SweepLds {
     double *w, *v;
-    int16_t *c, *p, *lv;
+    int16_t *c, *p, *lv, *ps;
     __device__ SweepLds(char *smem, int R, int CAP) {
         w = reinterpret_cast<double *>(smem);
         v = w + R;
         c = reinterpret_cast<int16_t *>(v + CAP + 4);
         p = c + CAP + 4;
         lv = p + R + 1;
+        ps = lv + R + 1;
     }
 };
 size_t sweep_lds_bytes(int R, int CAP) {
-    return ((size_t)8 * R + 10 * ((size_t)CAP + 4) + 4 * ((size_t)R + 1) + 15) & ~(size_t)15;
+    return ((size_t)8 * R + 10 * ((size_t)CAP + 4) + 6 * ((size_t)R + 1) + 15) & ~(size_t)15;
+}
+
+// Outside-block prefix: a row's leading terms that refer to rows finished by earlier launches
+// are already products in LDS (c < 0).  Subtracting them here, every row at once, takes them
+// off the level-by-level critical path; the level phase then continues each row from ps[k].
+// Same operations in the same order, so the result is bit-identical.  This is what makes the
+// upper rounds cheap: a separator row's many references into the subtrees below are all
+// outside its block.
+template <int TPB>
+__device__ __forceinline__ void fold_prefix(SweepLds &S, int nr) {
+    for (int i = threadIdx.x; i < nr; i += TPB) {
+        int e = S.p[i];
+        const int e1 = S.p[i + 1];
+        double acc = S.w[i];
+        while (e < e1 && S.c[e] < 0) acc -= S.v[e++];
+        S.w[i] = acc;
+        S.ps[i] = (int16_t)e;
+    }
+    __syncthreads();
 }
 
 // The level phase, out of LDS.  Per level every thread takes whole rows and consumes a row's
@@ -402,7 +424,8 @@ size_t sweep_lds_bytes(int R, int CAP) {
 // selects replace predicated loads, so a row costs a handful of instructions.  The terms are
 // still subtracted one at a time in the reference's order.  skip_first: the first level holds
 // only rows without entries (their values are already in place), as in round 0 forward.
-template <int TPB, bool BWD>
+// PS: rows start at ps[k] (after fold_prefix) instead of p[k].
+template <int TPB, bool BWD, bool PS = false>
 __device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_first = false) {
     int l = BWD ? nl - 1 : 0;
     int li0 = 0;
@@ -416,7 +439,7 @@ __device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_firs
         for (int k = a + (int)threadIdx.x; k < z; k += TPB) {
             const int e1 = S.p[k + 1];
             double acc = S.w[k];
-            for (int e = S.p[k]; e < e1; e += 4) {
+            for (int e = PS ? S.ps[k] : S.p[k]; e < e1; e += 4) {
                 int c[4];
                 double v[4], x[4];
 #pragma unroll
@@ -463,14 +486,21 @@ __global__ __launch_bounds__(TPB) void sptrsv_fwd_kernel(
         for (int l = tid; l <= l1 - l0; l += TPB) S.lv[l] = (int16_t)(lvl_row[l0 + l] - r0);
 #pragma unroll 4
         for (int e = tid; e < ne; e += TPB) {
-            const int32_t c = col[e0 + e];
-            const double v = val[e0 + e];
+            const int32_t c = __builtin_nontemporal_load(col + e0 + e);  // streamed once per sweep
+            const double v = __builtin_nontemporal_load(val + e0 + e);
             const bool local = c >= r0 && c < r1;
             S.c[e] = local ? (int16_t)(c - r0) : (int16_t)-1;
             S.v[e] = local ? v : v * w[c];
         }
         __syncthreads();
-        if (MODE == 0) sweep_levels<TPB, false>(S, l1 - l0, skip_first != 0);
+        if (MODE == 0) {
+            if (skip_first) {
+                sweep_levels<TPB, false>(S, l1 - l0, true);  // round 0: no outside references
+            } else {
+                fold_prefix<TPB>(S, nr);
+                sweep_levels<TPB, false, true>(S, l1 - l0);
+            }
+        }
         for (int i = tid; i < nr; i += TPB) w[r0 + i] = S.w[i];
         return;
     }
@@ -513,14 +543,15 @@ __global__ __launch_bounds__(TPB) void sptrsv_bwd_kernel(
         for (int l = tid; l <= l1 - l0; l += TPB) S.lv[l] = (int16_t)(lvl_row[l0 + l] - r0);
 #pragma unroll 4
         for (int e = tid; e < ne; e += TPB) {
-            const int32_t c = col[e0 + e];
-            const double v = val[e0 + e];
+            const int32_t c = __builtin_nontemporal_load(col + e0 + e);  // streamed once per sweep
+            const double v = __builtin_nontemporal_load(val + e0 + e);
             const bool local = c >= r0 && c < r1;
             S.c[e] = local ? (int16_t)(c - r0) : (int16_t)-1;
             S.v[e] = local ? v : v * w[c];
         }
         __syncthreads();
-        sweep_levels<TPB, true>(S, l1 - l0);
+        fold_prefix<TPB>(S, nr);
+        sweep_levels<TPB, true, true>(S, l1 - l0);
         for (int i = tid; i < nr; i += TPB) {
             const double z = S.w[i];
             w[r0 + i] = z;
@@ -591,7 +622,8 @@ __global__ __launch_bounds__(TPB) void sptrsv_pipe_kernel(
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
             const int e = tid + j * TPB;
-            if (e < ne) cc[j] = col[e0 + e], vv[j] = val[e0 + e];
+            if (e < ne)  // streamed once per sweep: non-temporal, keeps L2 for the gathered vector
+                cc[j] = __builtin_nontemporal_load(col + e0 + e), vv[j] = __builtin_nontemporal_load(val + e0 + e);
         }
     };
     int64_t b = blk0 + blockIdx.x;

@@ -147,10 +147,11 @@ struct EpiKrylov {
         xsel = f.select(st, base);
         return xsel;
     }
-    __device__ void row(int64_t r, double acc) {
+    __device__ double pre(int64_t r) const { return xsel[r]; }
+    __device__ void row(int64_t r, double acc, double xr) {
         y[r] = acc;
-        if (r < n) dn += acc * xsel[r];
-        else dm += acc * xsel[r];
+        if (r < n) dn += acc * xr;
+        else dm += acc * xr;
     }
     __device__ void finish() {
         double v[2] = {dn, dm}, tot[2];

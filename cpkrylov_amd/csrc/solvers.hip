@@ -147,13 +147,14 @@ void launch_krylov_spmv(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n
     }
     if (dist) CPK_HIP(hipMemsetAsync(c.red.p, 0, 2 * sizeof(double), c.stream));
     EpiKrylov<P> e{st, nullptr, y, n, RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr}, pol};
+    const unsigned grid = spmv_grid(AC.nblk, true);
     if (AC.halo())
-        hipLaunchKernelGGL((spmv_stream<EpiKrylov<P>, true>), dim3((unsigned)AC.nblk), dim3(kBlock), 0, c.stream,
-                           AC.ptr.p, AC.col.p, AC.val.p, AC.blk.p, (const double *)nullptr, (int64_t)0, e,
+        hipLaunchKernelGGL((spmv_stream<EpiKrylov<P>, true>), dim3(grid), dim3(kBlock), 0, c.stream, AC.ptr.p,
+                           AC.col.p, AC.val.p, AC.blk.p, AC.nblk, (const double *)nullptr, (int64_t)0, e,
                            (const double *)AC.rbuf.p, AC.nloc);
     else
-        hipLaunchKernelGGL((spmv_stream<EpiKrylov<P>, false>), dim3((unsigned)AC.nblk), dim3(kBlock), 0, c.stream,
-                           AC.ptr.p, AC.col.p, AC.val.p, AC.blk.p, (const double *)nullptr, (int64_t)0, e,
+        hipLaunchKernelGGL((spmv_stream<EpiKrylov<P>, false>), dim3(grid), dim3(kBlock), 0, c.stream, AC.ptr.p,
+                           AC.col.p, AC.val.p, AC.blk.p, AC.nblk, (const double *)nullptr, (int64_t)0, e,
                            (const double *)nullptr, (int64_t)0);
     if (dist) {
         c.comm->allreduce_sum(c.red.p, 2, c.stream);

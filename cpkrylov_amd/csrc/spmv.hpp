@@ -15,31 +15,65 @@
 namespace cpk {
 
 // HALO: distributed rows (DistCsr); column c >= nloc reads the allgathered halo xg[c - nloc].
+// A workgroup handles row blocks blockIdx.x, blockIdx.x + gridDim.x, ...: launched with one
+// block per workgroup for plain products, and with a bounded grid when the epilogue reduces
+// (fewer arrivals on the reduction ticket).
 template <class Epi, bool HALO = false>
 __global__ __launch_bounds__(kBlock) void spmv_stream(const uint32_t *__restrict__ ptr,
                                                       const int32_t *__restrict__ col,
                                                       const double *__restrict__ val,
-                                                      const int32_t *__restrict__ blk,
+                                                      const int32_t *__restrict__ blk, int64_t nblk,
                                                       const double *x, int64_t col_min, Epi epi,
                                                       const double *xg, int64_t nloc) {
     __shared__ double prod[kSpmvCap];
     if (epi.skip()) return;
     x = epi.xvec(x);
-    const int64_t r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
-    const uint32_t e0 = ptr[r0], e1 = ptr[r1];
     const int tid = threadIdx.x;
+    for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    if (b != blockIdx.x) __syncthreads();  // prod[] of the previous block fully consumed
+    const int64_t r0 = blk[b], r1 = blk[b + 1];
+    const uint32_t e0 = ptr[r0], e1 = ptr[r1];
     if (e1 - e0 <= (uint32_t)kSpmvCap) {
-        for (uint32_t e = e0 + tid; e < e1; e += kBlock) {
-            const int32_t c = col[e];
-            const double xv = (!HALO || c < nloc) ? x[c] : xg[c - nloc];
-            prod[e - e0] = (c >= col_min) ? val[e] * xv : 0.0;
+        // phase 1, fully unrolled so every load of a thread is in flight at once: the (col, val)
+        // stream and this thread's row pointers first, then the dependent x gathers
+        constexpr int EPT = kSpmvCap / kBlock, RPT = kSpmvMaxRows / kBlock;
+        int32_t cc[EPT];
+        double vv[EPT], xv[EPT];
+        uint32_t pa[RPT], pb[RPT];
+        double pr[RPT];  // the epilogue's per-row operand (e.g. x(i) of r = x - A*y), prefetched
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            const uint32_t e = e0 + tid + j * kBlock;
+            // the matrix is streamed once per launch: non-temporal, so it does not evict the
+            // gathered vector from L2
+            cc[j] = e < e1 ? __builtin_nontemporal_load(col + e) : 0;
+            vv[j] = e < e1 ? __builtin_nontemporal_load(val + e) : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const int64_t r = r0 + tid + j * kBlock;
+            if (r < r1) pa[j] = ptr[r], pb[j] = ptr[r + 1], pr[j] = epi.pre(r);
+        }
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            const int32_t c = cc[j];
+            xv[j] = (!HALO || c < nloc) ? x[c] : xg[c - nloc];
+        }
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            const uint32_t e = e0 + tid + j * kBlock;
+            if (e < e1) prod[e - e0] = (cc[j] >= col_min) ? vv[j] * xv[j] : 0.0;
         }
         __syncthreads();
-        for (int64_t r = r0 + tid; r < r1; r += kBlock) {
-            double acc = 0.0;
-            const uint32_t a = ptr[r] - e0, b = ptr[r + 1] - e0;
-            for (uint32_t e = a; e < b; e++) acc += prod[e];
-            epi.row(r, acc);
+        // phase 2: whole rows per thread, summed in column order from 0.0
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const int64_t r = r0 + tid + j * kBlock;
+            if (r < r1) {
+                double acc = 0.0;
+                for (uint32_t e = pa[j] - e0; e < pb[j] - e0; e++) acc += prod[e];
+                epi.row(r, acc, pr[j]);
+            }
         }
     } else {
         double acc = 0.0;  // one long row (r1 == r0 + 1)
@@ -55,9 +89,16 @@ __global__ __launch_bounds__(kBlock) void spmv_stream(const uint32_t *__restrict
                 for (uint32_t e = 0; e < c1 - c0; e++) acc += prod[e];
             __syncthreads();
         }
-        if (tid == 0) epi.row(r0, acc);
+        if (tid == 0) epi.row(r0, acc, epi.pre(r0));
+    }
     }
     epi.finish();
+}
+
+// grid of a launch: one row block per workgroup, or a bounded grid for reducing epilogues
+constexpr int64_t kSpmvRedGrid = 2048;
+inline unsigned spmv_grid(int64_t nblk, bool reduces) {
+    return (unsigned)(reduces ? std::min<int64_t>(nblk, kSpmvRedGrid) : nblk);
 }
 
 }  // namespace cpk
