@@ -186,7 +186,7 @@ static std::unique_ptr<cpk_ctx_s> ctx_base(int device, int rank, int nranks) {
     CPK_HIP(hipEventCreate(&c.ev0));
     CPK_HIP(hipEventCreate(&c.ev1));
     c.ensure_partials(4096);
-    c.red.alloc(64);
+    c.red.alloc(4096);  // distributed reductions (up to 2047 Arnoldi window pairs)
     return ctx;
 }
 
@@ -420,10 +420,7 @@ static void check_method_dims(cpk_mat A, cpk_mat C, cpk_pc M) {
     if (A->h.nrows != M->p->gn || C->h.nrows != M->p->gm) throw Error(CPK_ERR_DIM, "A, C and M dimensions disagree");
 }
 
-static void check_dist_method(const Ctx &c, int method) {
-    if (c.dist() && (method == CPK_GMRES || method == CPK_DQGMRES))
-        throw Error(CPK_ERR_UNSUPPORTED, "cpgmres/cpdqgmres are single-GPU in this version (DESIGN.md section 7)");
-}
+static void check_dist_method(const Ctx &, int) {}
 
 int cpk_method_solve_device(cpk_ctx ctx, int method, const double *d_b, cpk_mat A, cpk_mat C, cpk_pc M,
                             const cpk_opts *opts, double *d_xy, cpk_stats *stats) {

@@ -118,7 +118,7 @@ struct DFactor {
     DBuf<int32_t> meta;     // [nblk][8]: r0, r1, l0, l1, fwd e0, e1, bwd e0, e1
     bool pipelined = true;  // round 0 through the persistent pipelined kernel
     std::vector<int64_t> round_ptr;  // host copy: blocks per round
-    int sweep_rows[2] = {192, 2048}, sweep_cap[2] = {576, 8192}, sweep_threads[2] = {64, 512};  // round 0 / rest
+    int sweep_rows[2] = {192, 1024}, sweep_cap[2] = {576, 4096}, sweep_threads[2] = {64, 512};  // round 0 / rest
     size_t bytes() const {
         return fptr.bytes() + fcol.bytes() + fval.bytes() + bptr.bytes() + bcol.bytes() + bval.bytes() + D.bytes() +
                perm.bytes() + blk_lvl.bytes() + lvl_row.bytes() + meta.bytes();
@@ -137,7 +137,7 @@ size_t sweep_lds_bytes(int R, int CAP);
 // CPK_SWEEP="rows,cap,threads" overrides the default.
 // CPK_SWEEP="R0,CAP0,T0,R1,CAP1,T1": round 0 / upper rounds.
 struct SweepConfig {
-    int rows[2] = {192, 2048}, cap[2] = {576, 8192}, threads[2] = {64, 512};
+    int rows[2] = {192, 1024}, cap[2] = {576, 4096}, threads[2] = {64, 512};
     int sub0 = 0;  // round-0 subtree cap (0: cap[0])
 };
 SweepConfig sweep_config();

@@ -767,6 +767,7 @@ static void fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
         case 64: fwd_round<64, MODE>(c, F, r, xin, neg_from, w, run, active); break;
         case 128: fwd_round<128, MODE>(c, F, r, xin, neg_from, w, run, active); break;
         case 512: fwd_round<512, MODE>(c, F, r, xin, neg_from, w, run, active); break;
+        case 1024: fwd_round<1024, MODE>(c, F, r, xin, neg_from, w, run, active); break;
         default: fwd_round<256, MODE>(c, F, r, xin, neg_from, w, run, active); break;
         }
     }
@@ -794,6 +795,8 @@ void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
         case 257: bwd_round<128, true>(c, F, r, w, out, run, active); break;
         case 1024: bwd_round<512, false>(c, F, r, w, out, run, active); break;
         case 1025: bwd_round<512, true>(c, F, r, w, out, run, active); break;
+        case 2048: bwd_round<1024, false>(c, F, r, w, out, run, active); break;
+        case 2049: bwd_round<1024, true>(c, F, r, w, out, run, active); break;
         case 513: bwd_round<256, true>(c, F, r, w, out, run, active); break;
         default: bwd_round<256, false>(c, F, r, w, out, run, active); break;
         }

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -764,6 +765,17 @@ __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double
     }
     __syncthreads();
     if (!s_last) return;
+    if (rb.defer) {  // distributed mode: local window sums out; arnoldi_fin_kernel after the allreduce
+        for (int64_t j = 0; j < 2 * win.nv; j++) {
+            double a[1] = {0.0};
+            for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x)
+                a[0] += ld_agent(rb.partials + (size_t)b * 2 * maxv + j);
+            block_sum<1>(a);
+            if (threadIdx.x == 0) rb.defer[j] = a[0];
+        }
+        if (threadIdx.x == 0) __hip_atomic_store(rb.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     __shared__ double hv[2];
     if (ring && threadIdx.x == 0) {  // fresh ring row for H(kk, .)
         for (int64_t c = 1; c <= st->mem + 2; c++) Hd(st, kk, c) = 0.0;
@@ -784,6 +796,35 @@ __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double
         __syncthreads();
     }
     if (threadIdx.x == 0) __hip_atomic_store(rb.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// distributed mode: H(j, k) from the allreduced window sums (same additions as above)
+__global__ void arnoldi_fin_kernel(DState *st, int64_t ring, const double *tot) {
+    if (threadIdx.x || blockIdx.x || !st->running) return;
+    const Window win = window(st, ring);
+    const int64_t kk = win.kk;
+    if (ring)
+        for (int64_t c = 1; c <= st->mem + 2; c++) Hd(st, kk, c) = 0.0;
+    for (int64_t j = 0; j < win.nv; j++) {
+        const int64_t jj = win.jlo + j;
+        const double h = tot[2 * j] + tot[2 * j + 1];
+        if (ring) Hd(st, jj, 2 + kk - jj) = h;
+        else Hg(st, jj, kk) = h;
+    }
+}
+
+// the window dots of one Arnoldi step (with the distributed allreduce when needed)
+static void launch_arnoldi_dots(Ctx &c, DState *st, double *V, const double *w, const double *ut, int64_t n, int64_t N,
+                                int64_t ring, int64_t maxv) {
+    const bool dist = c.dist();
+    if (dist && (size_t)(2 * maxv) > c.red.n) throw Error(CPK_ERR_UNSUPPORTED, "Arnoldi window too wide for the distributed reduction buffer");
+    if (dist) CPK_HIP(hipMemsetAsync(c.red.p, 0, 2 * maxv * sizeof(double), c.stream));
+    hipLaunchKernelGGL(arnoldi_dots_kernel, dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, st, V, w, ut, n, N, ring, maxv,
+                       RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr});
+    if (dist) {
+        c.comm->allreduce_sum(c.red.p, (size_t)(2 * maxv), c.stream);
+        hipLaunchKernelGGL(arnoldi_fin_kernel, dim3(1), dim3(64), 0, c.stream, st, ring, (const double *)c.red.p);
+    }
 }
 
 // V(:,k+1) -= H(j,k) V(:,j) for the window in order; H(k+1,k) = sqrt(dot(u,V_{k+1}) + dot(t,Q_{k+1}));
@@ -1085,33 +1126,57 @@ struct SolveCore {
         CPK_HIP(hipStreamSynchronize(c.stream));
     }
 
-    // replay `body` (one iteration) in batches until the device sets `stop`.  The batch graph of
-    // a loop site is captured once and replayed by later calls with the same key.
+    // replay `body` (one iteration) in batches until the device sets `stop`.  A batch is a
+    // captured graph of b iterations (b a power of two <= batch), captured once per loop site
+    // and size and replayed by later calls with the same key.  After the first batch the size
+    // follows the observed convergence rate, so the batch that crosses the tolerance carries
+    // few no-op iterations (every kernel tests the device-side `running` flag, so the size
+    // only affects time, never results).
+    hipGraphExec_t graph_for(size_t site, int b, const std::function<void()> &body) {
+        const size_t slot = site * 8 + (size_t)__builtin_ctz((unsigned)b);
+        if (graphs.size() <= slot) graphs.resize(slot + 1, {nullptr, nullptr});
+        if (!graphs[slot].second) {
+            hipGraph_t graph = nullptr;
+            CPK_HIP(hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
+            for (int i = 0; i < b; i++) body();
+            CPK_HIP(hipStreamEndCapture(c.stream, &graph));
+            graphs[slot].first = graph;
+            CPK_HIP(hipGraphInstantiate(&graphs[slot].second, graph, nullptr, nullptr, 0));
+        }
+        return graphs[slot].second;
+    }
+
+    static int pow2_at_least(double v, int cap) {
+        int b = 1;
+        while (b < cap && b < v) b <<= 1;
+        return b;
+    }
+
     void loop(const std::function<void()> &body, const std::function<void()> &printer, size_t site = 0) {
         pull();
         if (h.stop) return;
-        hipGraphExec_t exec = nullptr;
-        if (use_graph) {
-            if (graphs.size() <= site) graphs.resize(site + 1, {nullptr, nullptr});
-            if (!graphs[site].second) {
-                hipGraph_t graph = nullptr;
-                CPK_HIP(hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
-                for (int b = 0; b < batch; b++) body();
-                CPK_HIP(hipStreamEndCapture(c.stream, &graph));
-                graphs[site].first = graph;
-                CPK_HIP(hipGraphInstantiate(&graphs[site].second, graph, nullptr, nullptr, 0));
-            }
-            exec = graphs[site].second;
-        }
         const int64_t guard = h.k + (int64_t)std::min(itmax, 4.0e9) + 2 * batch + 2;
+        int b = pow2_at_least(batch, 64);
+        const bool adapt = getenv("CPK_BATCH") == nullptr;
         for (;;) {
-            if (exec) CPK_HIP(hipGraphLaunch(exec, c.stream));
+            const double res0 = h.residNorm;
+            const int64_t k0 = h.k;
+            if (use_graph) CPK_HIP(hipGraphLaunch(graph_for(site, b, body), c.stream));
             else
-                for (int b = 0; b < batch; b++) body();
+                for (int i = 0; i < b; i++) body();
             pull();
             if (print && printer) printer();
             if (h.stop) break;
             if (h.k > guard) throw Error(CPK_ERR_HIP, "solver loop did not terminate");
+            b = pow2_at_least(batch, 64);
+            const double res = h.residNorm, tol = h.stopTol;
+            if (adapt && h.k > k0 && res > 0 && res0 > res && tol > 0 && tol < res) {
+                // geometric model of the residual over the last batch: iterations still needed
+                const double rate = std::log(res / res0) / (double)(h.k - k0);
+                const double rem = std::log(tol / res) / rate;
+                if (rem > 0 && rem < 1e6) b = pow2_at_least(std::ceil(rem), b);
+            }
+            if (itmax - (double)h.k < b) b = pow2_at_least(std::max(1.0, itmax - (double)h.k), b);
         }
     }
 
@@ -1398,8 +1463,7 @@ void SolveCore::gmres(const double *b, double *xy, cpk_stats *stats) {
         auto body = [&]() {
             launch_krylov_spmv(c, AC, st, UT, n, PolArnoldiSpmv{V, N, 0});
             M.apply(UT, n, Wv, &st->running);
-            hipLaunchKernelGGL(arnoldi_dots_kernel, dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, st, V, Wv, UT, n, N,
-                               (int64_t)0, R, RedBuf{c.partials.p, c.counter.p});
+            launch_arnoldi_dots(c, st, V, Wv, UT, n, N, 0, R);
             launch_ewred<2>(c, N, ArnoldiOrth{st, V, UT, n, N, 0, Window{}, nullptr});
             launch_ew(c, N, GmresNormalize{st, V, N});
         };
@@ -1454,8 +1518,7 @@ void SolveCore::dqgmres(const double *b, double *xy, cpk_stats *stats) {
     auto body = [&]() {
         launch_krylov_spmv(c, AC, st, UT, n, PolArnoldiSpmv{V, N, M1});
         M.apply(UT, n, Wv, &st->running);
-        hipLaunchKernelGGL(arnoldi_dots_kernel, dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, st, V, Wv, UT, n, N, M1,
-                           Mm, RedBuf{c.partials.p, c.counter.p});
+        launch_arnoldi_dots(c, st, V, Wv, UT, n, N, M1, Mm);
         launch_ewred<2>(c, N, ArnoldiOrth{st, V, UT, n, N, M1, Window{}, nullptr});
         launch_ew(c, N, DqgmresDirection{st, V, PV, xy, n, N});
     };
@@ -1473,9 +1536,9 @@ static std::string solver_key(const Ctx &c, const Precond &M, const DMat &AC, in
     char buf[512];
     const double restart = o && o->has_restart ? o->restart : 50, mem = o && o->has_mem ? o->mem : 50;
     const double itmax = o && o->has_itmax ? o->itmax : -1;
-    snprintf(buf, sizeof buf, "%d|%llu|%p|%p|%p|%p|%.17g|%.17g|%.17g|%.17g|%.17g|%.17g|%s|%s", method,
+    snprintf(buf, sizeof buf, "%d|%llu|%p|%p|%p|%p|%p|%.17g|%.17g|%.17g|%.17g|%.17g|%.17g|%s|%s", method,
              (unsigned long long)AC.gen, (const void *)d_b, (const void *)d_xy, (const void *)c.partials.p,
-             (const void *)c.counter.p, M.nitref, M.force_itref, M.itref_tol, restart, mem,
+             (const void *)c.counter.p, (const void *)c.red.p, M.nitref, M.force_itref, M.itref_tol, restart, mem,
              method == CPK_DQGMRES ? itmax : 0.0, getenv("CPK_BATCH") ? getenv("CPK_BATCH") : "",
              getenv("CPK_NO_GRAPH") ? getenv("CPK_NO_GRAPH") : "");
     return buf;

@@ -79,13 +79,18 @@ def test_dist_apply_bitexact(name, P, props):
         assert np.all(d[:nl] < S["n"]) and np.all(d[nl:] >= S["n"])
 
 
+DIST_CASES = [("cvxqp1_m", "minres", {}), ("cvxqp1_m", "cg", {}), ("cvxqp1_m", "cglanczos", {}),
+              ("cvxqp1_m", "symmlq", {}), ("cvxqp1_m", "dqgmres", {"mem": 2}),
+              ("cvxqp2_s", "gmres", {"restart": 20}), ("cvxqp2_s", "gmres", {"restart": 100}),
+              ("cvxqp2_s", "dqgmres", {"mem": 20}), ("cvxqp2_s", "dqgmres", {"mem": 100})]
+
+
 @pytest.mark.parametrize("P", [2, 3])
-@pytest.mark.parametrize("method", ["minres", "cg", "cglanczos", "symmlq"])
-def test_dist_reg_cpkrylov_matches_oracle(method, P):
+@pytest.mark.parametrize("name,method,extra", DIST_CASES)
+def test_dist_reg_cpkrylov_matches_oracle(name, method, extra, P):
     import cpkrylov_amd as cpk
-    name = "cvxqp1_m"
     Pd = F.load(name)
-    opts = dict(F.EXPROG_OPTS)
+    opts = dict(F.EXPROG_OPTS, **extra)
     fn = getattr(cpk, "cp" + method)
 
     def work(ctx, r):
@@ -100,7 +105,7 @@ def test_dist_reg_cpkrylov_matches_oracle(method, P):
     xo, so = O.reg_cpkrylov(method, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts, perm=perm)
     assert stats["niters"] == so["niters"]
     assert flag["solved"] == so["solved"]
-    bd = band(name, method, {}, perm)
+    bd = band(name, method, extra, perm)
     h0 = stats.get("residHistory", stats.get("cgresidHistory"))[0]
     for k in [k for k in so if k.endswith("History")]:
         assert len(stats[k]) == len(so[k]), k
