@@ -39,15 +39,30 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--size", type=int, default=10_000_000, help="total dofs N (S10: 10,000,000)")
-    ap.add_argument("--method", default="minres")
+    ap.add_argument("--config", choices=("s10", "s50"), default="s10",
+                    help="s10: symmetric 10M cpminres (the headline metric); s50: nonsymmetric 3x3-block "
+                         "50M cpdqgmres(40) (SURVEY.md section 8d config 5)")
+    ap.add_argument("--size", type=int, default=None, help="total dofs N (default 10M for s10, 50M for s50)")
+    ap.add_argument("--method", default=None)
+    ap.add_argument("--itmax", type=int, default=None, help="s50: iterations per step (default 120)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-reps", type=int, default=20)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE passes")
     ap.add_argument("--dist", action="store_true", help="run the distributed path even on one GPU (1-rank RCCL)")
     ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)
-    return ap.parse_args()
+    a = ap.parse_args()
+    s50 = a.config == "s50"
+    if a.size is None:
+        a.size = 50_000_000 if s50 else 10_000_000
+    if a.method is None:
+        a.method = "dqgmres" if s50 else "minres"
+    a.opts = dict(EXPROG_OPTS)
+    if s50:
+        a.opts.update(mem=40, restart=40, itmax=a.itmax or 120)
+    elif a.itmax:
+        a.opts["itmax"] = a.itmax
+    return a
 
 
 class _quiet_stdout:
@@ -84,10 +99,10 @@ def main():
 
     import cpkrylov_amd as cpk
     from cpkrylov_amd import _lib
-    from cpkrylov_amd.synthetic import saddle_system
+    from cpkrylov_amd.synthetic import nonsym_system, saddle_system
 
     t_setup = time.perf_counter()
-    S = saddle_system(N=args.size)
+    S = nonsym_system(N=args.size) if args.config == "s50" else saddle_system(N=args.size)
     n, m, N = S["n"], S["m"], S["N"]
     # N > 1 (or --dist): one distributed solve over all ranks (strong scaling), RCCL collectives
     # and halo exchanges inside the solver; every rank holds its row block
@@ -115,9 +130,9 @@ def main():
     shifted = C.c_int()
     _lib.check(_lib.lib.cpk_reg_shift_device(ctx.h, C.c_void_p(b.data_ptr()), A.h, B.h, Cm.h, M.h,
                                              C.c_void_p(b1.data_ptr()), C.c_void_p(xy0.data_ptr()), C.byref(shifted)))
-    opts = _lib.make_opts(EXPROG_OPTS)
+    opts = _lib.make_opts(args.opts)
     mid = _lib.METHODS[args.method]
-    cap = int(EXPROG_OPTS["itmax"]) + 4
+    cap = int(args.opts["itmax"]) + 64
     hist = np.zeros(cap)
     st = _lib.Stats()
     st.hist = hist.ctypes.data_as(C.POINTER(C.c_double))
@@ -172,7 +187,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not distributed:
         cpu, parity = cpu_baseline(S, b1.cpu().numpy(), M, args, hist_gpu, niters_last)
     pmc = None
-    if rank == 0 and world == 1 and not args.no_pmc and not distributed:
+    if rank == 0 and world == 1 and not args.no_pmc and not distributed and args.config == "s10":
         pmc = pmc_traffic(args)
         if pmc and "resid" in pmc:
             roofline["traffic"] = pmc["resid"]["bytes"]
@@ -181,12 +196,17 @@ def main():
     value = total_iters / dt
     if rank == 0:
         line = {
-            "metric": "Krylov iters/sec + SpMV GB/s (% HBM peak), cpminres 10M-dof, 1/2/4/8 GPU",
+            "metric": ("Krylov iters/sec + SpMV GB/s (% HBM peak), cpminres 10M-dof, 1/2/4/8 GPU"
+                       if args.config == "s10" else
+                       "Krylov iters/sec, cpdqgmres(40) 50M-dof nonsymmetric 3x3-block"),
             "value": round(value, 2), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"S10 synthetic symmetric saddle-point system, cp{args.method} to convergence "
-                                   "(cpk_exprog1 options), step = one method call",
+            "config": {"workload": (f"S10 synthetic symmetric saddle-point system, cp{args.method} to convergence "
+                                    "(cpk_exprog1 options), step = one method call" if args.config == "s10" else
+                                    f"S50 synthetic nonsymmetric 3x3-block saddle-point system, cp{args.method}"
+                                    f"(mem 40), step = one method call of at most {args.opts['itmax']} iterations "
+                                    "(cpk_exprog1 tolerances)"),
                        "N": N, "n": n, "m": m, "nnz_kp": M.info["nnz_kp"], "nnz_l": M.info["nnz_l"],
                        "sweep_launches": M.info["nrounds"], "elim_tree_depth": M.info["depth"],
                        "parallelism": f"rowblock{world}" if distributed else "single", "seed": S["seed"],
@@ -213,19 +233,19 @@ def cpu_baseline(S, b1, M_gpu, args, hist_gpu, niters_gpu):
     from oracle import oracle as O
     L, D, perm = M_gpu.export_factors()
     Mo = O.LDL2(S["G"], S["B"], -S["C"], perm=perm)  # the oracle's own factorization, same pivot order
-    Mo.set(nitref=EXPROG_OPTS["nitref"], itref_tol=EXPROG_OPTS["itref_tol"],
+    Mo.set(nitref=args.opts["nitref"], itref_tol=args.opts["itref_tol"],
            force_itref=1.0, residual_update=1.0)
     # probe two iterations to size a 10-30 s sample
     t = time.perf_counter()
-    O.method(args.method, b1, S["Q"], S["C"], Mo, dict(EXPROG_OPTS, itmax=2))
+    O.method(args.method, b1, S["Q"], S["C"], Mo, dict(args.opts, itmax=2))
     per_iter = (time.perf_counter() - t) / 3.0  # init M-apply + 2 iterations
-    itmax = int(max(2, min(EXPROG_OPTS["itmax"], args.cpu_seconds / max(per_iter, 1e-9))))
+    itmax = int(max(2, min(args.opts["itmax"], args.cpu_seconds / max(per_iter, 1e-9))))
     t = time.perf_counter()
-    x, y, st = O.method(args.method, b1, S["Q"], S["C"], Mo, dict(EXPROG_OPTS, itmax=itmax))
+    x, y, st = O.method(args.method, b1, S["Q"], S["C"], Mo, dict(args.opts, itmax=itmax))
     dt = time.perf_counter() - t
     it = int(st["niters"])
     cpu = {"value": round(it / dt, 4), "unit": "iters/s", "cores": 1, "kind": "port",
-           "sample": f"oracle cp{args.method} on S10 (same b1, same pivot order), {it} iterations "
+           "sample": f"oracle cp{args.method} on {args.config.upper()} (same b1, same pivot order), {it} iterations "
                      f"(itmax {itmax}, solved {bool(st['solved'])}), {dt:.1f} s, gcc -O2 single thread"}
     parity = None
     if st["solved"]:
@@ -245,8 +265,8 @@ def pmc_probe(args):
     SpMVs, then the forward and backward sweeps, round by round."""
     import cpkrylov_amd as cpk
     from cpkrylov_amd import _lib
-    from cpkrylov_amd.synthetic import saddle_system
-    S = saddle_system(N=args.size)
+    from cpkrylov_amd.synthetic import nonsym_system, saddle_system
+    S = nonsym_system(N=args.size) if args.config == "s50" else saddle_system(N=args.size)
     ctx = cpk.Context(device=0)
     A, Cm = cpk.Matrix(S["Q"], ctx), cpk.Matrix(S["C"], ctx)
     M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)

@@ -727,7 +727,7 @@ __device__ inline double &Hd(DState *st, int64_t j, int64_t kk) {  // H(j, kk), 
 
 // V(:,k+1) = w(1:n) ; Q(:,k+1) = Q(:,k) - w(n+1:N) ; H(j,k) = dot(V_j,u) + dot(Q_j,t) for the window
 // (cpgmres.m:212-215, cpdqgmres.m:479-484).  All window dots in one streaming pass.
-constexpr int kDotGroup = 8;
+constexpr int kDotGroup = 16;
 __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double *V, const double *w,
                                                               const double *ut, int64_t n, int64_t N, int64_t ring,
                                                               int64_t maxv, RedBuf rb) {
@@ -736,26 +736,41 @@ __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double
     const int64_t kk = win.kk;
     double *vnew = V + (ring ? (kk % ring) : kk) * N;
     const double *vk = V + win.slot(kk) * N;
-    // phase 0: new basis vector (fused with the first dot group)
+    // phase 0: new basis vector (fused with the first dot group).  A thread's indices grow, so
+    // it meets the [x; y] boundary at most once: one accumulator per vector, whose x-part
+    // sum is parked in accn when the thread crosses into the y-part (same additions, same
+    // order as separate x/y accumulators).
     for (int64_t g0 = 0; g0 < win.nv; g0 += kDotGroup) {
-        double acc[2 * kDotGroup];
+        double acc[kDotGroup], accn[kDotGroup];
 #pragma unroll
-        for (int j = 0; j < 2 * kDotGroup; j++) acc[j] = 0.0;
+        for (int j = 0; j < kDotGroup; j++) acc[j] = 0.0, accn[j] = 0.0;
         const double *vj[kDotGroup];
 #pragma unroll
         for (int j = 0; j < kDotGroup; j++) vj[j] = (g0 + j < win.nv) ? V + win.slot(win.jlo + g0 + j) * N : nullptr;
+        bool crossed = false;
         for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) {
+            if (!crossed && i >= n) {
+#pragma unroll
+                for (int j = 0; j < kDotGroup; j++) accn[j] = acc[j], acc[j] = 0.0;
+                crossed = true;
+            }
             const double u = ut[i];
             if (g0 == 0) vnew[i] = i < n ? w[i] : vk[i] - w[i];
-            const int part = i < n ? 0 : 1;
 #pragma unroll
             for (int j = 0; j < kDotGroup; j++)
-                if (vj[j]) acc[2 * j + part] += vj[j][i] * u;
+                if (vj[j]) acc[j] += vj[j][i] * u;
         }
-        block_sum<2 * kDotGroup>(acc);
+        if (!crossed) {
+#pragma unroll
+            for (int j = 0; j < kDotGroup; j++) accn[j] = acc[j], acc[j] = 0.0;
+        }
+        double red[2 * kDotGroup];
+#pragma unroll
+        for (int j = 0; j < kDotGroup; j++) red[2 * j] = accn[j], red[2 * j + 1] = acc[j];
+        block_sum<2 * kDotGroup>(red);
         if (threadIdx.x == 0)
             for (int j = 0; j < 2 * kDotGroup && 2 * g0 + j < 2 * win.nv; j++)
-                st_agent(rb.partials + (size_t)blockIdx.x * 2 * maxv + 2 * g0 + j, acc[j]);
+                st_agent(rb.partials + (size_t)blockIdx.x * 2 * maxv + 2 * g0 + j, red[j]);
     }
     __shared__ int s_last;
     if (threadIdx.x == 0) {
@@ -829,6 +844,16 @@ static void launch_arnoldi_dots(Ctx &c, DState *st, double *V, const double *w, 
 
 // V(:,k+1) -= H(j,k) V(:,j) for the window in order; H(k+1,k) = sqrt(dot(u,V_{k+1}) + dot(t,Q_{k+1}));
 // then rotations, SymGivens and the g update (cpgmres.m:214-247, cpdqgmres.m:481-521).
+// Window coefficients and basis pointers of one step, tabulated in LDS once per workgroup:
+// the per-element loops then read (h_j, V_j) from LDS instead of recomputing ring slots and
+// H indices (64-bit divisions) for every element.
+constexpr int kWinTab = 1024;
+struct WinTab {
+    const double *const *p;
+    const double *h;
+    int nv;
+};
+
 struct ArnoldiOrth {
     DState *st;
     double *V;
@@ -836,10 +861,20 @@ struct ArnoldiOrth {
     int64_t n, N, ring;
     Window win;
     double *vnew;
+    WinTab tab;
     __device__ bool setup() {
         if (!st->running) return false;
         win = window(st, ring);
         vnew = V + (ring ? (win.kk % ring) : win.kk) * N;
+        __shared__ const double *tp[kWinTab];
+        __shared__ double th[kWinTab];
+        tab.nv = win.nv <= kWinTab ? (int)win.nv : -1;
+        for (int j = threadIdx.x; j < tab.nv; j += blockDim.x) {
+            tp[j] = V + win.slot(win.jlo + j) * N;
+            th[j] = h(win.jlo + j);
+        }
+        __syncthreads();
+        tab.p = tp, tab.h = th;
         return true;
     }
     __device__ double h(int64_t j) const {
@@ -847,7 +882,12 @@ struct ArnoldiOrth {
     }
     __device__ void operator()(int64_t i, double *acc) {
         double v = vnew[i];
-        for (int64_t j = win.jlo; j <= win.kk; j++) v = v - h(j) * V[win.slot(j) * N + i];
+        if (tab.nv >= 0) {
+#pragma unroll 8
+            for (int j = 0; j < tab.nv; j++) v = v - tab.h[j] * tab.p[j][i];
+        } else {
+            for (int64_t j = win.jlo; j <= win.kk; j++) v = v - h(j) * V[win.slot(j) * N + i];
+        }
         vnew[i] = v;
         acc[i < n ? 0 : 1] += ut[i] * v;
     }
@@ -925,6 +965,9 @@ struct DqgmresDirection {
     int64_t n, N;
     int64_t kk, mem, M1, kpos, jlo;
     double h, hkk, gk;
+    double *vn, *pk;
+    const double *vk;
+    WinTab tab;
     __device__ bool setup() {
         if (!st->running) return false;
         kk = st->k, mem = st->mem, M1 = mem + 1;
@@ -933,15 +976,31 @@ struct DqgmresDirection {
         h = st->hk1;
         hkk = Hd(st, kk, 2);
         gk = st->g[kpos];
+        vn = V + (kk % M1) * N, vk = V + kpos * N, pk = PV + kpos * N;
+        __shared__ const double *tp[kWinTab];
+        __shared__ double th[kWinTab];
+        const int64_t nv = kk - jlo;
+        tab.nv = nv <= kWinTab ? (int)nv : -1;
+        for (int j = threadIdx.x; j < tab.nv; j += blockDim.x) {
+            const int64_t jj = jlo + j;
+            tp[j] = PV + ((jj - 1) % M1) * N;
+            th[j] = Hd(st, jj, 2 + kk - jj);
+        }
+        __syncthreads();
+        tab.p = tp, tab.h = th;
         return true;
     }
     __device__ void operator()(int64_t i) {
-        double *vn = V + (kk % M1) * N;
         if (h != 0) vn[i] = vn[i] / h;
-        double pv = V[kpos * N + i];
-        for (int64_t j = jlo; j <= kk - 1; j++) pv = pv - Hd(st, j, 2 + kk - j) * PV[((j - 1) % M1) * N + i];
+        double pv = vk[i];
+        if (tab.nv >= 0) {
+#pragma unroll 8
+            for (int j = 0; j < tab.nv; j++) pv = pv - tab.h[j] * tab.p[j][i];
+        } else {
+            for (int64_t j = jlo; j <= kk - 1; j++) pv = pv - Hd(st, j, 2 + kk - j) * PV[((j - 1) % M1) * N + i];
+        }
         pv = pv / hkk;
-        PV[kpos * N + i] = pv;
+        pk[i] = pv;
         xy[i] = i < n ? xy[i] + gk * pv : xy[i] - gk * pv;
     }
 };

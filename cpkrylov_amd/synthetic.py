@@ -70,3 +70,69 @@ def saddle_system(N=10_000_000, seed=SEED, window=4, frac_n=0.55, scale=1e3):
     Cm = sp.diags(np.full(m, 1e-8), 0, shape=(m, m), format="csr")
     rhs = np.concatenate([1e3 * rr.standard_normal(n), rr.standard_normal(m)])
     return dict(Q=Q, B=B, C=Cm, G=G, rhs=rhs, n=n, m=m, N=N, seed=seed, window=window)
+
+
+def nonsym_system(N=50_000_000, seed=SEED + 1, window=4, scale=1e2, z1_range=(0.2, 60.0), s1_range=(1e-2, 1.0)):
+    """Nonsymmetric 3x3-block system modelled on cvxqp2_s (examples/cvxqp2_s_3x3_nonsymm_perm_iter10.mat),
+    the structure of SURVEY.md section 8d config 5 (S50 at the default N):
+
+      A = [ H        -E1'  -E2' ]     H   nH x nH SPD tridiagonal (as Q of saddle_system)
+          [ Z1 E1     S1    0   ]     E1, E2 select the variables with a lower / upper bound
+          [ Z2 E2     0     S2  ]     Z, S positive diagonals (C3: z in [0.2, 60], s1 in
+                                      [3e-3, 1], z2 ~ 1.5e-2, s2 ~ 9-10; here s1 >= 1e-2:
+                                      below that CP-DQGMRES(40) with G = diag(A) stagnates on
+                                      the synthetic system, while at 1e-2 it needs ~90 iterations,
+                                      so the 40-vector window is exercised)
+      B  m x n touching only the H columns (C3: 200 zero columns), built as in saddle_system
+      G = diag(A), C = 1e-8 I, rhs ~ N(0, 1)
+
+    Block sizes follow C3 (nH : nZ : m = 300 : 200 : 225), each bound set takes every
+    other-ish variable so a row-block partition stays local."""
+    nH = int(round(N * 300 / 725))
+    nZ = int(round(N * 200 / 725))
+    m = N - nH - nZ
+    nZ1 = nZ // 2
+    nZ2 = nZ - nZ1
+    n = nH + nZ
+    rq, rb, rr = _rngs(seed)
+    # H: SPD tridiagonal
+    g = np.exp(rq.uniform(np.log(4.0), np.log(1.3e2), size=nH))
+    a = rq.uniform(0.5, 1.0, size=nH) * np.where(rq.random(nH) < 0.5, -1.0, 1.0)
+    b = rq.uniform(0.5, 1.0, size=nH - 1) * np.where(rq.random(nH - 1) < 0.5, -1.0, 1.0)
+    hd = g + scale * a * a
+    hd[1:] += scale * b * b
+    ho = scale * a[:-1] * b
+    i1 = (np.arange(nZ1, dtype=np.int64) * nH) // max(nZ1, 1)
+    i2 = np.minimum((np.arange(nZ2, dtype=np.int64) * nH) // max(nZ2, 1) + 1, nH - 1)
+    z1 = np.exp(rq.uniform(np.log(z1_range[0]), np.log(z1_range[1]), size=nZ1))
+    s1 = np.exp(rq.uniform(np.log(s1_range[0]), np.log(s1_range[1]), size=nZ1))
+    z2 = rq.uniform(1.5e-2, 1.7e-2, size=nZ2)
+    s2 = rq.uniform(9.0, 10.0, size=nZ2)
+    k1 = nH + np.arange(nZ1)
+    k2 = nH + nZ1 + np.arange(nZ2)
+    r = np.arange(nH)
+    rows = np.concatenate([r, r[1:], r[:-1], i1, i2, k1, k1, k2, k2])
+    cols = np.concatenate([r, r[:-1], r[1:], k1, k2, i1, k1, i2, k2])
+    vals = np.concatenate([hd, ho, ho, -np.ones(nZ1), -np.ones(nZ2), z1, s1, z2, s2])
+    A = sp.csr_matrix((vals, (rows, cols)), shape=(n, n))
+    A.sum_duplicates()
+    A.sort_indices()
+    G = sp.diags(A.diagonal(), 0, shape=(n, n), format="csr")
+    # B: m x n on the H columns only
+    piv = np.floor(np.arange(m, dtype=np.float64) * nH / m).astype(np.int64)
+    nextra = np.where(rb.random(m) < 0.1, 2, 1)
+    offs = np.concatenate([np.arange(-window, 0), np.arange(1, window + 1)])
+    c1 = np.empty(m, dtype=np.int64)
+    c1[:-1] = piv[1:]
+    c1[-1] = max(piv[-1] - 1, 0) if m > 1 else min(1, nH - 1)
+    c2 = np.clip(piv + offs[rb.integers(0, offs.size, size=m)], 0, nH - 1)
+    brow = np.concatenate([np.arange(m), np.arange(m), np.nonzero(nextra == 2)[0]])
+    bcol = np.concatenate([piv, c1, c2[nextra == 2]])
+    bval = rb.uniform(1.0 / 3.0, 1.0, size=brow.size) * np.where(rb.random(brow.size) < 0.5, -1.0, 1.0)
+    B = sp.csr_matrix((bval, (brow, bcol)), shape=(m, n))
+    B.sum_duplicates()
+    B.sort_indices()
+    Cm = sp.diags(np.full(m, 1e-8), 0, shape=(m, m), format="csr")
+    rhs = rr.standard_normal(n + m)
+    return dict(Q=A, B=B, C=Cm, G=G, rhs=rhs, n=n, m=m, N=n + m, nH=nH, nZ1=nZ1, nZ2=nZ2, seed=seed,
+                window=window)

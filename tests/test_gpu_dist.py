@@ -82,7 +82,8 @@ def test_dist_apply_bitexact(name, P, props):
 DIST_CASES = [("cvxqp1_m", "minres", {}), ("cvxqp1_m", "cg", {}), ("cvxqp1_m", "cglanczos", {}),
               ("cvxqp1_m", "symmlq", {}), ("cvxqp1_m", "dqgmres", {"mem": 2}),
               ("cvxqp2_s", "gmres", {"restart": 20}), ("cvxqp2_s", "gmres", {"restart": 100}),
-              ("cvxqp2_s", "dqgmres", {"mem": 20}), ("cvxqp2_s", "dqgmres", {"mem": 100})]
+              ("cvxqp2_s", "dqgmres", {"mem": 20}), ("cvxqp2_s", "dqgmres", {"mem": 100}),
+              ("syn_nonsym20k", "dqgmres", {"mem": 40})]
 
 
 @pytest.mark.parametrize("P", [2, 3])

@@ -33,6 +33,10 @@ CASES = [
     ("cvxqp2_s", "gmres", {"restart": 20}),
     ("cvxqp2_s", "dqgmres", {"mem": 100}),
     ("cvxqp2_s", "dqgmres", {"mem": 20}),
+    # the benchmark generators at 20k dofs (S50's nonsymmetric 3x3 structure, S10's symmetric one)
+    ("syn_nonsym20k", "dqgmres", {"mem": 40}),
+    ("syn_nonsym20k", "gmres", {"restart": 40}),
+    ("syn_symm20k", "minres", {}),
 ]
 
 
