@@ -59,6 +59,25 @@ __device__ __forceinline__ double ld_agent(const double *p) {
     return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Arrival ticket of a grid reduction (thread 0 of each workgroup, after its partials have been
+// stored and drained).  Workgroups first count in on one of 16 group tickets, each on its own
+// cache line, and only the last of a group counts in on the global ticket: same-address
+// atomics per ticket drop from gridDim.x to ~gridDim.x/16, which is what bounds the tail of a
+// reduction over thousands of workgroups.  Tickets are reset by their last arrival.
+constexpr unsigned kTicketGroups = 16, kTicketStride = 16;  // 64-byte lines
+constexpr size_t kTicketWords = kTicketStride * (1 + kTicketGroups);
+__device__ __forceinline__ bool arrive_last(unsigned *counter) {
+    const unsigned G = gridDim.x, g = blockIdx.x % kTicketGroups;
+    const unsigned ngroups = G < kTicketGroups ? G : kTicketGroups;
+    const unsigned gsize = (G - g + kTicketGroups - 1) / kTicketGroups;
+    unsigned *cg = counter + kTicketStride * (1 + g);
+    if (__hip_atomic_fetch_add(cg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gsize - 1) return false;
+    __hip_atomic_store(cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ngroups - 1) return false;
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
 // Reduce v over the whole grid.  Returns true in every thread of the last-arriving
 // workgroup, where tot[] (thread 0) holds the grid-wide sums in a fixed summation order.
 template <int NV>
@@ -69,22 +88,36 @@ __device__ __forceinline__ bool grid_sum(double (&v)[NV], RedBuf rb, double (&to
 #pragma unroll
         for (int j = 0; j < NV; j++) st_agent(rb.partials + (size_t)blockIdx.x * NV + j, v[j]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned prev = __hip_atomic_fetch_add(rb.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (prev == gridDim.x - 1);
+        s_last = arrive_last(rb.counter);
     }
     __syncthreads();
     if (!s_last) return false;
     double acc[NV];
 #pragma unroll
     for (int j = 0; j < NV; j++) acc[j] = 0.0;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x)
+    constexpr int kTail = 8;  // grids up to 8 * blockDim: every partial load in flight at once
+    if (gridDim.x <= kTail * blockDim.x) {
+        double t[kTail][NV];
 #pragma unroll
-        for (int j = 0; j < NV; j++) acc[j] += ld_agent(rb.partials + (size_t)b * NV + j);
+        for (int q = 0; q < kTail; q++) {
+            const unsigned b = threadIdx.x + q * blockDim.x;
+#pragma unroll
+            for (int j = 0; j < NV; j++) t[q][j] = b < gridDim.x ? ld_agent(rb.partials + (size_t)b * NV + j) : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < kTail; q++)
+            if (threadIdx.x + q * blockDim.x < gridDim.x)
+#pragma unroll
+                for (int j = 0; j < NV; j++) acc[j] += t[q][j];  // same additions, same order
+    } else {
+        for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x)
+#pragma unroll
+            for (int j = 0; j < NV; j++) acc[j] += ld_agent(rb.partials + (size_t)b * NV + j);
+    }
     block_sum<NV>(acc);
     if (threadIdx.x == 0) {
 #pragma unroll
         for (int j = 0; j < NV; j++) tot[j] = acc[j];
-        __hip_atomic_store(rb.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (rb.defer)
 #pragma unroll
             for (int j = 0; j < NV; j++) rb.defer[j] = acc[j];

@@ -19,7 +19,7 @@ namespace cpk {
 void Ctx::ensure_partials(size_t count) {
     if (partials.n < count) partials.alloc(count);
     if (!counter.n) {
-        counter.alloc(64);
+        counter.alloc(kTicketWords);
         CPK_HIP(hipMemset(counter.p, 0, counter.bytes()));
     }
 }
@@ -382,21 +382,22 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
 // contiguously.  Each row still subtracts its terms in the reference's order, one rounding per
 // product and per subtraction, so the result is bit-identical to the direct path.
 // LDS image of a staged block (dynamic shared memory, sized per launch):
-//   double w[R] | double v[CAP + 4] | int16 c[CAP + 4] | int16 p[R + 1] | int16 lv[R + 1] | int16 ps[R + 1]
+//   double w[R] | double v[CAP + 8] | int16 c[CAP + 8] | int16 p[R + 1] | int16 lv[R + 1] | int16 ps[R + 1]
+constexpr int kSweepPad = 8;  // entry arrays padded for the branchless 8-entry chunks
 struct SweepLds {
     double *w, *v;
     int16_t *c, *p, *lv, *ps;
     __device__ SweepLds(char *smem, int R, int CAP) {
         w = reinterpret_cast<double *>(smem);
         v = w + R;
-        c = reinterpret_cast<int16_t *>(v + CAP + 4);
-        p = c + CAP + 4;
+        c = reinterpret_cast<int16_t *>(v + CAP + kSweepPad);
+        p = c + CAP + kSweepPad;
         lv = p + R + 1;
         ps = lv + R + 1;
     }
 };
 size_t sweep_lds_bytes(int R, int CAP) {
-    return ((size_t)8 * R + 10 * ((size_t)CAP + 4) + 6 * ((size_t)R + 1) + 15) & ~(size_t)15;
+    return ((size_t)8 * R + 10 * ((size_t)CAP + kSweepPad) + 6 * ((size_t)R + 1) + 15) & ~(size_t)15;
 }
 
 // Outside-block prefix: a row's leading terms that refer to rows finished by earlier launches
@@ -411,7 +412,21 @@ __device__ __forceinline__ void fold_prefix(SweepLds &S, int nr) {
         int e = S.p[i];
         const int e1 = S.p[i + 1];
         double acc = S.w[i];
-        while (e < e1 && S.c[e] < 0) acc -= S.v[e++];
+        for (;;) {  // eight entries per LDS round trip; absent / stopped terms subtract +0.0
+            int c[kSweepPad];
+            double v[kSweepPad];
+#pragma unroll
+            for (int j = 0; j < kSweepPad; j++) c[j] = S.c[e + j], v[j] = S.v[e + j];
+            int t = 0;
+#pragma unroll
+            for (int j = 0; j < kSweepPad; j++) {
+                const bool take = t == j && e + j < e1 && c[j] < 0;
+                acc -= take ? v[j] : 0.0;
+                t += take;
+            }
+            e += t;
+            if (t < kSweepPad) break;
+        }
         S.w[i] = acc;
         S.ps[i] = (int16_t)e;
     }
@@ -425,8 +440,9 @@ __device__ __forceinline__ void fold_prefix(SweepLds &S, int nr) {
 // still subtracted one at a time in the reference's order.  skip_first: the first level holds
 // only rows without entries (their values are already in place), as in round 0 forward.
 // PS: rows start at ps[k] (after fold_prefix) instead of p[k].
-template <int TPB, bool BWD, bool PS = false>
+template <int TPB, bool BWD, bool PS = false, int CH = 4>
 __device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_first = false) {
+    static_assert(CH <= kSweepPad, "chunk wider than the padding");
     int l = BWD ? nl - 1 : 0;
     int li0 = 0;
     if (skip_first && !BWD) l = 1, li0 = 1;
@@ -439,15 +455,15 @@ __device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_firs
         for (int k = a + (int)threadIdx.x; k < z; k += TPB) {
             const int e1 = S.p[k + 1];
             double acc = S.w[k];
-            for (int e = PS ? S.ps[k] : S.p[k]; e < e1; e += 4) {
-                int c[4];
-                double v[4], x[4];
+            for (int e = PS ? S.ps[k] : S.p[k]; e < e1; e += CH) {
+                int c[CH];
+                double v[CH], x[CH];
 #pragma unroll
-                for (int j = 0; j < 4; j++) c[j] = S.c[e + j], v[j] = S.v[e + j];
+                for (int j = 0; j < CH; j++) c[j] = S.c[e + j], v[j] = S.v[e + j];
 #pragma unroll
-                for (int j = 0; j < 4; j++) x[j] = S.w[(c[j] >= 0 && e + j < e1) ? c[j] : 0];
+                for (int j = 0; j < CH; j++) x[j] = S.w[(c[j] >= 0 && e + j < e1) ? c[j] : 0];
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
+                for (int j = 0; j < CH; j++) {
                     const double t = (c[j] >= 0) ? v[j] * x[j] : v[j];
                     acc -= (e + j < e1) ? t : 0.0;
                 }
@@ -498,7 +514,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_fwd_kernel(
                 sweep_levels<TPB, false>(S, l1 - l0, true);  // round 0: no outside references
             } else {
                 fold_prefix<TPB>(S, nr);
-                sweep_levels<TPB, false, true>(S, l1 - l0);
+                sweep_levels<TPB, false, true, 8>(S, l1 - l0);
             }
         }
         for (int i = tid; i < nr; i += TPB) w[r0 + i] = S.w[i];
@@ -551,7 +567,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_bwd_kernel(
         }
         __syncthreads();
         fold_prefix<TPB>(S, nr);
-        sweep_levels<TPB, true, true>(S, l1 - l0);
+        sweep_levels<TPB, true, true, 8>(S, l1 - l0);
         for (int i = tid; i < nr; i += TPB) {
             const double z = S.w[i];
             w[r0 + i] = z;

@@ -775,8 +775,7 @@ __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double
     __shared__ int s_last;
     if (threadIdx.x == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned prev = __hip_atomic_fetch_add(rb.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (prev == gridDim.x - 1);
+        s_last = arrive_last(rb.counter);
     }
     __syncthreads();
     if (!s_last) return;
@@ -788,7 +787,6 @@ __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double
             block_sum<1>(a);
             if (threadIdx.x == 0) rb.defer[j] = a[0];
         }
-        if (threadIdx.x == 0) __hip_atomic_store(rb.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     __shared__ double hv[2];
@@ -810,7 +808,6 @@ __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) __hip_atomic_store(rb.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // distributed mode: H(j, k) from the allreduced window sums (same additions as above)
