@@ -1,6 +1,7 @@
-"""Summarise a rocprofv3 --kernel-trace CSV per kernel, separating live launches from the
-post-convergence no-op launches of the captured iteration batches (a skipped launch exits at
-entry and lasts a few microseconds).  Usage: prof_summary.py kernel_trace.csv [min_us]"""
+"""Summarise a rocprofv3 --kernel-trace CSV per kernel, separating launches shorter than min_us
+(default 8): the no-op launches of a captured iteration batch after convergence (they exit at
+entry, ~4-5 us) -- and genuinely short launches such as the one-block top round of a sweep.
+Usage: prof_summary.py kernel_trace.csv [min_us]"""
 import collections
 import csv
 import sys
