@@ -1193,11 +1193,26 @@ struct SolveCore {
         if (graphs.size() <= slot) graphs.resize(slot + 1, {nullptr, nullptr});
         if (!graphs[slot].second) {
             hipGraph_t graph = nullptr;
-            CPK_HIP(hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
-            for (int i = 0; i < b; i++) body();
-            CPK_HIP(hipStreamEndCapture(c.stream, &graph));
-            graphs[slot].first = graph;
-            CPK_HIP(hipGraphInstantiate(&graphs[slot].second, graph, nullptr, nullptr, 0));
+            try {
+                CPK_HIP(hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
+                for (int i = 0; i < b; i++) body();
+                CPK_HIP(hipStreamEndCapture(c.stream, &graph));
+                graphs[slot].first = graph;
+                CPK_HIP(hipGraphInstantiate(&graphs[slot].second, graph, nullptr, nullptr, 0));
+            } catch (const Error &e) {
+                // a transport that cannot be captured (deterministic, so every rank lands here):
+                // end the capture, drop the graph and run this solver's batches eagerly
+                hipGraph_t g2 = nullptr;
+                (void)hipStreamEndCapture(c.stream, &g2);
+                if (g2) (void)hipGraphDestroy(g2);
+                if (graph && graph != g2) (void)hipGraphDestroy(graph);
+                graphs[slot] = {nullptr, nullptr};
+                (void)hipGetLastError();
+                if (!c.dist()) throw;
+                fprintf(stderr, "cpk: iteration-graph capture failed (%s); running batches eagerly\n", e.what());
+                use_graph = false;
+                return nullptr;
+            }
         }
         return graphs[slot].second;
     }
@@ -1217,7 +1232,8 @@ struct SolveCore {
         for (;;) {
             const double res0 = h.residNorm;
             const int64_t k0 = h.k;
-            if (use_graph) CPK_HIP(hipGraphLaunch(graph_for(site, b, body), c.stream));
+            hipGraphExec_t exec = use_graph ? graph_for(site, b, body) : nullptr;
+            if (exec) CPK_HIP(hipGraphLaunch(exec, c.stream));
             else
                 for (int i = 0; i < b; i++) body();
             pull();
