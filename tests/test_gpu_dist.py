@@ -174,3 +174,32 @@ def test_rccl_one_rank_graph_capture():
         del s2
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("P", [8])
+def test_dist_more_ranks_than_subtrees(P):
+    """A small system on many ranks: the separator set takes most rows and some ranks own
+    nothing; the apply and a solve still agree with the oracle."""
+    import cpkrylov_amd as cpk
+    Pd = F.load("cvxqp2_s")
+    z = np.random.default_rng(2).standard_normal(Pd["n"] + Pd["m"])
+    opts = dict(F.EXPROG_OPTS, mem=20)
+
+    def work(ctx, r):
+        M = cpk.opLDL2(Pd["G"], Pd["B"], -Pd["C"], ctx=ctx)
+        M.nitref, M.force_itref = 1, True
+        y = M * z
+        x, stats, flag = cpk.reg_cpkrylov(cpk.cpdqgmres, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts, ctx=ctx)
+        return y, M.export_factors() if r == 0 else None, len(M.local_dofs()[0]), stats["niters"], x
+
+    res = _run_ranks(P, work)
+    L, D, perm = res[0][1]
+    Mo = O.LDL2(Pd["G"], Pd["B"], -Pd["C"], factors=(L, D, perm))
+    Mo.set(nitref=1.0, force_itref=1.0)
+    yo = Mo @ z
+    for y, _, _, it, x in res:
+        assert np.array_equal(y, yo)
+        assert it == res[0][3] and np.array_equal(x, res[0][4])
+    assert sum(nl for _, _, nl, _, _ in res) == Pd["n"] + Pd["m"]
+    xo, so = O.reg_cpkrylov("dqgmres", Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts, perm=perm)
+    assert res[0][3] == so["niters"]
