@@ -396,9 +396,10 @@ struct SweepLds {
         ps = lv + R + 1;
     }
 };
-size_t sweep_lds_bytes(int R, int CAP) {
+__host__ __device__ constexpr size_t sweep_lds_bytes_dev(int R, int CAP) {
     return ((size_t)8 * R + 10 * ((size_t)CAP + kSweepPad) + 6 * ((size_t)R + 1) + 15) & ~(size_t)15;
 }
+size_t sweep_lds_bytes(int R, int CAP) { return sweep_lds_bytes_dev(R, CAP); }
 
 // Outside-block prefix: a row's leading terms that refer to rows finished by earlier launches
 // are already products in LDS (c < 0).  Subtracting them here, every row at once, takes them
@@ -407,8 +408,9 @@ size_t sweep_lds_bytes(int R, int CAP) {
 // upper rounds cheap: a separator row's many references into the subtrees below are all
 // outside its block.
 template <int TPB>
-__device__ __forceinline__ void fold_prefix(SweepLds &S, int nr) {
-    for (int i = threadIdx.x; i < nr; i += TPB) {
+__device__ __forceinline__ void fold_prefix(SweepLds &S, int nr, int tid = -1) {
+    if (tid < 0) tid = threadIdx.x;
+    for (int i = tid; i < nr; i += TPB) {
         int e = S.p[i];
         const int e1 = S.p[i + 1];
         double acc = S.w[i];
@@ -441,7 +443,8 @@ __device__ __forceinline__ void fold_prefix(SweepLds &S, int nr) {
 // only rows without entries (their values are already in place), as in round 0 forward.
 // PS: rows start at ps[k] (after fold_prefix) instead of p[k].
 template <int TPB, bool BWD, bool PS = false, int CH = 4>
-__device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_first = false) {
+__device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_first = false, int tid = -1) {
+    if (tid < 0) tid = threadIdx.x;
     static_assert(CH <= kSweepPad, "chunk wider than the padding");
     int l = BWD ? nl - 1 : 0;
     int li0 = 0;
@@ -452,7 +455,7 @@ __device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_firs
         const int ln = BWD ? l - 1 : l + 1;
         int an = 0, zn = 0;
         if (li + 1 < nl) an = S.lv[ln], zn = S.lv[ln + 1];
-        for (int k = a + (int)threadIdx.x; k < z; k += TPB) {
+        for (int k = a + tid; k < z; k += TPB) {
             const int e1 = S.p[k + 1];
             double acc = S.w[k];
             for (int e = PS ? S.ps[k] : S.p[k]; e < e1; e += CH) {
@@ -603,18 +606,24 @@ struct BlkMeta {
     int32_t r0, r1, l0, l1, fe0, fe1, be0, be1;
 };
 
-template <int TPB, int RPT, int EPT, bool BWD, bool ADD>
-__global__ __launch_bounds__(TPB) void sptrsv_pipe_kernel(
+// SPLIT > 1: the workgroup is one wave holding SPLIT independent logical blocks of TPB lanes
+// (TPB * SPLIT = 64), each with its own LDS image.  A level that occupies a few rows then costs
+// one instruction stream for SPLIT blocks instead of one per block; lanes of different logical
+// blocks never synchronise (within a single wave __syncthreads is a no-op fence).
+template <int TPB, int RPT, int EPT, bool BWD, bool ADD, int SPLIT = 1>
+__global__ __launch_bounds__(TPB * SPLIT) void sptrsv_pipe_kernel(
     int64_t blk0, int64_t nblk, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,
     int64_t neg_from, double *w, double *out, const int *run, const int *active) {
+    static_assert(SPLIT == 1 || TPB * SPLIT == 64, "split blocks must share one wave");
     constexpr int R = RPT * TPB, CAP = EPT * TPB;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
-    SweepLds S(smem, R, CAP);
-    const int tid = threadIdx.x;
-    const int64_t G = gridDim.x;
+    const int sub = SPLIT > 1 ? (int)threadIdx.x / TPB : 0;
+    SweepLds S(smem + (SPLIT > 1 ? sub * (int)sweep_lds_bytes_dev(R, CAP) : 0), R, CAP);
+    const int tid = SPLIT > 1 ? (int)threadIdx.x % TPB : (int)threadIdx.x;
+    const int64_t G = (int64_t)gridDim.x * SPLIT;
     // prefetched registers of the next block
     uint32_t q[RPT];
     int32_t sp[RPT], lvr[RPT];
@@ -642,7 +651,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_pipe_kernel(
                 cc[j] = __builtin_nontemporal_load(col + e0 + e), vv[j] = __builtin_nontemporal_load(val + e0 + e);
         }
     };
-    int64_t b = blk0 + blockIdx.x;
+    int64_t b = blk0 + (int64_t)blockIdx.x * SPLIT + sub;
     const int64_t bend = blk0 + nblk;
     if (b >= bend) return;
     BlkMeta cur = meta[b];
@@ -688,7 +697,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_pipe_kernel(
             nxt = meta[bn];
             issue(nxt);  // in flight during the level phase
         }
-        sweep_levels<TPB, BWD>(S, nl, true);
+        sweep_levels<TPB, BWD>(S, nl, true, tid);
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             const int i = tid + j * TPB;
@@ -705,32 +714,35 @@ __global__ __launch_bounds__(TPB) void sptrsv_pipe_kernel(
     }
 }
 
-template <int TPB, int RPT, int EPT>
+// threads == 32 in a sweep configuration selects the split kernel: 2 logical blocks of 32 lanes
+// per 64-lane wave
+template <int TPB, int RPT, int EPT, int SPLIT = 1>
 static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
                        double *w, double *out, const int *run, const int *active) {
     if (F.sweep_threads[0] != TPB || F.sweep_rows[0] != RPT * TPB || F.sweep_cap[0] != EPT * TPB) return false;
     const int64_t nb = F.round_ptr[1] - F.round_ptr[0];
-    const size_t lds = sweep_lds_bytes(RPT * TPB, EPT * TPB);
+    const size_t lds = sweep_lds_bytes(RPT * TPB, EPT * TPB) * SPLIT;
     int occ = 0;
-    const void *fn = bwd ? (add ? (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, true, true>
-                                : (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, true, false>)
-                         : (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, false, false>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, TPB, lds) != hipSuccess || occ < 1) occ = 1;
+    const void *fn = bwd ? (add ? (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>
+                                : (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>)
+                         : (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, TPB * SPLIT, lds) != hipSuccess || occ < 1) occ = 1;
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const int64_t grid = std::min<int64_t>(nb, (int64_t)occ * cus);
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>((nb + SPLIT - 1) / SPLIT, (int64_t)occ * cus));
     const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
+    const dim3 blk(TPB * SPLIT);
     if (!bwd)
-        hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false>), dim3((unsigned)grid), dim3(TPB), lds,
+        hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active);
     else if (add)
-        hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, true>), dim3((unsigned)grid), dim3(TPB), lds,
+        hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active);
     else
-        hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, false>), dim3((unsigned)grid), dim3(TPB), lds,
+        hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active);
     return true;
@@ -740,7 +752,10 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
 static bool pipe_round0(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
                         double *w, double *out, const int *run, const int *active) {
     if (!F.pipelined || F.round_ptr.size() < 2) return false;
-    return pipe_round<128, 2, 6>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
+    return pipe_round<32, 6, 18, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
+           pipe_round<32, 4, 12, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
+           pipe_round<32, 8, 24, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
+           pipe_round<128, 2, 6>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
            pipe_round<64, 3, 9>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
            pipe_round<64, 4, 12>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
            pipe_round<64, 6, 18>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
@@ -780,6 +795,7 @@ static void fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
     for (int64_t r = 0; r < R; r++) {
         if (r == 0 && MODE == 0 && pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active)) continue;
         switch (F.sweep_threads[r == 0 ? 0 : 1]) {
+        case 32: fwd_round<32, MODE>(c, F, r, xin, neg_from, w, run, active); break;
         case 64: fwd_round<64, MODE>(c, F, r, xin, neg_from, w, run, active); break;
         case 128: fwd_round<128, MODE>(c, F, r, xin, neg_from, w, run, active); break;
         case 512: fwd_round<512, MODE>(c, F, r, xin, neg_from, w, run, active); break;
@@ -805,6 +821,8 @@ void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
     for (int64_t r = R - 1; r >= 0; r--) {
         if (r == 0 && pipe_round0(c, F, true, add, nullptr, 0, w, out, run, active)) continue;
         switch (F.sweep_threads[r == 0 ? 0 : 1] * 2 + (add ? 1 : 0)) {
+        case 64: bwd_round<32, false>(c, F, r, w, out, run, active); break;
+        case 65: bwd_round<32, true>(c, F, r, w, out, run, active); break;
         case 128: bwd_round<64, false>(c, F, r, w, out, run, active); break;
         case 129: bwd_round<64, true>(c, F, r, w, out, run, active); break;
         case 256: bwd_round<128, false>(c, F, r, w, out, run, active); break;

@@ -27,7 +27,7 @@ SweepConfig sweep_config() {
         const int got = sscanf(e, "%d,%d,%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5], &v[6]);
         if (got == 3) v[3] = v[0], v[4] = v[1], v[5] = v[2];
         auto ok = [](int r, int c, int t) {
-            return r > 0 && r <= 16384 && c > 0 && c <= 16384 && (t == 64 || t == 128 || t == 256 || t == 512 || t == 1024) &&
+            return r > 0 && r <= 16384 && c > 0 && c <= 16384 && (t == 32 || t == 64 || t == 128 || t == 256 || t == 512 || t == 1024) &&
                    sweep_lds_bytes(r, c) <= 160 * 1024;
         };
         if ((got == 3 || got == 6 || got == 7) && ok(v[0], v[1], v[2]) && ok(v[3], v[4], v[5])) {

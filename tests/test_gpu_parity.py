@@ -129,7 +129,7 @@ def test_divide_and_transpose(gpu_ctx):
     assert np.linalg.norm(Kp @ y - z) <= 1e-8 * np.linalg.norm(z)
 
 
-@pytest.mark.parametrize("sweep", ["1024,3072,256", "512,1536,128", "256,768,64", "64,128,64", "256,768,128,2048,8192,512", "192,576,64", "128,512,128", "384,1152,64,2048,8192,512,400", "512,1536,64,1024,4096,256,300"])
+@pytest.mark.parametrize("sweep", ["1024,3072,256", "512,1536,128", "256,768,64", "64,128,64", "256,768,128,2048,8192,512", "192,576,64", "128,512,128", "384,1152,64,2048,8192,512,400", "512,1536,64,1024,4096,256,300", "192,576,32,1024,4096,512", "128,384,32,1024,4096,512"])
 @pytest.mark.parametrize("name", ["cvxqp1_m", "cvxqp2_s", "synthetic"])
 def test_precond_apply_bitexact_sweep_configs(gpu_ctx, name, sweep, monkeypatch):
     """Every LDS staging configuration (and the direct path for blocks that do not fit) gives
