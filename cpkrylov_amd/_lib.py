@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcpk.so")
+LIB_PATH = os.environ.get("CPK_LIB_PATH") or os.path.join(_HERE, "libcpk.so")  # override: tools/ A/B runs
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"libcpk.so not built ({LIB_PATH}); run `make -C cpkrylov_amd/csrc` "

@@ -194,7 +194,11 @@ int cpk_ctx_create(int device, int rank, int nranks, const unsigned char *unique
     API_BEGIN
     need(out != nullptr, "out is NULL");
     auto ctx = ctx_base(device, rank, nranks);
-    if (nranks > 1 || unique_id) {  // a 1-rank communicator runs the distributed path (tests)
+    const char *cm = getenv("CPK_COMM");
+    if (nranks > 1 && cm && std::string(cm) == "null") {  // diagnostic timing stand-in (comm.cpp)
+        ctx->comm.reset(make_null_comm(rank));
+        ctx->c.comm = ctx->comm.get();
+    } else if (nranks > 1 || unique_id) {  // a 1-rank communicator runs the distributed path (tests)
         need(unique_id != nullptr, "unique_id required when nranks > 1");
         ctx->comm.reset(make_rccl_comm(nranks, rank, unique_id));
         ctx->c.comm = ctx->comm.get();

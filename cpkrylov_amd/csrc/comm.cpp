@@ -1,6 +1,7 @@
 // comm.cpp -- collectives of the distributed solve.
 //
 // RcclComm: RCCL over xGMI, one process per GPU (production; graph-capturable).
+// NullComm: timing stand-in (no peers; see below).
 // SimComm:  P ranks as host threads of one process sharing one GPU, exchanging through a
 //           shared HBM buffer with host barriers.  It exists so the multi-rank device path
 //           can be exercised on a one-GPU box (RCCL refuses two ranks on one device); it is
@@ -61,6 +62,23 @@ void rccl_unique_id(unsigned char *uid) {
     nccl_check(ncclGetUniqueId(&u), "ncclGetUniqueId");
     std::memcpy(uid, &u, 128);
 }
+
+// ---- timing stand-in ---------------------------------------------------------------------------
+// NullComm (diagnostic only, CPK_COMM=null): rank `rank` of a P-way partition with no peers.
+// Collectives leave the local contribution in place, so results are meaningless; it exists to
+// time one rank's share of a P-way solve on a single GPU (tools/dist_timing.py).
+namespace {
+struct NullComm : Comm {
+    int rank;
+    explicit NullComm(int r) : rank(r) {}
+    void allreduce_sum(double *, size_t, hipStream_t) override {}
+    void allgather(const double *send, double *recv, size_t n, hipStream_t s) override {
+        if (n) CPK_HIP(hipMemcpyAsync(recv + (size_t)rank * n, send, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+    }
+    bool capturable() const override { return true; }
+};
+}  // namespace
+Comm *make_null_comm(int rank) { return new NullComm(rank); }
 
 // ---- simulated group --------------------------------------------------------------------------
 struct SimGroup {

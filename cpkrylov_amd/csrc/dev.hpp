@@ -171,6 +171,7 @@ struct SimGroup;
 SimGroup *simgroup_create(int nranks);
 void simgroup_destroy(SimGroup *g);
 Comm *make_sim_comm(SimGroup *g, int rank);
+Comm *make_null_comm(int rank);  // diagnostic: CPK_COMM=null
 void launch_sum_slots(hipStream_t s, const double *slots, int P, size_t n, double *out);
 struct DSep;
 // pack this rank's separator payload (w rows read by T, rank 0: +-x at the T dofs), allgather
@@ -197,7 +198,16 @@ struct DSep {
     int64_t nT = 0, kt = 0, nlev = 0, nsend = 0, ntdof = 0;
     DBuf<int32_t> tf_ptr, tf_col, tf_src, tb_ptr, tb_col, lev_ptr, lev_rows, send, tdof;
     DBuf<double> tf_val, tb_val, DT, sbuf, rbuf;
+    // staged solve (tsolve_staged_kernel): forward rows split into their leading payload terms
+    // (tk_*) and the rest (tr_*); the rest, the backward rows, D_T and the level lists live in LDS
+    DBuf<int32_t> tk_ptr, tk_col, tr_ptr, tr_col, tr_lcol;
+    DBuf<double> tk_val, tr_val, tr_rv, pre;  // tr_rv, pre: written by tprefix_kernel per solve
+    int64_t nrest = 0, nbwd = 0;
+    size_t lds = 0;  // bytes of the staged image, 0 = too large (one-pass global kernel)
 };
+// Split the forward rows of T and size the LDS image of the staged separator solve.
+void dsep_stage(DSep &T, const std::vector<int64_t> &tf_ptr, const std::vector<int32_t> &tf_col,
+                const std::vector<double> &tf_val, int64_t nbwd);
 struct DofMap;
 
 struct Precond {

@@ -337,6 +337,140 @@ __global__ __launch_bounds__(256) void tsolve_kernel(
     }
 }
 
+// Staged separator solve: the same arithmetic in the same order, restructured for latency.
+// The one-pass kernel above walks each row's terms with two dependent global loads per term;
+// at S10 / 8 ranks T has 593 rows, 13 levels and rows of up to 49 payload terms, and it took
+// ~160 us.  Here:
+//  (1) tprefix_kernel, one wave per row across the chip: each row subtracts its LEADING payload
+//      terms (coalesced loads, one gather, the subtractions in order on one lane), and the
+//      payload terms of the rest of the row are pre-multiplied (read later against 1.0);
+//  (2) tsolve_staged_kernel, one workgroup: stages the rest of the forward rows, the backward
+//      rows, D_T and the level lists in LDS and runs the levels out of LDS.
+// Row sums keep the exported factor's order: bit-identical.
+constexpr int kTsolveThreads = 1024;
+constexpr size_t kTsolveMaxLds = 160 * 1024;  // gfx950: 160 KB of LDS per workgroup
+
+// acc - v[e] * w[col(e)] for e in [e0, e1), in order, eight terms per LDS round trip (absent
+// terms subtract +0.0)
+__device__ __forceinline__ double lds_row_sum(double acc, int e0, int e1, const int32_t *col, const double *v,
+                                              const double *w) {
+    constexpr int K = 8;
+    for (int e = e0; e < e1; e += K) {
+        int c[K];
+        double a[K], x[K];
+#pragma unroll
+        for (int u = 0; u < K; u++) {
+            const int q = e + u < e1 ? e + u : e1 - 1;
+            c[u] = col[q], a[u] = v[q];
+        }
+#pragma unroll
+        for (int u = 0; u < K; u++) x[u] = w[c[u]];
+#pragma unroll
+        for (int u = 0; u < K; u++) acc -= (e + u < e1) ? a[u] * x[u] : 0.0;
+    }
+    return acc;
+}
+
+__global__ __launch_bounds__(256) void tprefix_kernel(
+    int nT, const int32_t *__restrict__ tk_ptr, const int32_t *__restrict__ tk_col, const double *__restrict__ tk_val,
+    const int32_t *__restrict__ tr_ptr, const int32_t *__restrict__ tr_col, const double *__restrict__ tr_val,
+    const int32_t *__restrict__ tf_src, const double *__restrict__ rbuf, double *__restrict__ pre,
+    double *__restrict__ rv_out, const int *run, const int *active) {
+    __shared__ double prod[4][kWave];
+    if (skip(run, active)) return;
+    const int wv = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    const int t = blockIdx.x * 4 + wv;
+    if (t >= nT) return;
+    double acc = rbuf[tf_src[t]];
+    const int k1 = tk_ptr[t + 1];
+    for (int e = tk_ptr[t]; e < k1; e += kWave) {
+        const int q = e + lane;
+        double p = 0.0;
+        if (q < k1) p = tk_val[q] * rbuf[tk_col[q]];
+        prod[wv][lane] = p;
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+            const int n = min(kWave, k1 - e);
+            for (int u = 0; u < n; u++) acc -= prod[wv][u];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) pre[t] = acc;
+    for (int q = tr_ptr[t] + lane; q < tr_ptr[t + 1]; q += kWave) {
+        const int c = tr_col[q];
+        const double v = tr_val[q];
+        rv_out[q] = c >= 0 ? v * rbuf[c] : v;
+    }
+}
+
+__global__ __launch_bounds__(kTsolveThreads) void tsolve_staged_kernel(
+    int nlev, int nT, int nrest, int nbwd, const int32_t *__restrict__ lev_ptr, const int32_t *__restrict__ lev_rows,
+    const int32_t *__restrict__ tr_ptr, const int32_t *__restrict__ tr_lcol, const double *__restrict__ tr_rv,
+    const double *__restrict__ pre, const int32_t *__restrict__ tb_ptr, const int32_t *__restrict__ tb_col,
+    const double *__restrict__ tb_val, const double *__restrict__ DT, const int32_t *__restrict__ tdof, int ntdof,
+    double *wT, double *y, int add, const int *run, const int *active) {
+    extern __shared__ __attribute__((aligned(16))) char tsm[];
+    if (skip(run, active)) return;
+    double *wt = reinterpret_cast<double *>(tsm);  // nT + 1: wt[nT] = 1.0 (pre-multiplied terms)
+    double *dt = wt + nT + 1, *rv = dt + nT, *bv = rv + nrest;
+    int32_t *rc = reinterpret_cast<int32_t *>(bv + nbwd);
+    int32_t *bc = rc + nrest, *rp = bc + nbwd, *bp = rp + nT + 1, *lr = bp + nT + 1, *lp = lr + nT;
+    const int tid = threadIdx.x;
+    if (tid == 0) wt[nT] = 1.0;
+    for (int i = tid; i < nrest; i += kTsolveThreads) rc[i] = tr_lcol[i], rv[i] = tr_rv[i];
+    for (int i = tid; i < nbwd; i += kTsolveThreads) bc[i] = tb_col[i], bv[i] = tb_val[i];
+    for (int i = tid; i <= nT; i += kTsolveThreads) {
+        rp[i] = tr_ptr[i], bp[i] = tb_ptr[i];
+        if (i < nT) dt[i] = DT[i], lr[i] = lev_rows[i], wt[i] = pre[i];
+    }
+    for (int i = tid; i <= nlev; i += kTsolveThreads) lp[i] = lev_ptr[i];
+    __syncthreads();
+    for (int l = 0; l < nlev; l++) {  // forward: the rest of each row
+        for (int q = lp[l] + tid; q < lp[l + 1]; q += kTsolveThreads) {
+            const int t = lr[q];
+            wt[t] = lds_row_sum(wt[t], rp[t], rp[t + 1], rc, rv, wt);
+        }
+        __syncthreads();
+    }
+    for (int l = nlev - 1; l >= 0; l--) {  // backward
+        for (int q = lp[l] + tid; q < lp[l + 1]; q += kTsolveThreads) {
+            const int t = lr[q];
+            wt[t] = lds_row_sum(wt[t] / dt[t], bp[t], bp[t + 1], bc, bv, wt);
+        }
+        __syncthreads();
+    }
+    for (int t = tid; t < nT; t += kTsolveThreads) {
+        wT[t] = wt[t];
+        if (t < ntdof) {
+            const int32_t d = tdof[t];
+            y[d] = add ? y[d] + wt[t] : wt[t];
+        }
+    }
+}
+
+void dsep_stage(DSep &T, const std::vector<int64_t> &tf_ptr, const std::vector<int32_t> &tf_col,
+                const std::vector<double> &tf_val, int64_t nbwd) {
+    const int64_t nT = T.nT;
+    std::vector<int32_t> kp(nT + 1, 0), kc, rp(nT + 1, 0), rc, rl;
+    std::vector<double> kv, rv;
+    for (int64_t t = 0; t < nT; t++) {
+        int64_t e = tf_ptr[t];
+        for (; e < tf_ptr[t + 1] && tf_col[e] >= 0; e++) kc.push_back(tf_col[e]), kv.push_back(tf_val[e]);
+        for (; e < tf_ptr[t + 1]; e++) {
+            rc.push_back(tf_col[e]), rv.push_back(tf_val[e]);
+            rl.push_back(tf_col[e] >= 0 ? (int32_t)nT : -tf_col[e] - 1);  // LDS column: T row, or the 1.0 slot
+        }
+        kp[t + 1] = (int32_t)kc.size(), rp[t + 1] = (int32_t)rc.size();
+    }
+    T.tk_ptr.upload(kp), T.tk_col.upload(kc), T.tk_val.upload(kv);
+    T.tr_ptr.upload(rp), T.tr_col.upload(rc), T.tr_val.upload(rv), T.tr_lcol.upload(rl);
+    T.tr_rv.alloc(std::max<size_t>(rv.size(), 1));
+    T.pre.alloc(std::max<int64_t>(nT, 1));
+    T.nrest = (int64_t)rc.size(), T.nbwd = nbwd;
+    const size_t bytes = 8 * (size_t)(2 * nT + 1 + T.nrest + nbwd) + 4 * (size_t)(T.nrest + nbwd + 3 * (nT + 1) + T.nlev + 1);
+    T.lds = bytes <= kTsolveMaxLds ? bytes : 0;
+}
+
 // payload: w of this rank's rows that separator rows read, then (rank 0) the T inputs +-x[tdof]
 __global__ void tpack_kernel(const double *__restrict__ w, const int32_t *__restrict__ send, int nsend,
                              const double *__restrict__ x, int64_t neg_from, const int32_t *__restrict__ tdof,
@@ -362,6 +496,21 @@ void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x
 
 void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active) {
     if (S.nT == 0) return;
+    static bool lds_attr = [] {
+        return hipFuncSetAttribute((const void *)tsolve_staged_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)kTsolveMaxLds) == hipSuccess;
+    }();
+    if (S.lds && (S.lds <= 64 * 1024 || lds_attr) && !getenv("CPK_TSOLVE_ONEPASS")) {
+        hipLaunchKernelGGL(tprefix_kernel, dim3((unsigned)((S.nT + 3) / 4)), dim3(256), 0, c.stream, (int)S.nT,
+                           S.tk_ptr.p, S.tk_col.p, S.tk_val.p, S.tr_ptr.p, S.tr_col.p, S.tr_val.p, S.tf_src.p,
+                           S.rbuf.p, S.pre.p, S.tr_rv.p, run, active);
+        hipLaunchKernelGGL(tsolve_staged_kernel, dim3(1), dim3(kTsolveThreads), S.lds, c.stream, (int)S.nlev,
+                           (int)S.nT, (int)S.nrest, (int)S.nbwd, S.lev_ptr.p, S.lev_rows.p, S.tr_ptr.p, S.tr_lcol.p,
+                           S.tr_rv.p, S.pre.p, S.tb_ptr.p, S.tb_col.p, S.tb_val.p, S.DT.p, S.tdof.p, (int)S.ntdof,
+                           wT, y, add ? 1 : 0, run, active);
+        CPK_HIP(hipGetLastError());
+        return;
+    }
     hipLaunchKernelGGL(tsolve_kernel, dim3(1), dim3(256), (size_t)S.nT * sizeof(double), c.stream, (int)S.nlev,
                        (int)S.nT, S.lev_ptr.p, S.lev_rows.p, S.tf_ptr.p, S.tf_col.p, S.tf_val.p, S.tf_src.p,
                        S.tb_ptr.p, S.tb_col.p, S.tb_val.p, S.DT.p, S.rbuf.p, S.tdof.p, (int)S.ntdof, wT, y,

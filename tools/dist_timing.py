@@ -1,0 +1,62 @@
+"""Per-rank work of a P-way distributed S10 solve, timed on ONE GPU (diagnostic).
+
+CPK_COMM=null gives the context a communicator without peers: collectives are no-ops, so the
+numbers are meaningless but the kernels are exactly one rank's share of the P-way solve.
+Prints, per (P, rank): the local rows, kernel timings (cpk_profile_kernels) and the wall time
+per iteration of a 20-iteration cpminres call (collective latency NOT included).
+"""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch  # before libcpk initialises HIP
+
+os.environ["CPK_COMM"] = "null"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import cpkrylov_amd as cpk  # noqa: E402
+from cpkrylov_amd import _lib  # noqa: E402
+from cpkrylov_amd.synthetic import saddle_system  # noqa: E402
+
+torch.cuda.init()
+S = saddle_system(int(os.environ.get("N", "10000000")))
+runs = [(int(a.split(":")[0]), int(a.split(":")[1])) for a in sys.argv[1:]] or [(1, 0), (2, 0), (4, 0), (8, 0), (8, 7)]
+for P, r in runs:
+    ctx = cpk.Context(device=0, rank=r, nranks=P) if P > 1 else cpk.Context(device=0)
+    A, B, Cm, G = (cpk.Matrix(S[k], ctx) for k in ("Q", "B", "C", "G"))
+    M = cpk.opLDL2(G, B, -S["C"], ctx=ctx)
+    M.nitref, M.force_itref = 1, True
+    dofs, n_loc = M.local_dofs()
+    p = _lib.Profile()
+    _lib.check(_lib.lib.cpk_profile_kernels(ctx.h, A.h, Cm.h, M.h, 20, C.byref(p)))
+    # a fixed 20-iteration solve (tolerance 0): wall time per iteration of the rank's kernels
+    dev = torch.device("cuda", 0)
+    b1 = torch.from_numpy(np.ascontiguousarray(S["rhs"][dofs[:n_loc]])).to(dev)
+    xy = torch.empty(max(len(dofs), 1), dtype=torch.float64, device=dev)
+    opts = _lib.make_opts(dict(atol=0.0, rtol=0.0, itmax=20, print=False, nitref=1, force_itref=True))
+    st = _lib.Stats()
+    hist = np.zeros(64)
+    st.hist = hist.ctypes.data_as(C.POINTER(C.c_double))
+    st.hist_cap = 64
+    per_it = None
+    err = None
+    try:
+        for rep in range(3):
+            ctx.synchronize()
+            t = time.perf_counter()
+            _lib.check(_lib.lib.cpk_method_solve_device(ctx.h, 2, C.c_void_p(b1.data_ptr()), A.h, Cm.h, M.h,
+                                                        C.byref(opts), C.c_void_p(xy.data_ptr()), C.byref(st)))
+            ctx.synchronize()
+            dt = time.perf_counter() - t
+        per_it = dt / max(int(st.niters), 1) * 1e3
+    except cpk.CpkError as e:
+        err = str(e)[:120]
+    print(json.dumps({"P": P, "rank": r, "N_loc": len(dofs), "nrounds": M.info["nrounds"],
+                      "spmv_us": round(p.spmv_ms * 1e3, 1), "resid_us": round(p.resid_ms * 1e3, 1),
+                      "fwd_us": round(p.fwd_ms * 1e3, 1), "bwd_us": round(p.bwd_ms * 1e3, 1),
+                      "apply_us": round(p.apply_ms * 1e3, 1), "niters": int(st.niters),
+                      "ms_per_iter_no_comm": per_it and round(per_it, 4), "error": err}), flush=True)
+    del M, A, B, Cm, G
+    ctx.close()

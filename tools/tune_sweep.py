@@ -16,7 +16,7 @@ for cfg in sys.argv[1:]:
     M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
     M.nitref, M.force_itref = 1, True
     p = _lib.Profile()
-    _lib.check(_lib.lib.cpk_profile_kernels(ctx.h, A.h, Cm.h, M.h, 20, C.byref(p)))
+    _lib.check(_lib.lib.cpk_profile_kernels(ctx.h, A.h, Cm.h, M.h, int(os.environ.get("REPS", "20")), C.byref(p)))
     print(f"{cfg:16s} rounds {M.info['nrounds']} blocks {M.info['nblocks']:6d} fwd {p.fwd_ms*1e3:7.1f} us "
           f"({p.fwd_bytes/p.fwd_ms/1e6:6.0f} GB/s) bwd {p.bwd_ms*1e3:7.1f} us ({p.bwd_bytes/p.bwd_ms/1e6:6.0f} GB/s) "
           f"apply {p.apply_ms*1e3:7.1f} us resid {p.resid_ms*1e3:6.1f} us spmv {p.spmv_ms*1e3:6.1f} us", flush=True)
