@@ -118,6 +118,7 @@ struct DFactor {
     DBuf<int32_t> meta;     // [nblk][8]: r0, r1, l0, l1, fwd e0, e1, bwd e0, e1
     bool pipelined = true;  // round 0 through the persistent pipelined kernel
     std::vector<int64_t> round_ptr;  // host copy: blocks per round
+    std::vector<char> round_fits;    // host: every block of round r fits (sweep_rows[1], sweep_cap[1])
     int sweep_rows[2] = {192, 1024}, sweep_cap[2] = {576, 4096}, sweep_threads[2] = {64, 512};  // round 0 / rest
     size_t bytes() const {
         return fptr.bytes() + fcol.bytes() + fval.bytes() + bptr.bytes() + bcol.bytes() + bval.bytes() + D.bytes() +

@@ -16,6 +16,8 @@
 
 namespace cpk {
 
+constexpr size_t kFactorPadEntries = 64;  // zero entries after fcol/fval/bcol/bval
+
 void Ctx::ensure_partials(size_t count) {
     if (partials.n < count) partials.alloc(count);
     if (!counter.n) {
@@ -107,6 +109,18 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
             for (size_t t = 0; t < row.size(); t++) bcol[bptr[j] + t] = row[t].second.first, bval[bptr[j] + t] = row[t].second.second;
         }
     }
+    // rounds whose blocks all fit the upper-round staging image (sptrsv_upper_kernel)
+    d.round_fits.assign(s.round_ptr.empty() ? 0 : s.round_ptr.size() - 1, 1);
+    for (size_t r = 0; r < d.round_fits.size(); r++)
+        for (int64_t b = s.round_ptr[r]; b < s.round_ptr[r + 1]; b++) {
+            const int64_t r0 = s.lvl_row[s.blk_lvl[b]], r1 = s.lvl_row[s.blk_lvl[b + 1]];
+            if (r1 - r0 > d.sweep_rows[1] || fptr[r1] - fptr[r0] > (uint32_t)d.sweep_cap[1] ||
+                bptr[r1] - bptr[r0] > (uint32_t)d.sweep_cap[1])
+                d.round_fits[r] = 0;
+        }
+    // padding entries: clamped, unconditional loads may touch one entry past a block's end
+    fcol.resize(fcol.size() + kFactorPadEntries, 0), fval.resize(fval.size() + kFactorPadEntries, 0.0);
+    bcol.resize(bcol.size() + kFactorPadEntries, 0), bval.resize(bval.size() + kFactorPadEntries, 0.0);
     d.fptr.upload(fptr);
     d.fcol.upload(fcol);
     d.fval.upload(fval);
@@ -591,7 +605,7 @@ __device__ __forceinline__ void fold_prefix(SweepLds &S, int nr, int tid = -1) {
 // still subtracted one at a time in the reference's order.  skip_first: the first level holds
 // only rows without entries (their values are already in place), as in round 0 forward.
 // PS: rows start at ps[k] (after fold_prefix) instead of p[k].
-template <int TPB, bool BWD, bool PS = false, int CH = 4>
+template <int TPB, bool BWD, bool PS = false, int CH = 4, bool WAVE = false>
 __device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_first = false, int tid = -1) {
     if (tid < 0) tid = threadIdx.x;
     static_assert(CH <= kSweepPad, "chunk wider than the padding");
@@ -622,7 +636,8 @@ __device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_firs
             }
             S.w[k] = acc;
         }
-        __syncthreads();
+        if (WAVE) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: LDS in program order
+        else __syncthreads();
         l = ln, a = an, z = zn;
     }
 }
@@ -754,6 +769,112 @@ __global__ __launch_bounds__(TPB) void sptrsv_bwd_kernel(
 struct BlkMeta {
     int32_t r0, r1, l0, l1, fe0, fe1, be0, be1;
 };
+
+// ---- upper rounds ------------------------------------------------------------------------------
+// One workgroup per block, as sptrsv_fwd_kernel / sptrsv_bwd_kernel, with the staging laid out
+// for memory-level parallelism: the block's 32-byte record is one scalar load, every thread
+// issues all of its row and entry loads at once, then all of its gathers (input through perm,
+// w of outside-block columns) with clamped, unconditional addresses, so staging costs about two
+// dependent round trips instead of one per predicated slot.  Fold and levels as before.
+template <int TPB, int RPU, int EPU, bool BWD, bool ADD>
+__global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
+    int64_t blk0, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
+    const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
+    const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
+    double *w, double *out, const int *run, const int *active) {
+    constexpr int R = RPU * TPB, CAP = EPU * TPB;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (skip(run, active)) return;
+    const BlkMeta m = meta[blk0 + blockIdx.x];
+    const int r0 = m.r0, r1 = m.r1, nr = r1 - r0, nl = m.l1 - m.l0;
+    const uint32_t e0 = BWD ? (uint32_t)m.be0 : (uint32_t)m.fe0;
+    const int ne = BWD ? m.be1 - m.be0 : m.fe1 - m.fe0;
+    const int tid = threadIdx.x;
+    SweepLds S(smem, R, CAP);
+    uint32_t q[RPU];
+    int32_t sp[RPU];
+    double a[RPU], d[RPU];
+    int32_t c[EPU];
+    double v[EPU], g[EPU];
+#pragma unroll
+    for (int j = 0; j < RPU; j++) {
+        const int i = tid + j * TPB, rr = r0 + (i < nr ? i : nr - 1);
+        q[j] = ptr[rr], sp[j] = perm[rr];
+        if (BWD) a[j] = w[rr], d[j] = D[rr];
+    }
+#pragma unroll
+    for (int u = 0; u < EPU; u++) {
+        const int e = tid + u * TPB;
+        const uint32_t ec = e0 + (uint32_t)(e < ne ? e : 0);
+        c[u] = __builtin_nontemporal_load(col + ec), v[u] = __builtin_nontemporal_load(val + ec);
+    }
+    for (int l = tid; l <= nl; l += TPB) S.lv[l] = (int16_t)(lvl_row[m.l0 + l] - r0);
+#pragma unroll
+    for (int j = 0; j < RPU; j++) {
+        if (!BWD) a[j] = xin[sp[j]];
+    }
+#pragma unroll
+    for (int u = 0; u < EPU; u++) g[u] = w[(c[u] >= r0 && c[u] < r1) ? r0 : c[u]];
+#pragma unroll
+    for (int j = 0; j < RPU; j++) {
+        const int i = tid + j * TPB;
+        if (i < nr) {
+            S.p[i] = (int16_t)(q[j] - e0);
+            S.w[i] = BWD ? a[j] / d[j] : ((sp[j] >= neg_from) ? -a[j] : a[j]);
+        }
+    }
+    if (tid == 0) S.p[nr] = (int16_t)ne;
+#pragma unroll
+    for (int u = 0; u < EPU; u++) {
+        const int e = tid + u * TPB;
+        if (e < ne) {
+            const bool local = c[u] >= r0 && c[u] < r1;
+            S.c[e] = local ? (int16_t)(c[u] - r0) : (int16_t)-1;
+            S.v[e] = local ? v[u] : v[u] * g[u];
+        }
+    }
+    __syncthreads();
+    fold_prefix<TPB>(S, nr);
+    // levels on one wave: a level holds a few rows, and without a workgroup barrier per level
+    // (a single wave's LDS accesses complete in program order) the chain is LDS latency only
+    if (tid < kWave) sweep_levels<kWave, BWD, true, 8, true>(S, nl, false, tid);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RPU; j++) {
+        const int i = tid + j * TPB;
+        if (i < nr) {
+            const double z = S.w[i];
+            w[r0 + i] = z;
+            if (BWD) out[sp[j]] = ADD ? out[sp[j]] + z : z;
+        }
+    }
+}
+
+// upper round r through sptrsv_upper_kernel when the configuration matches an instantiation
+static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add, const double *xin,
+                        int64_t neg_from, double *w, double *out, const int *run, const int *active) {
+    constexpr int TPB = 512, RPU = 2, EPU = 8;
+    if (getenv("CPK_NO_UPPER") || F.sweep_threads[1] != TPB || F.sweep_rows[1] > RPU * TPB ||
+        F.sweep_cap[1] > EPU * TPB || r >= (int64_t)F.round_fits.size() || !F.round_fits[r])
+        return false;
+    const int64_t b0 = F.round_ptr[r], nb = F.round_ptr[r + 1] - b0;
+    if (!nb) return true;
+    const size_t lds = sweep_lds_bytes(F.sweep_rows[1], F.sweep_cap[1]);
+    const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
+    if (!bwd)
+        hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, false, false>), dim3((unsigned)nb), dim3(TPB), lds,
+                           c.stream, b0, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p, F.perm.p, xin,
+                           neg_from, w, out, run, active);
+    else if (add)
+        hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, true>), dim3((unsigned)nb), dim3(TPB), lds,
+                           c.stream, b0, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, xin,
+                           neg_from, w, out, run, active);
+    else
+        hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, false>), dim3((unsigned)nb), dim3(TPB), lds,
+                           c.stream, b0, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, xin,
+                           neg_from, w, out, run, active);
+    return true;
+}
 
 // SPLIT > 1: the workgroup is one wave holding SPLIT independent logical blocks of TPB lanes
 // (TPB * SPLIT = 64), each with its own LDS image.  A level that occupies a few rows then costs
@@ -943,6 +1064,7 @@ static void fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
     const int64_t R = (int64_t)F.round_ptr.size() - 1;
     for (int64_t r = 0; r < R; r++) {
         if (r == 0 && MODE == 0 && pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active)) continue;
+        if (r > 0 && MODE == 0 && upper_round(c, F, r, false, false, xin, neg_from, w, nullptr, run, active)) continue;
         switch (F.sweep_threads[r == 0 ? 0 : 1]) {
         case 32: fwd_round<32, MODE>(c, F, r, xin, neg_from, w, run, active); break;
         case 64: fwd_round<64, MODE>(c, F, r, xin, neg_from, w, run, active); break;
@@ -969,6 +1091,7 @@ void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
     const int64_t R = (int64_t)F.round_ptr.size() - 1;
     for (int64_t r = R - 1; r >= 0; r--) {
         if (r == 0 && pipe_round0(c, F, true, add, nullptr, 0, w, out, run, active)) continue;
+        if (r > 0 && upper_round(c, F, r, true, add, nullptr, 0, w, out, run, active)) continue;
         switch (F.sweep_threads[r == 0 ? 0 : 1] * 2 + (add ? 1 : 0)) {
         case 64: bwd_round<32, false>(c, F, r, w, out, run, active); break;
         case 65: bwd_round<32, true>(c, F, r, w, out, run, active); break;

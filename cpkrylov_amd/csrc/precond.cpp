@@ -63,15 +63,15 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
     pc->Kp = std::move(an.Kp);
     pc->S = std::move(an.S);
     make_dmat(pc->Kp, pc->dKp);
+    for (int i = 0; i < 2; i++)  // before make_dfactor: the device layout follows the configuration
+        pc->dF.sweep_rows[i] = an.sweep.rows[i], pc->dF.sweep_cap[i] = an.sweep.cap[i],
+        pc->dF.sweep_threads[i] = an.sweep.threads[i];
     {
         const std::vector<int64_t> key(pc->S.order.begin(), pc->S.order.end());
         make_dfactor(an.F, pc->S, pc->dF, &key);
     }
     an.F = Factor();
     pc->F = std::move(an.F0);
-    for (int i = 0; i < 2; i++)
-        pc->dF.sweep_rows[i] = an.sweep.rows[i], pc->dF.sweep_cap[i] = an.sweep.cap[i],
-        pc->dF.sweep_threads[i] = an.sweep.threads[i];
     pc->w.alloc(pc->N);
     pc->r.alloc(pc->N);
     pc->active.alloc(1);
@@ -100,6 +100,8 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an) {
     for (int64_t j = 0; j < rp.nsub; j++) nextra[j] = (int64_t)rp.extra[j].size();
     const SweepConfig &sw = an.sweep;
     Schedule S = build_schedule(rp.Fsub, sw.rows[0], sw.cap[0], sw.rows[1], sw.cap[1], sw.sub0, &nextra);
+    for (int i = 0; i < 2; i++)
+        pc->dF.sweep_rows[i] = sw.rows[i], pc->dF.sweep_cap[i] = sw.cap[i], pc->dF.sweep_threads[i] = sw.threads[i];
     {
         Factor Fl = relabel(rp.Fsub, S);
         std::vector<int64_t> key(rp.nsub);
@@ -116,8 +118,6 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an) {
         pc->sep.send.upload(send);
         pc->sep.nsend = (int64_t)send.size();
     }
-    for (int i = 0; i < 2; i++)
-        pc->dF.sweep_rows[i] = sw.rows[i], pc->dF.sweep_cap[i] = sw.cap[i], pc->dF.sweep_threads[i] = sw.threads[i];
     // separator solve
     DSep &T = pc->sep;
     T.nT = rp.nT, T.kt = rp.kt, T.nlev = (int64_t)rp.tlev_ptr.size() - 1, T.ntdof = (int64_t)rp.tdof.size();
