@@ -290,7 +290,6 @@ void launch_spmv_resid_norm(Ctx &c, const DMat &A, const double *xin, int64_t ne
                             double tol, int *active_out, const int *run, const int *active) {
     launch_halo(c, A, y);
     const bool dist = c.dist();
-    if (dist) CPK_HIP(hipMemsetAsync(c.red.p, 0, 2 * sizeof(double), c.stream));  // a rank with no rows adds 0
     if (A.nblk) {
         c.ensure_partials((size_t)A.nblk * 2);
         EpiResidNorm e{xin, neg_from, r, tol, active_out, RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr},

@@ -107,6 +107,9 @@ inline void launch_ew(Ctx &c, int64_t N, const F &f) {
 }
 // Distributed mode: the reduction kernel leaves its local sums in c.red, RCCL allreduces them
 // and this single-thread kernel runs the epilogue on the global sums (identical on every rank).
+// Every reduction grid has at least one workgroup, so a rank with no rows still writes its zero
+// sums; when the step is not live the kernel writes nothing, and the epilogue, which tests the
+// same device predicate, ignores the buffer.
 template <class F>
 __global__ void ewred_fin_kernel(F f, const double *tot) {
     if (threadIdx.x || blockIdx.x) return;
@@ -116,7 +119,6 @@ template <int NV, class F>
 inline void launch_ewred(Ctx &c, int64_t N, const F &f) {
     c.ensure_partials((size_t)ew_grid(N) * NV);
     const bool dist = c.dist();
-    if (dist) CPK_HIP(hipMemsetAsync(c.red.p, 0, NV * sizeof(double), c.stream));
     hipLaunchKernelGGL((ewred_kernel<NV, F>), dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f,
                        RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr});
     if (dist) {

@@ -146,7 +146,6 @@ void launch_krylov_spmv(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n
                                dim3(256), 0, c.stream, pol, st, AC.send.p, AC.nsend, AC.sbuf.p);
         c.comm->allgather(AC.sbuf.p, AC.rbuf.p, (size_t)AC.kmax, c.stream);
     }
-    if (dist) CPK_HIP(hipMemsetAsync(c.red.p, 0, 2 * sizeof(double), c.stream));
     EpiKrylov<P> e{st, nullptr, y, n, RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr}, pol};
     const unsigned grid = spmv_grid(AC.nblk, true);
     if (AC.halo())
@@ -830,7 +829,6 @@ static void launch_arnoldi_dots(Ctx &c, DState *st, double *V, const double *w, 
                                 int64_t ring, int64_t maxv) {
     const bool dist = c.dist();
     if (dist && (size_t)(2 * maxv) > c.red.n) throw Error(CPK_ERR_UNSUPPORTED, "Arnoldi window too wide for the distributed reduction buffer");
-    if (dist) CPK_HIP(hipMemsetAsync(c.red.p, 0, 2 * maxv * sizeof(double), c.stream));
     hipLaunchKernelGGL(arnoldi_dots_kernel, dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, st, V, w, ut, n, N, ring, maxv,
                        RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr});
     if (dist) {
