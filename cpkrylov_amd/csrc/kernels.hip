@@ -544,14 +544,14 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
 // contiguously.  Each row still subtracts its terms in the reference's order, one rounding per
 // product and per subtraction, so the result is bit-identical to the direct path.
 // LDS image of a staged block (dynamic shared memory, sized per launch):
-//   double w[R] | double v[CAP + 8] | int16 c[CAP + 8] | int16 p[R + 1] | int16 lv[R + 1] | int16 ps[R + 1]
+//   double w[R + 1] | double v[CAP + 8] | int16 c[CAP + 8] | int16 p[R + 1] | int16 lv[R + 1] | int16 ps[R + 1]
 constexpr int kSweepPad = 8;  // entry arrays padded for the branchless 8-entry chunks
 struct SweepLds {
     double *w, *v;
     int16_t *c, *p, *lv, *ps;
     __device__ SweepLds(char *smem, int R, int CAP) {
         w = reinterpret_cast<double *>(smem);
-        v = w + R;
+        v = w + R + 1;  // w[R]: the 1.0 slot of sweep_levels<..., ONE>
         c = reinterpret_cast<int16_t *>(v + CAP + kSweepPad);
         p = c + CAP + kSweepPad;
         lv = p + R + 1;
@@ -559,7 +559,7 @@ struct SweepLds {
     }
 };
 __host__ __device__ constexpr size_t sweep_lds_bytes_dev(int R, int CAP) {
-    return ((size_t)8 * R + 10 * ((size_t)CAP + kSweepPad) + 6 * ((size_t)R + 1) + 15) & ~(size_t)15;
+    return ((size_t)8 * (R + 1) + 10 * ((size_t)CAP + kSweepPad) + 6 * ((size_t)R + 1) + 15) & ~(size_t)15;
 }
 size_t sweep_lds_bytes(int R, int CAP) { return sweep_lds_bytes_dev(R, CAP); }
 
@@ -604,7 +604,10 @@ __device__ __forceinline__ void fold_prefix(SweepLds &S, int nr, int tid = -1) {
 // still subtracted one at a time in the reference's order.  skip_first: the first level holds
 // only rows without entries (their values are already in place), as in round 0 forward.
 // PS: rows start at ps[k] (after fold_prefix) instead of p[k].
-template <int TPB, bool BWD, bool PS = false, int CH = 4, bool WAVE = false>
+// ONE: outside-block terms are staged against the 1.0 slot w[R] (column R, value pre-multiplied:
+// an exact product) and the padding after the block's entries holds column R, so every column
+// read is a valid LDS index and the loop needs no select on the column.
+template <int TPB, bool BWD, bool PS = false, int CH = 4, bool WAVE = false, bool ONE = false>
 __device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_first = false, int tid = -1) {
     if (tid < 0) tid = threadIdx.x;
     static_assert(CH <= kSweepPad, "chunk wider than the padding");
@@ -625,12 +628,19 @@ __device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_firs
                 double v[CH], x[CH];
 #pragma unroll
                 for (int j = 0; j < CH; j++) c[j] = S.c[e + j], v[j] = S.v[e + j];
+                if (ONE) {
 #pragma unroll
-                for (int j = 0; j < CH; j++) x[j] = S.w[(c[j] >= 0 && e + j < e1) ? c[j] : 0];
+                    for (int j = 0; j < CH; j++) x[j] = S.w[c[j]];
 #pragma unroll
-                for (int j = 0; j < CH; j++) {
-                    const double t = (c[j] >= 0) ? v[j] * x[j] : v[j];
-                    acc -= (e + j < e1) ? t : 0.0;
+                    for (int j = 0; j < CH; j++) acc -= (e + j < e1) ? v[j] * x[j] : 0.0;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < CH; j++) x[j] = S.w[(c[j] >= 0 && e + j < e1) ? c[j] : 0];
+#pragma unroll
+                    for (int j = 0; j < CH; j++) {
+                        const double t = (c[j] >= 0) ? v[j] * x[j] : v[j];
+                        acc -= (e + j < e1) ? t : 0.0;
+                    }
                 }
             }
             S.w[k] = acc;
@@ -906,11 +916,10 @@ __global__ __launch_bounds__(TPB * SPLIT) void sptrsv_pipe_kernel(
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             const int i = tid + j * TPB;
-            if (i < nr) {
-                q[j] = ptr[m.r0 + i];
-                sp[j] = perm[m.r0 + i];
-                if (BWD) wr[j] = w[m.r0 + i], dr[j] = D[m.r0 + i];
-            }
+            const int rr = m.r0 + (i < nr ? i : nr - 1);  // clamped: later gathers need no predicate
+            q[j] = ptr[rr];
+            sp[j] = perm[rr];
+            if (BWD) wr[j] = w[rr], dr[j] = D[rr];
             if (i < nl) lvr[j] = lvl_row[m.l0 + i];
         }
 #pragma unroll
@@ -930,33 +939,46 @@ __global__ __launch_bounds__(TPB * SPLIT) void sptrsv_pipe_kernel(
         const uint32_t e0 = BWD ? (uint32_t)cur.be0 : (uint32_t)cur.fe0;
         const int ne = BWD ? cur.be1 - cur.be0 : cur.fe1 - cur.fe0;
         const int r0 = cur.r0, r1 = cur.r1;
-        // registers -> LDS, with the dependent gathers
+        // registers -> LDS, with the dependent gathers (all in flight at once: forward the input
+        // through perm, backward-accumulate the output rows read back after the levels)
+        double xg[RPT];
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            if (!BWD) xg[j] = xin[sp[j]];
+            if (BWD && ADD) xg[j] = out[sp[j]];
+        }
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             const int i = tid + j * TPB;
             if (i < nr) {
                 S.p[i] = (int16_t)(q[j] - e0);
-                if (BWD) {
-                    S.w[i] = wr[j] / dr[j];
-                } else {
-                    const double x = xin[sp[j]];
-                    S.w[i] = (sp[j] >= neg_from) ? -x : x;
-                }
+                if (BWD) S.w[i] = wr[j] / dr[j];
+                else S.w[i] = (sp[j] >= neg_from) ? -xg[j] : xg[j];
             }
             if (i < nl) S.lv[i] = (int16_t)(lvr[j] - r0);
         }
         int32_t dst[RPT];
 #pragma unroll
         for (int j = 0; j < RPT; j++) dst[j] = sp[j];
-        if (tid == 0) S.p[nr] = (int16_t)ne, S.lv[nl] = (int16_t)nr;
+        if (tid == 0) S.p[nr] = (int16_t)ne, S.lv[nl] = (int16_t)nr, S.w[R] = 1.0;
+        if (tid < kSweepPad) S.c[ne + tid] = (int16_t)R;
+        double g[EPT];  // backward: w of the rows of earlier launches, every gather in flight at once
+        if (BWD) {
+#pragma unroll
+            for (int j = 0; j < EPT; j++) {
+                const int e = tid + j * TPB;
+                const bool out = e < ne && (cc[j] < r0 || cc[j] >= r1);
+                g[j] = w[out ? cc[j] : r0];
+            }
+        }
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
             const int e = tid + j * TPB;
             if (e < ne) {
                 const int32_t c = cc[j];
                 const bool local = c >= r0 && c < r1;
-                S.c[e] = local ? (int16_t)(c - r0) : (int16_t)-1;
-                S.v[e] = local ? vv[j] : vv[j] * w[c];
+                S.c[e] = local ? (int16_t)(c - r0) : (int16_t)R;
+                S.v[e] = local ? vv[j] : vv[j] * (BWD ? g[j] : w[c]);
             }
         }
         __syncthreads();
@@ -966,14 +988,14 @@ __global__ __launch_bounds__(TPB * SPLIT) void sptrsv_pipe_kernel(
             nxt = meta[bn];
             issue(nxt);  // in flight during the level phase
         }
-        sweep_levels<TPB, BWD>(S, nl, true, tid);
+        sweep_levels<TPB, BWD, false, 4, false, true>(S, nl, true, tid);
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             const int i = tid + j * TPB;
             if (i < nr) {
                 const double z = S.w[i];
                 w[r0 + i] = z;
-                if (BWD) out[dst[j]] = ADD ? out[dst[j]] + z : z;
+                if (BWD) out[dst[j]] = ADD ? xg[j] + z : z;
             }
         }
         if (bn >= bend) break;
