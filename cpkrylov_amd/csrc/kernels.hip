@@ -545,7 +545,10 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
 // product and per subtraction, so the result is bit-identical to the direct path.
 // LDS image of a staged block (dynamic shared memory, sized per launch):
 //   double w[R + 1] | double v[CAP + 8] | int16 c[CAP + 8] | int16 p[R + 1] | int16 lv[R + 1] | int16 ps[R + 1]
-constexpr int kSweepPad = 8;  // entry arrays padded for the branchless 8-entry chunks
+constexpr int kSweepPad = 8;
+#ifndef CPK_PIPE_CH
+#define CPK_PIPE_CH 2  // entries per LDS round trip in the round-0 level loop
+#endif  // entry arrays padded for the branchless 8-entry chunks
 struct SweepLds {
     double *w, *v;
     int16_t *c, *p, *lv, *ps;
@@ -988,7 +991,7 @@ __global__ __launch_bounds__(TPB * SPLIT) void sptrsv_pipe_kernel(
             nxt = meta[bn];
             issue(nxt);  // in flight during the level phase
         }
-        sweep_levels<TPB, BWD, false, 4, false, true>(S, nl, true, tid);
+        sweep_levels<TPB, BWD, false, CPK_PIPE_CH, false, true>(S, nl, true, tid);
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             const int i = tid + j * TPB;
