@@ -546,6 +546,9 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
 // LDS image of a staged block (dynamic shared memory, sized per launch):
 //   double w[R + 1] | double v[CAP + 8] | int16 c[CAP + 8] | int16 p[R + 1] | int16 lv[R + 1] | int16 ps[R + 1]
 constexpr int kSweepPad = 8;
+#ifndef CPK_UPPER_CH
+#define CPK_UPPER_CH 4  // entries per LDS round trip in the upper-round level loop
+#endif
 #ifndef CPK_PIPE_CH
 #define CPK_PIPE_CH 2  // entries per LDS round trip in the round-0 level loop
 #endif  // entry arrays padded for the branchless 8-entry chunks
@@ -572,8 +575,8 @@ size_t sweep_lds_bytes(int R, int CAP) { return sweep_lds_bytes_dev(R, CAP); }
 // Same operations in the same order, so the result is bit-identical.  This is what makes the
 // upper rounds cheap: a separator row's many references into the subtrees below are all
 // outside its block.
-template <int TPB>
-__device__ __forceinline__ void fold_prefix(SweepLds &S, int nr, int tid = -1) {
+template <int TPB, int OUTC = -1>  // OUTC: column marking outside terms (-1, or R for the 1.0 slot)
+__device__ __forceinline__ void fold_prefix(SweepLds &S, int nr, int tid = -1, int outc = OUTC) {
     if (tid < 0) tid = threadIdx.x;
     for (int i = tid; i < nr; i += TPB) {
         int e = S.p[i];
@@ -587,7 +590,7 @@ __device__ __forceinline__ void fold_prefix(SweepLds &S, int nr, int tid = -1) {
             int t = 0;
 #pragma unroll
             for (int j = 0; j < kSweepPad; j++) {
-                const bool take = t == j && e + j < e1 && c[j] < 0;
+                const bool take = t == j && e + j < e1 && (OUTC < 0 ? c[j] < 0 : c[j] == outc);
                 acc -= take ? v[j] : 0.0;
                 t += take;
             }
@@ -835,21 +838,22 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
             S.w[i] = BWD ? a[j] / d[j] : ((sp[j] >= neg_from) ? -a[j] : a[j]);
         }
     }
-    if (tid == 0) S.p[nr] = (int16_t)ne;
+    if (tid == 0) S.p[nr] = (int16_t)ne, S.w[R] = 1.0;
+    if (tid < kSweepPad) S.c[ne + tid] = (int16_t)R;
 #pragma unroll
     for (int u = 0; u < EPU; u++) {
         const int e = tid + u * TPB;
         if (e < ne) {
             const bool local = c[u] >= r0 && c[u] < r1;
-            S.c[e] = local ? (int16_t)(c[u] - r0) : (int16_t)-1;
+            S.c[e] = local ? (int16_t)(c[u] - r0) : (int16_t)R;  // outside: pre-multiplied, 1.0 slot
             S.v[e] = local ? v[u] : v[u] * g[u];
         }
     }
     __syncthreads();
-    fold_prefix<TPB>(S, nr);
+    fold_prefix<TPB, 1>(S, nr, -1, R);
     // levels on one wave: a level holds a few rows, and without a workgroup barrier per level
     // (a single wave's LDS accesses complete in program order) the chain is LDS latency only
-    if (tid < kWave) sweep_levels<kWave, BWD, true, 8, true>(S, nl, false, tid);
+    if (tid < kWave) sweep_levels<kWave, BWD, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < RPU; j++) {
@@ -871,7 +875,7 @@ static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add,
         return false;
     const int64_t b0 = F.round_ptr[r], nb = F.round_ptr[r + 1] - b0;
     if (!nb) return true;
-    const size_t lds = sweep_lds_bytes(F.sweep_rows[1], F.sweep_cap[1]);
+    const size_t lds = sweep_lds_bytes(RPU * TPB, EPU * TPB);  // the kernel's image (>= the configured block)
     const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
     if (!bwd)
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, false, false>), dim3((unsigned)nb), dim3(TPB), lds,
@@ -893,7 +897,7 @@ static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add,
 // one instruction stream for SPLIT blocks instead of one per block; lanes of different logical
 // blocks never synchronise (within a single wave __syncthreads is a no-op fence).
 template <int TPB, int RPT, int EPT, bool BWD, bool ADD, int SPLIT = 1>
-__global__ __launch_bounds__(TPB * SPLIT) void sptrsv_pipe_kernel(
+__global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(4))) void sptrsv_pipe_kernel(
     int64_t blk0, int64_t nblk, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,

@@ -96,7 +96,10 @@ __global__ __launch_bounds__(kBlock) void spmv_stream(const uint32_t *__restrict
 }
 
 // grid of a launch: one row block per workgroup, or a bounded grid for reducing epilogues
-constexpr int64_t kSpmvRedGrid = 2048;
+#ifndef CPK_SPMV_RED_GRID
+#define CPK_SPMV_RED_GRID 2048
+#endif
+constexpr int64_t kSpmvRedGrid = CPK_SPMV_RED_GRID;
 inline unsigned spmv_grid(int64_t nblk, bool reduces) {
     return (unsigned)(reduces ? std::min<int64_t>(nblk, kSpmvRedGrid) : nblk);
 }
