@@ -62,6 +62,7 @@ _SIGS = {
     "cpk_pc_destroy": ([vp], C.c_int),
     "cpk_pc_set": ([vp, P(Opts)], C.c_int),
     "cpk_pc_get": ([vp] + [P(C.c_double)] * 4, C.c_int),
+    "cpk_pc_set_handle": ([vp, C.c_int], C.c_int),
     "cpk_pc_apply": ([vp, P(C.c_double), P(C.c_double)], C.c_int),
     "cpk_pc_apply_device": ([vp, vp, vp], C.c_int),
     "cpk_pc_divide": ([vp, P(C.c_double), P(C.c_double)], C.c_int),

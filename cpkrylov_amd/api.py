@@ -180,6 +180,16 @@ class opLDL2:
     force_itref = property(lambda s: bool(s._get()[2]), lambda s, v: s._set(force_itref=v))
     residual_update = property(lambda s: s._get()[3], lambda s, v: s._set(residual_update=v))
 
+    @property
+    def handle_semantics(self):
+        """Opt-in (not in the reference): keep op.Aty / op.Cy between applies (cpk_pc_set_handle)."""
+        return getattr(self, "_handle", False)
+
+    @handle_semantics.setter
+    def handle_semantics(self, on):
+        check(lib.cpk_pc_set_handle(self.h, 1 if on else 0))
+        self._handle = bool(on)
+
     # ---- operator surface --------------------------------------------------------------------
     def __mul__(self, z):
         z = np.ascontiguousarray(z, dtype=np.float64).ravel()

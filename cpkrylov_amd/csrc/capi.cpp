@@ -346,6 +346,13 @@ int cpk_pc_get(cpk_pc M, double *nitref, double *itref_tol, double *force_itref,
     API_END
 }
 
+int cpk_pc_set_handle(cpk_pc M, int on) {
+    API_BEGIN
+    need(M, "NULL argument");
+    M->p->set_handle(on != 0);
+    API_END
+}
+
 int cpk_pc_apply(cpk_pc M, const double *x, double *y) {
     API_BEGIN
     need(M && x && y, "NULL argument");

@@ -176,6 +176,9 @@ Comm *make_null_comm(int rank);  // diagnostic: CPK_COMM=null
 void launch_sum_slots(hipStream_t s, const double *slots, int P, size_t n, double *out);
 struct DSep;
 // pack this rank's separator payload (w rows read by T, rank 0: +-x at the T dofs), allgather
+// t = x_eff - g with x_eff[i] = (i >= neg_from ? -x[i] : x[i])  (the GHN residual update)
+void launch_sub_state(Ctx &c, const double *x, int64_t neg_from, const double *g, int64_t N, double *t,
+                      const int *run);
 void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x, int64_t neg_from);
 // redundant separator solve into wT (= w + nsub); rank 0 writes (add: accumulates) y at the T dofs
 void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active);
@@ -229,11 +232,17 @@ struct Precond {
     DBuf<int> active;    // refinement predicate
     // public properties of opLDL2 (opLDL2.m:45-50)
     double nitref = 3, itref_tol = 1.0e-8, force_itref = 0, residual_update = 0;
+    // opt-in handle semantics of the residual-update state (opLDL2.m:164-172 as reg_cpkrylov.m:
+    // 47-52 intends): ghn = [op.Aty; op.Cy] persists between applies.  Off by default: Spot
+    // operators are value objects, so in the reference the state never survives a multiply.
+    bool handle = false;
+    DBuf<double> ghn, t;
     double ptime = 0;
     // cached solvers (workspace + captured iteration graphs), keyed; see solvers.hip
     std::vector<std::pair<std::string, std::shared_ptr<void>>> solvers;
     // y = M*x  (opLDL2.multiply); all pointers on the device, enqueued on ctx->stream
     void apply(const double *x, int64_t neg_from, double *y, const int *run);
+    void set_handle(bool on);  // enabling or disabling clears the state
     void ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run, const int *act);
     // algorithmic HBM bytes of one apply
     double apply_bytes() const;

@@ -1139,6 +1139,23 @@ void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
 }
 
 // ---- small helpers ---------------------------------------------------------------------------
+__global__ void sub_state_kernel(const double *__restrict__ x, int64_t neg_from, const double *__restrict__ g,
+                                 int64_t N, double *__restrict__ t, const int *run) {
+    if (run && *run == 0) return;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        const double xi = i >= neg_from ? -x[i] : x[i];
+        t[i] = xi - g[i];
+    }
+}
+
+void launch_sub_state(Ctx &c, const double *x, int64_t neg_from, const double *g, int64_t N, double *t,
+                      const int *run) {
+    if (N <= 0) return;
+    const int grid = (int)std::min<int64_t>((N + kBlock - 1) / kBlock, 2048);
+    hipLaunchKernelGGL(sub_state_kernel, dim3(grid), dim3(kBlock), 0, c.stream, x, neg_from, g, N, t, run);
+    CPK_HIP(hipGetLastError());
+}
+
 __global__ void set_concat_kernel(double *dst, const double *a, int64_t na, int64_t nb) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < na + nb; i += (int64_t)gridDim.x * blockDim.x)
         dst[i] = i < na ? a[i] : 0.0;

@@ -161,10 +161,29 @@ void Precond::ldl_solve(const double *xin, int64_t neg_from, double *y, bool add
     launch_sptrsv_bwd(c, dF, w.p, y, add, run, act);
 }
 
+void Precond::set_handle(bool on) {
+    if (on && dist) throw Error(CPK_ERR_UNSUPPORTED, "handle semantics of the residual update: single-GPU only");
+    handle = on;
+    if (on) {
+        if (ghn.n < (size_t)N) ghn.alloc(N), t.alloc(N);
+        ghn.zero(ctx->stream);
+        CPK_HIP(hipStreamSynchronize(ctx->stream));
+    }
+}
+
 void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run) {
     Ctx &c = *ctx;
-    // y = op.LDL * x   (opLDL2.m:165-167)
-    ldl_solve(x, neg_from, y, false, run, nullptr);
+    if (residual_update != 0 && handle) {
+        // y = op.LDL * [x(1:n) - op.Aty; x(n+1:N) - op.Cy]; then op.Aty = op.A(1:n, n+1:N) * y2,
+        // op.Cy = op.A(n+1:N, n+1:N) * y2 = the columns n+1:N of Kp times y2  (opLDL2.m:164-172)
+        launch_sub_state(c, x, neg_from, ghn.p, N, t.p, run);
+        ldl_solve(t.p, N, y, false, run, nullptr);
+        launch_spmv_colmask(c, dKp, n, y, ghn.p, run);
+    } else {
+        // y = op.LDL * x   (opLDL2.m:165-167); the residual-update branch subtracts the zero
+        // state of a value object and its SpMVs are dead: skipped
+        ldl_solve(x, neg_from, y, false, run, nullptr);
+    }
     if (nitref <= 0) return;
     const int64_t steps = (int64_t)nitref;
     if (force_itref != 0) {
@@ -184,6 +203,8 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
 }
 
 double Precond::apply_bytes() const {
+    const double ghn_bytes = (residual_update != 0 && handle)
+                                 ? 32.0 * N + 12.0 * (double)dKp.nnz + 4.0 * (N + 1) + 16.0 * N : 0.0;
     // SpTRSV sweep over the strict factor (l entries): 12*l + 4*(N+1) + 16*N (vector in/out)
     // + 4*N (perm) ; backward adds D (8*N) and the scatter (8*N, +8*N when accumulating).
     const double l = (double)dF.nnz, Nn = (double)N;
@@ -193,7 +214,7 @@ double Precond::apply_bytes() const {
     double b = fwd + bwd;
     const int64_t steps = nitref > 0 ? (int64_t)nitref : 0;
     b += steps * (kp + fwd + bwd + 8 * Nn);
-    return b;
+    return b + ghn_bytes;
 }
 
 }  // namespace cpk

@@ -1606,9 +1606,10 @@ static std::string solver_key(const Ctx &c, const Precond &M, const DMat &AC, in
     char buf[512];
     const double restart = o && o->has_restart ? o->restart : 50, mem = o && o->has_mem ? o->mem : 50;
     const double itmax = o && o->has_itmax ? o->itmax : -1;
-    snprintf(buf, sizeof buf, "%d|%llu|%p|%p|%p|%p|%p|%.17g|%.17g|%.17g|%.17g|%.17g|%.17g|%s|%s", method,
+    snprintf(buf, sizeof buf, "%d|%llu|%p|%p|%p|%p|%p|%.17g|%.17g|%.17g|%d|%.17g|%.17g|%.17g|%s|%s", method,
              (unsigned long long)AC.gen, (const void *)d_b, (const void *)d_xy, (const void *)c.partials.p,
-             (const void *)c.counter.p, (const void *)c.red.p, M.nitref, M.force_itref, M.itref_tol, restart, mem,
+             (const void *)c.counter.p, (const void *)c.red.p, M.nitref, M.force_itref, M.itref_tol,
+             (M.residual_update != 0 && M.handle) ? 1 : 0, restart, mem,
              method == CPK_DQGMRES ? itmax : 0.0, getenv("CPK_BATCH") ? getenv("CPK_BATCH") : "",
              getenv("CPK_NO_GRAPH") ? getenv("CPK_NO_GRAPH") : "");
     return buf;

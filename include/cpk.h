@@ -140,6 +140,14 @@ int cpk_pc_destroy(cpk_pc M);
 /* M.nitref = ...; M.itref_tol = ...; etc. (opLDL2.m:45-50, 97-115), has_* fields select. */
 int cpk_pc_set(cpk_pc M, const cpk_opts *opts);
 int cpk_pc_get(cpk_pc M, double *nitref, double *itref_tol, double *force_itref, double *residual_update);
+/* Opt-in (not in the reference): handle semantics of the residual-update state.  In the
+ * reference, opLDL2 is a Spot value object, so the op.Aty / op.Cy written inside multiply
+ * (opLDL2.m:169-171) are lost and residual_update is a functional no-op; cpk_pc_apply matches
+ * that by default.  on != 0 keeps [op.Aty; op.Cy] on the device between applies, as the
+ * residual update of reg_cpkrylov.m:47-52 (Gould-Hribar-Nocedal) intends; it takes effect while
+ * residual_update is set.  Enabling or disabling clears the state.  Single-GPU contexts only
+ * (CPK_ERR_UNSUPPORTED on a distributed preconditioner). */
+int cpk_pc_set_handle(cpk_pc M, int on);
 /* y = M*x (opLDL2.multiply, opLDL2.m:161-188).  Host vectors of length N. */
 int cpk_pc_apply(cpk_pc M, const double *x, double *y);
 /* Same on device pointers, enqueued on the context stream. */

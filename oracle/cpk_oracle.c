@@ -151,6 +151,11 @@ struct orc_ldl2 {
     /* public properties (opLDL2.m:45-50) */
     double nitref, itref_tol, force_itref, residual_update;
     double *w1, *w2, *w3; /* scratch */
+    /* handle semantics (opt-in, not the reference's effective behaviour): op.Aty = ghn[0, nA),
+     * op.Cy = ghn[nA, N) persist between applies, as reg_cpkrylov.m:47-52 and the GHN paper
+     * intend; off (the default) restates MATLAB's value-object semantics, where they stay zero */
+    int handle;
+    double *ghn;
 };
 
 static int assemble_kp(const orc_csr *A, const orc_csr *B, const orc_csr *C, csr *Kp) {
@@ -333,6 +338,8 @@ static int ldl2_common(const orc_csr *A, const orc_csr *B, const orc_csr *C, str
     op->w1 = malloc((size_t)op->N * sizeof(double));
     op->w2 = malloc((size_t)op->N * sizeof(double));
     op->w3 = malloc((size_t)op->N * sizeof(double));
+    op->handle = 0;
+    op->ghn = calloc((size_t)op->N, sizeof(double));
     *out = op;
     return 0;
 }
@@ -395,6 +402,7 @@ void orc_ldl2_destroy(orc_ldl2 *op) {
     free(op->w1);
     free(op->w2);
     free(op->w3);
+    free(op->ghn);
     free(op);
 }
 
@@ -408,6 +416,11 @@ void orc_ldl2_set_itref_tol(orc_ldl2 *op, double v) { op->itref_tol = v; }
 void orc_ldl2_set_force_itref(orc_ldl2 *op, double v) { op->force_itref = (v != 0 && v != 1) ? 0 : v; }
 /* set.residual_update: stored as given (opLDL2.m:113-115) */
 void orc_ldl2_set_residual_update(orc_ldl2 *op, double v) { op->residual_update = v; }
+/* opt-in handle semantics of the residual-update state; enabling or disabling clears it */
+void orc_ldl2_set_handle(orc_ldl2 *op, double v) {
+    op->handle = v != 0;
+    memset(op->ghn, 0, (size_t)op->N * sizeof(double));
+}
 void orc_ldl2_get_props(const orc_ldl2 *op, double *a, double *b, double *c, double *d) {
     *a = op->nitref, *b = op->itref_tol, *c = op->force_itref, *d = op->residual_update;
 }
@@ -438,17 +451,19 @@ static void ldl_apply(const struct orc_ldl2 *op, const double *x, double *y) {
 
 /* opLDL2.multiply (opLDL2.m:161-188).  Spot operators are value objects, so the writes to
  * op.Aty / op.Cy / op.rNorm inside multiply are lost on return: Aty and Cy stay zero and
- * the residual-update SpMVs are dead work, which is restated here as MATLAB executes it. */
+ * the residual-update SpMVs are dead work, which is restated here as MATLAB executes it.
+ * With handle semantics (orc_ldl2_set_handle) the state persists between applies. */
 int orc_ldl2_apply(orc_ldl2 *op, const double *x, double *y) {
     int64_t n = op->nA, N = op->N;
     double *r = op->w1, *t = op->w2;
     if (op->residual_update != 0) {
-        for (int64_t i = 0; i < N; i++) t[i] = x[i] - 0.0; /* x - [op.Aty; op.Cy], both zero */
+        for (int64_t i = 0; i < N; i++) t[i] = x[i] - op->ghn[i]; /* [x(1:n) - op.Aty; x(n+1:N) - op.Cy] */
         ldl_apply(op, t, y);
-        /* op.Aty = op.A(1:n, n+1:n+m) * y2; op.Cy = op.A(n+1:N, n+1:N) * y2 (discarded) */
+        /* op.Aty = op.A(1:n, n+1:n+m) * y2; op.Cy = op.A(n+1:N, n+1:N) * y2 (opLDL2.m:169-171) */
         orc_csr k12 = view(&op->K12), k22 = view(&op->K22);
         spmv(&k12, y + n, r);
         spmv(&k22, y + n, r + n);
+        if (op->handle) memcpy(op->ghn, r, (size_t)N * sizeof(double));
     } else {
         ldl_apply(op, x, y);
     }

@@ -78,6 +78,7 @@ void orc_ldl2_set_nitref(orc_ldl2 *op, double v);
 void orc_ldl2_set_itref_tol(orc_ldl2 *op, double v);
 void orc_ldl2_set_force_itref(orc_ldl2 *op, double v);
 void orc_ldl2_set_residual_update(orc_ldl2 *op, double v);
+void orc_ldl2_set_handle(orc_ldl2 *op, double v); /* opt-in handle semantics of op.Aty / op.Cy */
 void orc_ldl2_get_props(const orc_ldl2 *op, double *nitref, double *itref_tol, double *force_itref,
                         double *residual_update);
 /* y = M*x  (opLDL2.multiply, ops/opLDL2.m:161-188) */

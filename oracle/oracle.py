@@ -59,7 +59,7 @@ def lib():
         L.orc_ldl2_create_from_factors.argtypes = [P(_Csr), P(_Csr), P(_Csr), P(C.c_int64), P(C.c_int32),
                                                    P(C.c_double), P(C.c_double), P(C.c_int32), P(C.c_void_p)]
         L.orc_ldl2_destroy.argtypes = [C.c_void_p]
-        for nm in ("nitref", "itref_tol", "force_itref", "residual_update"):
+        for nm in ("nitref", "itref_tol", "force_itref", "residual_update", "handle"):
             f = getattr(L, "orc_ldl2_set_" + nm)
             f.argtypes = [C.c_void_p, C.c_double]
         L.orc_ldl2_get_props.argtypes = [C.c_void_p] + [P(C.c_double)] * 4
@@ -153,6 +153,10 @@ class LDL2:
     def set(self, **kw):
         for k, v in kw.items():
             getattr(lib(), "orc_ldl2_set_" + k)(self.h, float(v))
+
+    def set_handle(self, on):
+        """Opt-in handle semantics of op.Aty / op.Cy (orc_ldl2_set_handle); clears the state."""
+        lib().orc_ldl2_set_handle(self.h, C.c_double(1.0 if on else 0.0))
 
     def props(self):
         v = [C.c_double() for _ in range(4)]

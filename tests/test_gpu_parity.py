@@ -98,6 +98,53 @@ def test_precond_apply_bitexact(gpu_ctx, name, props):
 
 
 @pytest.mark.parametrize("name", ["cvxqp1_m", "cvxqp2_s"])
+@pytest.mark.parametrize("props", [dict(nitref=0), dict(nitref=1, force_itref=True)])
+def test_precond_apply_handle_semantics_bitexact(gpu_ctx, name, props):
+    """Opt-in handle semantics of the residual-update state (cpk_pc_set_handle): a sequence of
+    applies carries [op.Aty; op.Cy] from one to the next, bit-identical to the oracle's."""
+    import cpkrylov_amd as cpk
+    P = F.load(name)
+    M = cpk.opLDL2(P["G"], P["B"], -P["C"])
+    for k, v in dict(props, residual_update=True).items():
+        setattr(M, k, v)
+    M.handle_semantics = True
+    L, D, perm = M.export_factors()
+    Mo = O.LDL2(P["G"], P["B"], -P["C"], factors=(L, D, perm))
+    Mo.set(**{k: float(v) for k, v in dict(props, residual_update=1).items()})
+    Mo.set_handle(True)
+    rng = np.random.default_rng(9)
+    ys = []
+    for _ in range(4):
+        z = rng.standard_normal(P["n"] + P["m"])
+        y, yo = M * z, Mo @ z
+        assert np.array_equal(y, yo), np.max(np.abs(y - yo))
+        ys.append(y)
+    M.handle_semantics = False  # back to the reference's value semantics
+    z = rng.standard_normal(P["n"] + P["m"])
+    Mo.set_handle(False)
+    assert np.array_equal(M * z, Mo @ z)
+
+
+def test_minres_handle_semantics_matches_oracle(gpu_ctx):
+    """cpminres with the stateful residual update on the device vs the oracle with the same."""
+    import cpkrylov_amd as cpk
+    P = F.load("cvxqp1_m")
+    opts = dict(F.EXPROG_OPTS)
+    M = cpk.opLDL2(P["G"], P["B"], -P["C"])
+    M.handle_semantics = True
+    L, D, perm = M.export_factors()
+    Mo = O.LDL2(P["G"], P["B"], -P["C"], factors=(L, D, perm))
+    Mo.set_handle(True)
+    b = P["rhs"][:P["n"]]
+    x, y, st = cpk.cpminres(b, P["Q"], P["C"], M, opts)[:3]
+    xo, yo, so = O.method("minres", b, P["Q"], P["C"], Mo, opts)
+    assert st["niters"] == so["niters"]
+    h, ho = st["residHistory"], so["residHistory"]
+    assert len(h) == len(ho) and np.max(np.abs(h - ho)) <= 1e-8 * ho[0]
+    assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
+
+
+@pytest.mark.parametrize("name", ["cvxqp1_m", "cvxqp2_s"])
 def test_spmv_bitexact(gpu_ctx, name):
     import cpkrylov_amd as cpk
     P = F.load(name)

@@ -120,6 +120,31 @@ def test_residual_update_is_noop():
     assert np.array_equal(M @ z, y0)  # and stays so on the next call
 
 
+def test_handle_semantics_state():
+    """Opt-in handle semantics (not the reference's effective behaviour): op.Aty / op.Cy
+    persist, so the next apply solves with [x1 - Aty; x2 - Cy] (opLDL2.m:164-172).  The first
+    apply equals the value-object one; the state is Kp(:, n+1:N) * y(n+1:N); re-enabling clears it."""
+    P = F.load("cvxqp1_m")
+    n, m = P["n"], P["m"]
+    Mh = O.LDL2(P["G"], P["B"], -P["C"], order="rcm")
+    Mv = O.LDL2(P["G"], P["B"], -P["C"], order="rcm")
+    for M in (Mh, Mv):
+        M.set(nitref=0, residual_update=1)
+    Mh.set_handle(True)
+    rng = np.random.default_rng(4)
+    x1, x2 = rng.standard_normal(n + m), rng.standard_normal(n + m)
+    y1 = Mh @ x1
+    assert np.array_equal(y1, Mv @ x1)
+    Kp = sp.bmat([[P["G"], P["B"].T], [P["B"], -P["C"]]]).tocsr()
+    state = Kp[:, n:] @ y1[n:]
+    y2 = Mh @ x2
+    y2_ref = Mv @ (x2 - state)
+    assert np.linalg.norm(y2 - y2_ref) <= 1e-12 * np.linalg.norm(y2_ref)
+    assert not np.array_equal(y2, Mv @ x2)  # the state matters
+    Mh.set_handle(True)  # clears the state
+    assert np.array_equal(Mh @ x1, y1)
+
+
 def test_indefinite_error():
     """beta < -100*eps raises (cpminres.m:136-139): use a G that is not positive on the
     nullspace of B."""
