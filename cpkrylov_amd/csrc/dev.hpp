@@ -202,16 +202,19 @@ struct DSep {
     int64_t nT = 0, kt = 0, nlev = 0, nsend = 0, ntdof = 0;
     DBuf<int32_t> tf_ptr, tf_col, tf_src, tb_ptr, tb_col, lev_ptr, lev_rows, send, tdof;
     DBuf<double> tf_val, tb_val, DT, sbuf, rbuf;
-    // staged solve (tsolve_staged_kernel): forward rows split into their leading payload terms
-    // (tk_*) and the rest (tr_*); the rest, the backward rows, D_T and the level lists live in LDS
-    DBuf<int32_t> tk_ptr, tk_col, tr_ptr, tr_col, tr_lcol;
-    DBuf<double> tk_val, tr_val, tr_rv, pre;  // tr_rv, pre: written by tprefix_kernel per solve
-    int64_t nrest = 0, nbwd = 0;
-    size_t lds = 0;  // bytes of the staged image, 0 = too large (one-pass global kernel)
+    // staged solve (tprefix_kernel + tsolve_staged_kernel): forward rows split into their
+    // leading payload terms (tk_*) and the rest (tr_*); img is the LDS image of the level solve
+    // in HBM (static parts from setup; the row prefixes at off_pre and the pre-multiplied rest
+    // terms at off_rv, in doubles, are written by tprefix_kernel per solve)
+    DBuf<int32_t> tk_ptr, tk_col, tr_ptr, tr_col;
+    DBuf<double> tk_val, tr_val;
+    DBuf<char> img;
+    int64_t nrest = 0, nbwd = 0, off_pre = 0, off_rv = 0;
+    size_t lds = 0;  // bytes of the image (16-byte multiple), 0 = too large (one-pass global kernel)
 };
-// Split the forward rows of T and size the LDS image of the staged separator solve.
-void dsep_stage(DSep &T, const std::vector<int64_t> &tf_ptr, const std::vector<int32_t> &tf_col,
-                const std::vector<double> &tf_val, int64_t nbwd);
+struct RankPlan;
+// Split the forward rows of T and build the LDS image of the staged separator solve.
+void dsep_stage(DSep &T, const RankPlan &rp);
 struct DofMap;
 
 struct Precond {

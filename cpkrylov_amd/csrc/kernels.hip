@@ -388,7 +388,7 @@ __global__ __launch_bounds__(256) void tprefix_kernel(
     int nT, const int32_t *__restrict__ tk_ptr, const int32_t *__restrict__ tk_col, const double *__restrict__ tk_val,
     const int32_t *__restrict__ tr_ptr, const int32_t *__restrict__ tr_col, const double *__restrict__ tr_val,
     const int32_t *__restrict__ tf_src, const double *__restrict__ rbuf, double *__restrict__ pre,
-    double *__restrict__ rv_out, const int *run, const int *active) {
+    double *__restrict__ rv_out, const int *run, const int *active) {  // pre, rv_out: regions of the LDS image
     __shared__ double prod[4][kWave];
     if (skip(run, active)) return;
     const int wv = threadIdx.x / kWave, lane = threadIdx.x % kWave;
@@ -417,11 +417,8 @@ __global__ __launch_bounds__(256) void tprefix_kernel(
 }
 
 __global__ __launch_bounds__(kTsolveThreads) void tsolve_staged_kernel(
-    int nlev, int nT, int nrest, int nbwd, const int32_t *__restrict__ lev_ptr, const int32_t *__restrict__ lev_rows,
-    const int32_t *__restrict__ tr_ptr, const int32_t *__restrict__ tr_lcol, const double *__restrict__ tr_rv,
-    const double *__restrict__ pre, const int32_t *__restrict__ tb_ptr, const int32_t *__restrict__ tb_col,
-    const double *__restrict__ tb_val, const double *__restrict__ DT, const int32_t *__restrict__ tdof, int ntdof,
-    double *wT, double *y, int add, const int *run, const int *active) {
+    int nlev, int nT, int nrest, int nbwd, const uint4 *__restrict__ img, int img_vec, const int32_t *__restrict__ tdof,
+    int ntdof, double *wT, double *y, int add, const int *run, const int *active) {
     extern __shared__ __attribute__((aligned(16))) char tsm[];
     if (skip(run, active)) return;
     double *wt = reinterpret_cast<double *>(tsm);  // nT + 1: wt[nT] = 1.0 (pre-multiplied terms)
@@ -429,14 +426,23 @@ __global__ __launch_bounds__(kTsolveThreads) void tsolve_staged_kernel(
     int32_t *rc = reinterpret_cast<int32_t *>(bv + nbwd);
     int32_t *bc = rc + nrest, *rp = bc + nbwd, *bp = rp + nT + 1, *lr = bp + nT + 1, *lp = lr + nT;
     const int tid = threadIdx.x;
-    if (tid == 0) wt[nT] = 1.0;
-    for (int i = tid; i < nrest; i += kTsolveThreads) rc[i] = tr_lcol[i], rv[i] = tr_rv[i];
-    for (int i = tid; i < nbwd; i += kTsolveThreads) bc[i] = tb_col[i], bv[i] = tb_val[i];
-    for (int i = tid; i <= nT; i += kTsolveThreads) {
-        rp[i] = tr_ptr[i], bp[i] = tb_ptr[i];
-        if (i < nT) dt[i] = DT[i], lr[i] = lev_rows[i], wt[i] = pre[i];
+    // the LDS image is one contiguous HBM image (static parts from setup, the row prefixes and
+    // pre-multiplied rest terms from tprefix_kernel): 16-byte copies, every load in flight at once
+    constexpr int U = 8;
+    uint4 *dst = reinterpret_cast<uint4 *>(tsm);
+    for (int i0 = tid; i0 < img_vec; i0 += U * kTsolveThreads) {
+        uint4 q[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = i0 + u * kTsolveThreads;
+            q[u] = i < img_vec ? img[i] : uint4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = i0 + u * kTsolveThreads;
+            if (i < img_vec) dst[i] = q[u];
+        }
     }
-    for (int i = tid; i <= nlev; i += kTsolveThreads) lp[i] = lev_ptr[i];
     __syncthreads();
     for (int l = 0; l < nlev; l++) {  // forward: the rest of each row
         for (int q = lp[l] + tid; q < lp[l + 1]; q += kTsolveThreads) {
@@ -461,27 +467,43 @@ __global__ __launch_bounds__(kTsolveThreads) void tsolve_staged_kernel(
     }
 }
 
-void dsep_stage(DSep &T, const std::vector<int64_t> &tf_ptr, const std::vector<int32_t> &tf_col,
-                const std::vector<double> &tf_val, int64_t nbwd) {
+void dsep_stage(DSep &T, const RankPlan &rp) {
     const int64_t nT = T.nT;
-    std::vector<int32_t> kp(nT + 1, 0), kc, rp(nT + 1, 0), rc, rl;
+    std::vector<int32_t> kp(nT + 1, 0), kc, rptr(nT + 1, 0), rc, rl;
     std::vector<double> kv, rv;
     for (int64_t t = 0; t < nT; t++) {
-        int64_t e = tf_ptr[t];
-        for (; e < tf_ptr[t + 1] && tf_col[e] >= 0; e++) kc.push_back(tf_col[e]), kv.push_back(tf_val[e]);
-        for (; e < tf_ptr[t + 1]; e++) {
-            rc.push_back(tf_col[e]), rv.push_back(tf_val[e]);
-            rl.push_back(tf_col[e] >= 0 ? (int32_t)nT : -tf_col[e] - 1);  // LDS column: T row, or the 1.0 slot
+        int64_t e = rp.tf_ptr[t];
+        for (; e < rp.tf_ptr[t + 1] && rp.tf_col[e] >= 0; e++) kc.push_back(rp.tf_col[e]), kv.push_back(rp.tf_val[e]);
+        for (; e < rp.tf_ptr[t + 1]; e++) {
+            rc.push_back(rp.tf_col[e]), rv.push_back(rp.tf_val[e]);
+            rl.push_back(rp.tf_col[e] >= 0 ? (int32_t)nT : -rp.tf_col[e] - 1);  // LDS column: T row, or the 1.0 slot
         }
-        kp[t + 1] = (int32_t)kc.size(), rp[t + 1] = (int32_t)rc.size();
+        kp[t + 1] = (int32_t)kc.size(), rptr[t + 1] = (int32_t)rc.size();
     }
     T.tk_ptr.upload(kp), T.tk_col.upload(kc), T.tk_val.upload(kv);
-    T.tr_ptr.upload(rp), T.tr_col.upload(rc), T.tr_val.upload(rv), T.tr_lcol.upload(rl);
-    T.tr_rv.alloc(std::max<size_t>(rv.size(), 1));
-    T.pre.alloc(std::max<int64_t>(nT, 1));
-    T.nrest = (int64_t)rc.size(), T.nbwd = nbwd;
-    const size_t bytes = 8 * (size_t)(2 * nT + 1 + T.nrest + nbwd) + 4 * (size_t)(T.nrest + nbwd + 3 * (nT + 1) + T.nlev + 1);
-    T.lds = bytes <= kTsolveMaxLds ? bytes : 0;
+    T.tr_ptr.upload(rptr), T.tr_col.upload(rc), T.tr_val.upload(rv);
+    T.nrest = (int64_t)rc.size(), T.nbwd = (int64_t)rp.tb_col.size();
+    // the LDS image of tsolve_staged_kernel:
+    //   double wt[nT + 1] | dt[nT] | rv[nrest] | bv[nbwd] | int32 rc[nrest] | bc[nbwd] | rp[nT + 1] | bp[nT + 1]
+    //   | lr[nT] | lp[nlev + 1]
+    const int64_t nb = T.nbwd, nl = T.nlev;
+    const size_t bytes = 8 * (size_t)(2 * nT + 1 + T.nrest + nb) + 4 * (size_t)(T.nrest + nb + 3 * (nT + 1) + nl + 1);
+    const size_t padded = (bytes + 15) & ~(size_t)15;
+    std::vector<char> img(padded, 0);
+    double *wt = reinterpret_cast<double *>(img.data());
+    double *dt = wt + nT + 1, *rvv = dt + nT, *bv = rvv + T.nrest;
+    int32_t *rcc = reinterpret_cast<int32_t *>(bv + nb);
+    int32_t *bc = rcc + T.nrest, *rpp = bc + nb, *bp = rpp + nT + 1, *lr = bp + nT + 1, *lp = lr + nT;
+    wt[nT] = 1.0;
+    for (int64_t t = 0; t < nT; t++) dt[t] = rp.DT[t], lr[t] = rp.tlev_rows[t];
+    for (int64_t i = 0; i < nb; i++) bv[i] = rp.tb_val[i], bc[i] = rp.tb_col[i];
+    for (int64_t i = 0; i < T.nrest; i++) rcc[i] = rl[i];
+    for (int64_t t = 0; t <= nT; t++) rpp[t] = rptr[t], bp[t] = (int32_t)rp.tb_ptr[t];
+    for (int64_t l = 0; l <= nl; l++) lp[l] = rp.tlev_ptr[l];
+    T.img.upload(img);
+    T.off_pre = 0;
+    T.off_rv = (int64_t)((char *)rvv - img.data()) / 8;
+    T.lds = padded <= kTsolveMaxLds ? padded : 0;
 }
 
 // payload: w of this rank's rows that separator rows read, then (rank 0) the T inputs +-x[tdof]
@@ -514,13 +536,13 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
                                    (int)kTsolveMaxLds) == hipSuccess;
     }();
     if (S.lds && (S.lds <= 64 * 1024 || lds_attr) && !getenv("CPK_TSOLVE_ONEPASS")) {
+        double *img = reinterpret_cast<double *>(S.img.p);
         hipLaunchKernelGGL(tprefix_kernel, dim3((unsigned)((S.nT + 3) / 4)), dim3(256), 0, c.stream, (int)S.nT,
                            S.tk_ptr.p, S.tk_col.p, S.tk_val.p, S.tr_ptr.p, S.tr_col.p, S.tr_val.p, S.tf_src.p,
-                           S.rbuf.p, S.pre.p, S.tr_rv.p, run, active);
+                           S.rbuf.p, img + S.off_pre, img + S.off_rv, run, active);
         hipLaunchKernelGGL(tsolve_staged_kernel, dim3(1), dim3(kTsolveThreads), S.lds, c.stream, (int)S.nlev,
-                           (int)S.nT, (int)S.nrest, (int)S.nbwd, S.lev_ptr.p, S.lev_rows.p, S.tr_ptr.p, S.tr_lcol.p,
-                           S.tr_rv.p, S.pre.p, S.tb_ptr.p, S.tb_col.p, S.tb_val.p, S.DT.p, S.tdof.p, (int)S.ntdof,
-                           wT, y, add ? 1 : 0, run, active);
+                           (int)S.nT, (int)S.nrest, (int)S.nbwd, (const uint4 *)S.img.p, (int)(S.lds / 16), S.tdof.p,
+                           (int)S.ntdof, wT, y, add ? 1 : 0, run, active);
         CPK_HIP(hipGetLastError());
         return;
     }

@@ -126,7 +126,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an) {
     T.tf_src.upload(rp.tf_src), T.tb_ptr.upload(i32(rp.tb_ptr)), T.tb_col.upload(rp.tb_col);
     T.tb_val.upload(rp.tb_val), T.DT.upload(rp.DT), T.lev_ptr.upload(rp.tlev_ptr), T.lev_rows.upload(rp.tlev_rows);
     T.tdof.upload(rp.tdof);
-    dsep_stage(T, rp.tf_ptr, rp.tf_col, rp.tf_val, (int64_t)rp.tb_col.size());
+    dsep_stage(T, rp);
     T.sbuf.alloc((size_t)std::max<int64_t>(T.kt, 1));
     T.rbuf.alloc((size_t)std::max<int64_t>(T.kt * c.nranks, 1));
     // refinement residual rows of Kp with their halo
