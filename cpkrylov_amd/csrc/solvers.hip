@@ -778,33 +778,41 @@ __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double
     }
     __syncthreads();
     if (!s_last) return;
-    if (rb.defer) {  // distributed mode: local window sums out; arnoldi_fin_kernel after the allreduce
-        for (int64_t j = 0; j < 2 * win.nv; j++) {
-            double a[1] = {0.0};
-            for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x)
-                a[0] += ld_agent(rb.partials + (size_t)b * 2 * maxv + j);
-            block_sum<1>(a);
-            if (threadIdx.x == 0) rb.defer[j] = a[0];
-        }
-        return;
-    }
-    __shared__ double hv[2];
-    if (ring && threadIdx.x == 0) {  // fresh ring row for H(kk, .)
+    // the last workgroup sums the 2 * nv window sums over the grid's partials, kDotGroup sums at
+    // a time (an even count: a window pair stays in one group) with every partial load of a thread in flight (per sum: thread-strided over the
+    // workgroups, then the block tree -- the same order for every sum)
+    __shared__ double hv[kDotGroup];
+    if (!rb.defer && ring && threadIdx.x == 0)  // fresh ring row for H(kk, .)
         for (int64_t c = 1; c <= st->mem + 2; c++) Hd(st, kk, c) = 0.0;
-    }
-    for (int64_t j = 0; j < 2 * win.nv; j++) {
-        double a[1] = {0.0};
-        for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x)
-            a[0] += ld_agent(rb.partials + (size_t)b * 2 * maxv + j);
-        block_sum<1>(a);
-        if (threadIdx.x == 0) hv[j & 1] = a[0];
-        __syncthreads();
-        if (threadIdx.x == 0 && (j & 1)) {
-            const int64_t jj = win.jlo + j / 2;
-            const double h = hv[0] + hv[1];
-            if (ring) Hd(st, jj, 2 + kk - jj) = h;
-            else Hg(st, jj, kk) = h;
+    for (int64_t j0 = 0; j0 < 2 * win.nv; j0 += kDotGroup) {
+        double a[kDotGroup];
+#pragma unroll
+        for (int q = 0; q < kDotGroup; q++) a[q] = 0.0;
+        for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+            double t[kDotGroup];
+#pragma unroll
+            for (int q = 0; q < kDotGroup; q++)
+                t[q] = j0 + q < 2 * win.nv ? ld_agent(rb.partials + (size_t)b * 2 * maxv + j0 + q) : 0.0;
+#pragma unroll
+            for (int q = 0; q < kDotGroup; q++) a[q] += t[q];
         }
+        block_sum<kDotGroup>(a);
+        if (threadIdx.x == 0)
+#pragma unroll
+            for (int q = 0; q < kDotGroup; q++) hv[q] = a[q];
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int64_t q = 0; q < kDotGroup && j0 + q < 2 * win.nv; q++) {
+                const int64_t j = j0 + q;
+                if (rb.defer) {  // distributed mode: local window sums out; arnoldi_fin_kernel after the allreduce
+                    rb.defer[j] = hv[q];
+                } else if (j & 1) {
+                    const int64_t jj = win.jlo + j / 2;
+                    const double h = hv[q - 1] + hv[q];
+                    if (ring) Hd(st, jj, 2 + kk - jj) = h;
+                    else Hg(st, jj, kk) = h;
+                }
+            }
         __syncthreads();
     }
 }
