@@ -919,7 +919,7 @@ static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add,
 // one instruction stream for SPLIT blocks instead of one per block; lanes of different logical
 // blocks never synchronise (within a single wave __syncthreads is a no-op fence).
 template <int TPB, int RPT, int EPT, bool BWD, bool ADD, int SPLIT = 1>
-__global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(4))) void sptrsv_pipe_kernel(
+__global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPLIT == 1 ? 4 : 1))) void sptrsv_pipe_kernel(
     int64_t blk0, int64_t nblk, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,
