@@ -179,7 +179,8 @@ struct DSep;
 // t = x_eff - g with x_eff[i] = (i >= neg_from ? -x[i] : x[i])  (the GHN residual update)
 void launch_sub_state(Ctx &c, const double *x, int64_t neg_from, const double *g, int64_t N, double *t,
                       const int *run);
-void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x, int64_t neg_from);
+void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x, int64_t neg_from,
+                         const double *piggy_src = nullptr);
 // redundant separator solve into wT (= w + nsub); rank 0 writes (add: accumulates) y at the T dofs
 void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active);
 
@@ -198,8 +199,10 @@ struct Analysis {
 Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22);
 
 // The separator solve of a distributed preconditioner, device copy.
+constexpr int64_t kSepPiggy = 2;  // spare payload slots per rank in the separator exchange
 struct DSep {
     int64_t nT = 0, kt = 0, nlev = 0, nsend = 0, ntdof = 0;
+    int64_t kt_data = 0;  // payload values of the plan; [kt_data, kt) are the piggyback slots
     DBuf<int32_t> tf_ptr, tf_col, tf_src, tb_ptr, tb_col, lev_ptr, lev_rows, send, tdof;
     DBuf<double> tf_val, tb_val, DT, sbuf, rbuf;
     // staged solve (tprefix_kernel + tsolve_staged_kernel): forward rows split into their
@@ -244,9 +247,14 @@ struct Precond {
     // cached solvers (workspace + captured iteration graphs), keyed; see solvers.hip
     std::vector<std::pair<std::string, std::shared_ptr<void>>> solvers;
     // y = M*x  (opLDL2.multiply); all pointers on the device, enqueued on ctx->stream
-    void apply(const double *x, int64_t neg_from, double *y, const int *run);
+    // piggy_src (distributed only, piggyback_ok()): kSepPiggy device values appended to the first
+    // separator exchange's payload, e.g. a solver's deferred inner-product partials; after the
+    // apply every rank finds rank r's values at sep.rbuf[r * sep.kt + sep.kt_data + j]
+    void apply(const double *x, int64_t neg_from, double *y, const int *run, const double *piggy_src = nullptr);
+    bool piggyback_ok() const { return dist && sep.kt > 0; }
     void set_handle(bool on);  // enabling or disabling clears the state
-    void ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run, const int *act);
+    void ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run, const int *act,
+                   const double *piggy_src = nullptr);
     // algorithmic HBM bytes of one apply
     double apply_bytes() const;
 };

@@ -507,9 +507,10 @@ void dsep_stage(DSep &T, const RankPlan &rp) {
 }
 
 // payload: w of this rank's rows that separator rows read, then (rank 0) the T inputs +-x[tdof]
+// (and, with piggy, kSepPiggy values of a solver's into the spare slots [kt_data, kt))
 __global__ void tpack_kernel(const double *__restrict__ w, const int32_t *__restrict__ send, int nsend,
                              const double *__restrict__ x, int64_t neg_from, const int32_t *__restrict__ tdof,
-                             int ntdof, double *__restrict__ out) {
+                             int ntdof, double *__restrict__ out, const double *__restrict__ piggy, int kt_data) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nsend) out[i] = w[send[i]];
     else if (i < nsend + ntdof) {
@@ -517,14 +518,16 @@ __global__ void tpack_kernel(const double *__restrict__ w, const int32_t *__rest
         const double v = x[d];
         out[i] = d >= neg_from ? -v : v;
     }
+    if (piggy && blockIdx.x == 0 && threadIdx.x < kSepPiggy) out[kt_data + threadIdx.x] = piggy[threadIdx.x];
 }
 
-void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x, int64_t neg_from) {
+void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x, int64_t neg_from,
+                         const double *piggy_src) {
     if (S.kt == 0) return;
-    const int64_t n = S.nsend + S.ntdof;
+    const int64_t n = std::max<int64_t>(S.nsend + S.ntdof, piggy_src ? 1 : 0);
     if (n > 0)
         hipLaunchKernelGGL(tpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c.stream, w, S.send.p,
-                           (int)S.nsend, x, neg_from, S.tdof.p, (int)S.ntdof, S.sbuf.p);
+                           (int)S.nsend, x, neg_from, S.tdof.p, (int)S.ntdof, S.sbuf.p, piggy_src, (int)S.kt_data);
     CPK_HIP(hipGetLastError());
     c.comm->allgather(S.sbuf.p, S.rbuf.p, (size_t)S.kt, c.stream);
 }

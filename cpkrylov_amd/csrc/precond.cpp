@@ -120,7 +120,19 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an) {
     }
     // separator solve
     DSep &T = pc->sep;
+    // payload per rank: the plan's kt values, then kSepPiggy slots that can carry a solver's
+    // deferred inner-product partials through the same allgather (Precond::apply, piggy_src):
+    // positions r * kt + j of the plan become r * (kt + kSepPiggy) + j
+    if (rp.kt > 0) {
+        const int64_t kt0 = rp.kt, kt1 = kt0 + kSepPiggy;
+        auto remap = [&](int32_t q) { return (int32_t)((q / kt0) * kt1 + q % kt0); };
+        for (auto &q : rp.tf_col)
+            if (q >= 0) q = remap(q);
+        for (auto &q : rp.tf_src) q = remap(q);
+        rp.kt = kt1;
+    }
     T.nT = rp.nT, T.kt = rp.kt, T.nlev = (int64_t)rp.tlev_ptr.size() - 1, T.ntdof = (int64_t)rp.tdof.size();
+    T.kt_data = rp.kt > 0 ? rp.kt - kSepPiggy : 0;
     auto i32 = [](const std::vector<int64_t> &v) { return std::vector<int32_t>(v.begin(), v.end()); };
     T.tf_ptr.upload(i32(rp.tf_ptr)), T.tf_col.upload(rp.tf_col), T.tf_val.upload(rp.tf_val);
     T.tf_src.upload(rp.tf_src), T.tb_ptr.upload(i32(rp.tb_ptr)), T.tb_col.upload(rp.tb_col);
@@ -128,6 +140,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an) {
     T.tdof.upload(rp.tdof);
     dsep_stage(T, rp);
     T.sbuf.alloc((size_t)std::max<int64_t>(T.kt, 1));
+    T.sbuf.zero(c.stream);
     T.rbuf.alloc((size_t)std::max<int64_t>(T.kt * c.nranks, 1));
     // refinement residual rows of Kp with their halo
     make_dist_dmat(dist_csr(an.Kp, *dm, c.rank, false), c.nranks, pc->dKp);
@@ -151,11 +164,11 @@ Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22)
 
 // y (=|+=) LDL * xin: forward sweep, [distributed: separator exchange + solve], backward sweep
 void Precond::ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run,
-                        const int *act) {
+                        const int *act, const double *piggy_src) {
     Ctx &c = *ctx;
     launch_sptrsv_fwd(c, dF, xin, neg_from, w.p, run, act);
     if (dist) {
-        launch_sep_exchange(c, sep, w.p, xin, neg_from);
+        launch_sep_exchange(c, sep, w.p, xin, neg_from, piggy_src);
         launch_sep_solve(c, sep, w.p + nsub, y, add, run, act);
     }
     launch_sptrsv_bwd(c, dF, w.p, y, add, run, act);
@@ -171,18 +184,18 @@ void Precond::set_handle(bool on) {
     }
 }
 
-void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run) {
+void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run, const double *piggy_src) {
     Ctx &c = *ctx;
     if (residual_update != 0 && handle) {
         // y = op.LDL * [x(1:n) - op.Aty; x(n+1:N) - op.Cy]; then op.Aty = op.A(1:n, n+1:N) * y2,
         // op.Cy = op.A(n+1:N, n+1:N) * y2 = the columns n+1:N of Kp times y2  (opLDL2.m:164-172)
         launch_sub_state(c, x, neg_from, ghn.p, N, t.p, run);
-        ldl_solve(t.p, N, y, false, run, nullptr);
+        ldl_solve(t.p, N, y, false, run, nullptr, piggy_src);
         launch_spmv_colmask(c, dKp, n, y, ghn.p, run);
     } else {
         // y = op.LDL * x   (opLDL2.m:165-167); the residual-update branch subtracts the zero
         // state of a value object and its SpMVs are dead: skipped
-        ldl_solve(x, neg_from, y, false, run, nullptr);
+        ldl_solve(x, neg_from, y, false, run, nullptr, piggy_src);
     }
     if (nitref <= 0) return;
     const int64_t steps = (int64_t)nitref;

@@ -137,8 +137,28 @@ __global__ void krylov_fin_kernel(P pol, DState *st, const double *tot) {
     if (pol.ran(st)) pol.fin(st, tot);
 }
 
+// distributed mode with the partials carried by the separator exchange (Precond::apply with
+// piggy_src = c.red): the epilogue on the rank-ordered sum of every rank's two partials
 template <class P>
-void launch_krylov_spmv(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n, const P &pol) {
+__global__ void krylov_fin_sep_kernel(P pol, DState *st, const double *rbuf, int nranks, int64_t kt,
+                                      int64_t kt_data) {
+    if (threadIdx.x || blockIdx.x) return;
+    if (!pol.ran(st)) return;
+    double tot[2] = {0.0, 0.0};
+    for (int r = 0; r < nranks; r++)
+        for (int j = 0; j < 2; j++) tot[j] += rbuf[(int64_t)r * kt + kt_data + j];
+    pol.fin(st, tot);
+}
+template <class P>
+void launch_krylov_fin_sep(Ctx &c, const DSep &S, DState *st, const P &pol) {
+    hipLaunchKernelGGL(krylov_fin_sep_kernel<P>, dim3(1), dim3(64), 0, c.stream, pol, st, (const double *)S.rbuf.p,
+                       c.nranks, S.kt, S.kt_data);
+    CPK_HIP(hipGetLastError());
+}
+
+// defer (distributed): leave the local partials in c.red for the caller to carry
+template <class P>
+void launch_krylov_spmv(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n, const P &pol, bool defer = false) {
     const bool dist = c.dist();
     if (AC.halo() && AC.kmax > 0) {
         if (AC.nsend > 0)
@@ -156,7 +176,7 @@ void launch_krylov_spmv(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n
         hipLaunchKernelGGL((spmv_stream<EpiKrylov<P>, false>), dim3(grid), dim3(kBlock), 0, c.stream, AC.ptr.p,
                            AC.col.p, AC.val.p, AC.blk.p, AC.nblk, (const double *)nullptr, (int64_t)0, e,
                            (const double *)nullptr, (int64_t)0);
-    if (dist) {
+    if (dist && !defer) {
         c.comm->allreduce_sum(c.red.p, 2, c.stream);
         hipLaunchKernelGGL(krylov_fin_kernel<P>, dim3(1), dim3(64), 0, c.stream, pol, st, (const double *)c.red.p);
     }
@@ -1354,9 +1374,18 @@ void SolveCore::minres_like(int kind, const double *b, double *xy, cpk_stats *st
             printf("stopTol = %e\n", h.stopTol);
             printf("%5s  %9s\n", "iter", "|resid|");
         }
+        // distributed: vprec = M*[u; -t] does not depend on alpha (cpminres.m:187-190), so alpha's
+        // partials ride in the preconditioner's first separator allgather instead of an allreduce
+        const bool piggy = c.dist() && M.piggyback_ok() && !getenv("CPK_NO_PIGGY");
         auto body = [&]() {
-            launch_krylov_spmv(c, AC, st, UT, n, PolLanczosSpmv<0>{VQ, N, 0});
-            M.apply(UT, n, VPREC, &st->running);
+            if (piggy) {
+                launch_krylov_spmv(c, AC, st, UT, n, PolLanczosSpmv<0>{VQ, N, 0}, true);
+                M.apply(UT, n, VPREC, &st->running, c.red.p);
+                launch_krylov_fin_sep(c, M.sep, st, PolLanczosSpmv<0>{VQ, N, 0});
+            } else {
+                launch_krylov_spmv(c, AC, st, UT, n, PolLanczosSpmv<0>{VQ, N, 0});
+                M.apply(UT, n, VPREC, &st->running);
+            }
             launch_ewred<2>(c, N, LanczosStep<0>{st, VQ, VPREC, UT, xy, W, n, N, 0, 2, 1});
             launch_ew(c, N, MinresUpdate{st, VQ, W, xy, n, N});
         };
