@@ -205,18 +205,19 @@ struct DSep {
     int64_t kt_data = 0;  // payload values of the plan; [kt_data, kt) are the piggyback slots
     DBuf<int32_t> tf_ptr, tf_col, tf_src, tb_ptr, tb_col, lev_ptr, lev_rows, send, tdof;
     DBuf<double> tf_val, tb_val, DT, sbuf, rbuf;
-    // staged solve (tprefix_kernel + tsolve_staged_kernel): forward rows split into their
-    // leading payload terms (tk_*) and the rest (tr_*); img is the LDS image of the level solve
-    // in HBM (static parts from setup; the row prefixes at off_pre and the pre-multiplied rest
-    // terms at off_rv, in doubles, are written by tprefix_kernel per solve)
-    DBuf<int32_t> tk_ptr, tk_col, tr_ptr, tr_col;
-    DBuf<double> tk_val, tr_val;
-    DBuf<char> img;
-    int64_t nrest = 0, nbwd = 0, off_pre = 0, off_rv = 0;
-    size_t lds = 0;  // bytes of the image (16-byte multiple), 0 = too large (one-pass global kernel)
+    // stepped solve (tprefix_kernel + tsolve_steps_kernel): forward rows split into their
+    // leading payload terms (tk_*) and the rest; the level solve is nsf forward and nsb backward
+    // steps (steps[s] = waves | barrier flag) of records rec_v / rec_m (kernels.hip);
+    // tprefix_kernel writes the row prefixes into pre (pre[nT] = 1.0) and the rest's payload
+    // terms (tr_*, pre-multiplied) into their records' values (tr_slot)
+    DBuf<int32_t> tk_ptr, tk_col, tr_ptr, tr_col, tr_slot, steps;
+    DBuf<double> tk_val, tr_val, pre, rec_v;
+    DBuf<uint32_t> rec_m;
+    int64_t nsf = 0, nsb = 0, nrec = 0;
+    size_t lds = 0;  // LDS bytes of the stepped solve, 0 = not staged (one-pass global kernel)
 };
 struct RankPlan;
-// Split the forward rows of T and build the LDS image of the staged separator solve.
+// Split the forward rows of T and build the steps of the separator level solve.
 void dsep_stage(DSep &T, const RankPlan &rp);
 struct DofMap;
 

@@ -7,7 +7,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <array>
+#include <tuple>
 #include <cstdlib>
+#include <cstring>
 
 #include "dev.hpp"
 #include "devutil.hpp"
@@ -350,45 +353,36 @@ __global__ __launch_bounds__(256) void tsolve_kernel(
     }
 }
 
-// Staged separator solve: the same arithmetic in the same order, restructured for latency.
-// The one-pass kernel above walks each row's terms with two dependent global loads per term;
-// at S10 / 8 ranks T has 593 rows, 13 levels and rows of up to 49 payload terms, and it took
-// ~160 us.  Here:
-//  (1) tprefix_kernel, one wave per row across the chip: each row subtracts its LEADING payload
-//      terms (coalesced loads, one gather, the subtractions in order on one lane), and the
-//      payload terms of the rest of the row are pre-multiplied (read later against 1.0);
-//  (2) tsolve_staged_kernel, one workgroup: stages the rest of the forward rows, the backward
-//      rows, D_T and the level lists in LDS and runs the levels out of LDS.
+// Stepped separator solve: the same arithmetic in the same order, restructured for latency.
+// The one-pass kernel above walks each term with two dependent global loads; at S10 / 8 ranks
+// T has 593 rows, 13 levels and rows of up to 49 payload terms, and it took ~160 us.  Here:
+//  (1) tprefix_kernel, one wave per row across the chip: each forward row subtracts its LEADING
+//      payload terms (coalesced loads, one gather, the subtractions in order on one lane) into
+//      pre[t], and the payload terms of the rest of the row are pre-multiplied into their
+//      records (read later against the 1.0 slot wt[nT]);
+//  (2) tsolve_steps_kernel, one workgroup, stages the records in LDS and runs the levels as a
+//      list of steps built at setup.  A step hands each lane of its first W waves one record
+//      (value, meta).  A row chunk is a lead lane (row, length, flags) followed by its terms on
+//      the next lanes of the same wave; each lane forms its product, and the lead subtracts the
+//      chunk's products in the row's order.  No index is looked up at run time: a step costs
+//      one record read, one gather, the chain, one store and, at the end of a level, a barrier.
+//      (A level loop that looked its rows up in LDS spent ~1500 cycles per level on dependent
+//      index loads.)
 // Row sums keep the exported factor's order: bit-identical.
 constexpr int kTsolveThreads = 1024;
 constexpr size_t kTsolveMaxLds = 160 * 1024;  // gfx950: 160 KB of LDS per workgroup
-
-// acc - v[e] * w[col(e)] for e in [e0, e1), in order, eight terms per LDS round trip (absent
-// terms subtract +0.0)
-__device__ __forceinline__ double lds_row_sum(double acc, int e0, int e1, const int32_t *col, const double *v,
-                                              const double *w) {
-    constexpr int K = 8;
-    for (int e = e0; e < e1; e += K) {
-        int c[K];
-        double a[K], x[K];
-#pragma unroll
-        for (int u = 0; u < K; u++) {
-            const int q = e + u < e1 ? e + u : e1 - 1;
-            c[u] = col[q], a[u] = v[q];
-        }
-#pragma unroll
-        for (int u = 0; u < K; u++) x[u] = w[c[u]];
-#pragma unroll
-        for (int u = 0; u < K; u++) acc -= (e + u < e1) ? a[u] * x[u] : 0.0;
-    }
-    return acc;
-}
+constexpr int kTsChunk = 32;                  // terms per row chunk
+constexpr int kTsMaxSteps = 256;              // the step table lives in 4 VGPRs per lane
+constexpr int64_t kTsMaxRows = 1 << 16;
+// meta: a term lane holds its LDS column; a lead lane kTsLead | row | (length - 1) << 16 | flags
+constexpr uint32_t kTsLead = 1u << 31, kTsFirst = 1u << 30, kTsLast = 1u << 29;
+constexpr uint32_t kTsBarrier = 1u << 16;  // step table: waves | barrier after the step | longest chunk << 20
 
 __global__ __launch_bounds__(256) void tprefix_kernel(
     int nT, const int32_t *__restrict__ tk_ptr, const int32_t *__restrict__ tk_col, const double *__restrict__ tk_val,
     const int32_t *__restrict__ tr_ptr, const int32_t *__restrict__ tr_col, const double *__restrict__ tr_val,
-    const int32_t *__restrict__ tf_src, const double *__restrict__ rbuf, double *__restrict__ pre,
-    double *__restrict__ rv_out, const int *run, const int *active) {  // pre, rv_out: regions of the LDS image
+    const int32_t *__restrict__ tr_slot, const int32_t *__restrict__ tf_src, const double *__restrict__ rbuf,
+    double *__restrict__ pre, double *__restrict__ rec_v, const int *run, const int *active) {
     __shared__ double prod[4][kWave];
     if (skip(run, active)) return;
     const int wv = threadIdx.x / kWave, lane = threadIdx.x % kWave;
@@ -409,55 +403,102 @@ __global__ __launch_bounds__(256) void tprefix_kernel(
         __builtin_amdgcn_wave_barrier();
     }
     if (lane == 0) pre[t] = acc;
-    for (int q = tr_ptr[t] + lane; q < tr_ptr[t + 1]; q += kWave) {
-        const int c = tr_col[q];
-        const double v = tr_val[q];
-        rv_out[q] = c >= 0 ? v * rbuf[c] : v;
+    for (int q = tr_ptr[t] + lane; q < tr_ptr[t + 1]; q += kWave) rec_v[tr_slot[q]] = tr_val[q] * rbuf[tr_col[q]];
+}
+
+// x of lane i + 1 (wave shift; the last lane gets 0)
+__device__ __forceinline__ double ts_next_lane(double x) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x130, 0xf, 0xf, true);  // wave_shl:1
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x130, 0xf, 0xf, true);
+    return __hiloint2double(hi, lo);
+}
+
+// steps [s0, s1); woff: the first record of step s0 (in waves) on entry, of step s1 on exit
+__device__ __forceinline__ void ts_steps(int s0, int s1, const int (&tab)[kTsMaxSteps / kWave], int &woff,
+                                         const double *rv, const uint32_t *rm, double *wt, double &acc) {
+    const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+    for (int s = s0; s < s1; s++) {
+        int e = 0;
+#pragma unroll
+        for (int i = 0; i < kTsMaxSteps / kWave; i++)
+            if ((s >> 6) == i) e = __builtin_amdgcn_readlane(tab[i], s & 63);
+        const int W = e & 0xffff;
+        if (wave < W) {  // whole waves: the shifts below need every lane
+            const int r = (woff + wave) * kWave + lane;
+            const double v = rv[r];
+            const uint32_t m = rm[r];
+            const bool lead = m & kTsLead;
+            const double g = wt[m & 0xffffu];  // a term's column, or the lead's own row
+            double x = lead ? 0.0 : v * g;
+            const int n = lead ? (int)((m >> 16) & 31u) + 1 : 0;
+            if (lead && (m & kTsFirst)) acc = g;
+            // the lead subtracts the products of the next n lanes in order, shifted in one lane
+            // at a time (no LDS traffic: 16 waves reading each other's products through LDS
+            // cost more LDS-array cycles than the whole chain)
+            // (past its own chunk a lead subtracts +0.0, which leaves acc unchanged: the select
+            // stays off the chain of subtractions)
+            const int nmax = (e >> 20) & 63;
+            for (int k0 = 1; k0 <= nmax; k0 += 8) {  // the shifts of a group run ahead of its chain
+                double xs[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    x = ts_next_lane(x);
+                    xs[k] = k0 + k <= n ? x : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < 8; k++) acc -= xs[k];
+            }
+            if (lead && (m & kTsLast)) wt[m & 0xffffu] = acc;
+        }
+        woff += W;
+        if (e & kTsBarrier) __syncthreads();
     }
 }
 
-__global__ __launch_bounds__(kTsolveThreads) void tsolve_staged_kernel(
-    int nlev, int nT, int nrest, int nbwd, const uint4 *__restrict__ img, int img_vec, const int32_t *__restrict__ tdof,
-    int ntdof, double *wT, double *y, int add, const int *run, const int *active) {
-    extern __shared__ __attribute__((aligned(16))) char tsm[];
+__global__ __launch_bounds__(kTsolveThreads) void tsolve_steps_kernel(
+    int nT, int nsf, int nsb, int nrec, const double *__restrict__ rec_v, const uint32_t *__restrict__ rec_m,
+    const int32_t *__restrict__ steps, const double *__restrict__ pre, const double *__restrict__ DT,
+    const int32_t *__restrict__ tdof, int ntdof, double *wT, double *y, int add, const int *run, const int *active) {
+    // LDS: wt[nT + 1, even] | rv[nrec] | rm[nrec]
+    extern __shared__ __attribute__((aligned(16))) double tsw[];
     if (skip(run, active)) return;
-    double *wt = reinterpret_cast<double *>(tsm);  // nT + 1: wt[nT] = 1.0 (pre-multiplied terms)
-    double *dt = wt + nT + 1, *rv = dt + nT, *bv = rv + nrest;
-    int32_t *rc = reinterpret_cast<int32_t *>(bv + nbwd);
-    int32_t *bc = rc + nrest, *rp = bc + nbwd, *bp = rp + nT + 1, *lr = bp + nT + 1, *lp = lr + nT;
-    const int tid = threadIdx.x;
-    // the LDS image is one contiguous HBM image (static parts from setup, the row prefixes and
-    // pre-multiplied rest terms from tprefix_kernel): 16-byte copies, every load in flight at once
-    constexpr int U = 8;
-    uint4 *dst = reinterpret_cast<uint4 *>(tsm);
-    for (int i0 = tid; i0 < img_vec; i0 += U * kTsolveThreads) {
-        uint4 q[U];
+    const int tid = threadIdx.x, lane = tid % kWave;
+    double *wt = tsw, *rv = wt + ((nT + 2) & ~1);
+    uint32_t *rm = reinterpret_cast<uint32_t *>(rv + nrec);
+    int tab[kTsMaxSteps / kWave];  // lane i of tab[k]: step 64k + i (waves | barrier | longest chunk)
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int i = i0 + u * kTsolveThreads;
-            q[u] = i < img_vec ? img[i] : uint4{0, 0, 0, 0};
-        }
+    for (int k = 0; k < kTsMaxSteps / kWave; k++) {
+        const int s = k * kWave + lane;
+        tab[k] = s < nsf + nsb ? steps[s] : 0;
+    }
+    {  // stage: every load in flight at once
+        constexpr int U = 8;
+        for (int i0 = tid; i0 <= nT; i0 += kTsolveThreads) wt[i0] = pre[i0];  // pre[nT] = 1.0
+        for (int i0 = tid; i0 < nrec; i0 += U * kTsolveThreads) {
+            double a[U];
+            uint32_t b[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int i = i0 + u * kTsolveThreads;
-            if (i < img_vec) dst[i] = q[u];
+            for (int u = 0; u < U; u++) {
+                const int i = i0 + u * kTsolveThreads;
+                a[u] = i < nrec ? rec_v[i] : 0.0;
+                b[u] = i < nrec ? rec_m[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int i = i0 + u * kTsolveThreads;
+                if (i < nrec) rv[i] = a[u], rm[i] = b[u];
+            }
         }
     }
     __syncthreads();
-    for (int l = 0; l < nlev; l++) {  // forward: the rest of each row
-        for (int q = lp[l] + tid; q < lp[l + 1]; q += kTsolveThreads) {
-            const int t = lr[q];
-            wt[t] = lds_row_sum(wt[t], rp[t], rp[t + 1], rc, rv, wt);
-        }
-        __syncthreads();
-    }
-    for (int l = nlev - 1; l >= 0; l--) {  // backward
-        for (int q = lp[l] + tid; q < lp[l + 1]; q += kTsolveThreads) {
-            const int t = lr[q];
-            wt[t] = lds_row_sum(wt[t] / dt[t], bp[t], bp[t + 1], bc, bv, wt);
-        }
-        __syncthreads();
-    }
+    double acc = 0.0;
+    int woff = 0;
+    ts_steps(0, nsf, tab, woff, rv, rm, wt, acc);  // forward: the rest of each row
+    // backward: every row's diagonal step first (D is diagonal, and a row's terms read only rows
+    // of later levels, final by the time it runs), then the rows' terms
+    for (int t = tid; t < nT; t += kTsolveThreads) wt[t] = wt[t] / DT[t];
+    __syncthreads();
+    ts_steps(nsf, nsf + nsb, tab, woff, rv, rm, wt, acc);
     for (int t = tid; t < nT; t += kTsolveThreads) {
         wT[t] = wt[t];
         if (t < ntdof) {
@@ -467,43 +508,163 @@ __global__ __launch_bounds__(kTsolveThreads) void tsolve_staged_kernel(
     }
 }
 
+namespace {
+// Packs one direction's level rows into steps: a step has kTsolveThreads lanes in waves of 64,
+// a row chunk takes a lead lane plus one lane per term inside one wave.  Records are stored by
+// step, for the step's used waves only.
+struct StepPacker {
+    static constexpr int kWaves = kTsolveThreads / kWave;
+    struct Lane {
+        double v = 0.0;
+        uint32_t m = 0;
+        int64_t term = -1;  // caller's term id (slot callback), -1: none
+    };
+    std::vector<std::vector<Lane>> steps;  // kTsolveThreads lanes each
+    std::vector<int> used_waves;           // 1 + the last wave holding a chunk
+    std::vector<int> longest;              // the step's longest chunk
+    std::vector<bool> barrier;
+    // terms(t): (value, LDS column, term id) of row t in order
+    template <class Terms>
+    void level(const std::vector<int32_t> &rows, Terms terms) {
+        if (rows.empty()) return;
+        const size_t first = steps.size();
+        std::vector<std::array<int, kWaves>> used;
+        auto ensure = [&](size_t k) {
+            while (used.size() <= k) {
+                used.push_back({});
+                steps.emplace_back(kTsolveThreads);
+                used_waves.push_back(0);
+                longest.push_back(0);
+                barrier.push_back(false);
+            }
+        };
+        auto put = [&](int32_t t, size_t k, int w, int lane0, const std::vector<std::tuple<double, int32_t, int64_t>> &tv,
+                       size_t j0, size_t n, bool fst, bool lst) {
+            auto &st = steps[first + k];
+            Lane &ld = st[(size_t)(w * kWave + lane0)];
+            ld.m = kTsLead | (uint32_t)t | ((uint32_t)(n - 1) << 16) | (fst ? kTsFirst : 0u) | (lst ? kTsLast : 0u);
+            for (size_t j = 0; j < n; j++) {
+                Lane &l = st[(size_t)(w * kWave + lane0 + 1) + j];
+                l.v = std::get<0>(tv[j0 + j]), l.m = (uint32_t)std::get<1>(tv[j0 + j]), l.term = std::get<2>(tv[j0 + j]);
+            }
+            used_waves[first + k] = std::max(used_waves[first + k], w + 1);
+            longest[first + k] = std::max(longest[first + k], (int)n);
+        };
+        std::vector<std::pair<size_t, int32_t>> single;
+        for (int32_t t : rows) {
+            const auto tv = terms(t);
+            const size_t n = tv.size();
+            if (n <= (size_t)kTsChunk) {
+                single.push_back({n, t});
+                continue;
+            }
+            const size_t k = (n + kTsChunk - 1) / kTsChunk;  // a wave of its own in k consecutive steps
+            for (size_t s = 0;; s++) {
+                ensure(s + k - 1);
+                int w = 0;
+                for (; w < kWaves; w++) {
+                    bool fr = true;
+                    for (size_t j = 0; j < k && fr; j++) fr = used[s + j][w] == 0;
+                    if (fr) break;
+                }
+                if (w == kWaves) continue;
+                for (size_t j = 0; j < k; j++) {
+                    used[s + j][w] = kWave;
+                    put(t, s + j, w, 0, tv, j * kTsChunk, std::min<size_t>(kTsChunk, n - j * kTsChunk), j == 0, j == k - 1);
+                }
+                break;
+            }
+        }
+        std::stable_sort(single.begin(), single.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
+        for (const auto &rn : single) {
+            const auto tv = terms(rn.second);
+            const int need = (int)rn.first + 1;
+            bool placed = false;
+            for (size_t s = 0; !placed; s++) {
+                ensure(s);
+                for (int w = 0; w < kWaves && !placed; w++)
+                    if (kWave - used[s][w] >= need) {
+                        put(rn.second, s, w, used[s][w], tv, 0, rn.first, true, true);
+                        used[s][w] += need;
+                        placed = true;
+                    }
+            }
+        }
+        barrier.back() = true;
+    }
+};
+}  // namespace
+
 void dsep_stage(DSep &T, const RankPlan &rp) {
     const int64_t nT = T.nT;
-    std::vector<int32_t> kp(nT + 1, 0), kc, rptr(nT + 1, 0), rc, rl;
-    std::vector<double> kv, rv;
+    T.lds = 0;
+    if (nT <= 0 || nT >= kTsMaxRows) return;
+    // forward rows: leading payload terms (tprefix_kernel) | the rest, from the first T term on
+    std::vector<int32_t> kp(nT + 1, 0), kc, rptr(nT + 1, 0), rcol, rslot;
+    std::vector<double> kv, rval;
+    std::vector<int64_t> rest0(nT);
     for (int64_t t = 0; t < nT; t++) {
         int64_t e = rp.tf_ptr[t];
         for (; e < rp.tf_ptr[t + 1] && rp.tf_col[e] >= 0; e++) kc.push_back(rp.tf_col[e]), kv.push_back(rp.tf_val[e]);
-        for (; e < rp.tf_ptr[t + 1]; e++) {
-            rc.push_back(rp.tf_col[e]), rv.push_back(rp.tf_val[e]);
-            rl.push_back(rp.tf_col[e] >= 0 ? (int32_t)nT : -rp.tf_col[e] - 1);  // LDS column: T row, or the 1.0 slot
+        kp[t + 1] = (int32_t)kc.size();
+        rest0[t] = e;
+    }
+    StepPacker P;
+    using TV = std::vector<std::tuple<double, int32_t, int64_t>>;
+    auto rows_of = [&](int64_t l, bool bwd) {
+        std::vector<int32_t> r;
+        for (int64_t q = rp.tlev_ptr[l]; q < rp.tlev_ptr[l + 1]; q++) {
+            const int32_t t = rp.tlev_rows[q];
+            if (bwd ? rp.tb_ptr[t + 1] > rp.tb_ptr[t] : rp.tf_ptr[t + 1] > rest0[t]) r.push_back(t);
         }
-        kp[t + 1] = (int32_t)kc.size(), rptr[t + 1] = (int32_t)rc.size();
+        return r;
+    };
+    // forward terms: T rows against wt, payload terms (pre-multiplied per solve) against wt[nT]
+    for (int64_t l = 0; l < T.nlev; l++)
+        P.level(rows_of(l, false), [&](int32_t t) {
+            TV tv;
+            for (int64_t e = rest0[t]; e < rp.tf_ptr[t + 1]; e++)
+                tv.emplace_back(rp.tf_col[e] >= 0 ? 0.0 : rp.tf_val[e],
+                                rp.tf_col[e] >= 0 ? (int32_t)nT : (int32_t)(-rp.tf_col[e] - 1),
+                                rp.tf_col[e] >= 0 ? e : (int64_t)-1);
+            return tv;
+        });
+    T.nsf = (int64_t)P.steps.size();
+    for (int64_t l = T.nlev - 1; l >= 0; l--)
+        P.level(rows_of(l, true), [&](int32_t t) {
+            TV tv;
+            for (int64_t e = rp.tb_ptr[t]; e < rp.tb_ptr[t + 1]; e++) tv.emplace_back(rp.tb_val[e], rp.tb_col[e], (int64_t)-1);
+            return tv;
+        });
+    T.nsb = (int64_t)P.steps.size() - T.nsf;
+    if (T.nsf + T.nsb > kTsMaxSteps) return;
+    // records of the used waves, step by step
+    std::vector<double> rv;
+    std::vector<uint32_t> rm;
+    std::vector<int32_t> tab;
+    std::vector<int64_t> pay_slot(rp.tf_col.size(), -1);
+    for (size_t s = 0; s < P.steps.size(); s++) {
+        tab.push_back(P.used_waves[s] | (P.barrier[s] ? (int32_t)kTsBarrier : 0) | (P.longest[s] << 20));
+        for (int i = 0; i < P.used_waves[s] * kWave; i++) {
+            const auto &l = P.steps[s][(size_t)i];
+            if (l.term >= 0) pay_slot[(size_t)l.term] = (int64_t)rv.size();
+            rv.push_back(l.v), rm.push_back(l.m);
+        }
+    }
+    for (int64_t t = 0; t < nT; t++) {
+        for (int64_t e = rest0[t]; e < rp.tf_ptr[t + 1]; e++)
+            if (rp.tf_col[e] >= 0) rcol.push_back(rp.tf_col[e]), rval.push_back(rp.tf_val[e]), rslot.push_back((int32_t)pay_slot[(size_t)e]);
+        rptr[t + 1] = (int32_t)rcol.size();
     }
     T.tk_ptr.upload(kp), T.tk_col.upload(kc), T.tk_val.upload(kv);
-    T.tr_ptr.upload(rptr), T.tr_col.upload(rc), T.tr_val.upload(rv);
-    T.nrest = (int64_t)rc.size(), T.nbwd = (int64_t)rp.tb_col.size();
-    // the LDS image of tsolve_staged_kernel:
-    //   double wt[nT + 1] | dt[nT] | rv[nrest] | bv[nbwd] | int32 rc[nrest] | bc[nbwd] | rp[nT + 1] | bp[nT + 1]
-    //   | lr[nT] | lp[nlev + 1]
-    const int64_t nb = T.nbwd, nl = T.nlev;
-    const size_t bytes = 8 * (size_t)(2 * nT + 1 + T.nrest + nb) + 4 * (size_t)(T.nrest + nb + 3 * (nT + 1) + nl + 1);
-    const size_t padded = (bytes + 15) & ~(size_t)15;
-    std::vector<char> img(padded, 0);
-    double *wt = reinterpret_cast<double *>(img.data());
-    double *dt = wt + nT + 1, *rvv = dt + nT, *bv = rvv + T.nrest;
-    int32_t *rcc = reinterpret_cast<int32_t *>(bv + nb);
-    int32_t *bc = rcc + T.nrest, *rpp = bc + nb, *bp = rpp + nT + 1, *lr = bp + nT + 1, *lp = lr + nT;
-    wt[nT] = 1.0;
-    for (int64_t t = 0; t < nT; t++) dt[t] = rp.DT[t], lr[t] = rp.tlev_rows[t];
-    for (int64_t i = 0; i < nb; i++) bv[i] = rp.tb_val[i], bc[i] = rp.tb_col[i];
-    for (int64_t i = 0; i < T.nrest; i++) rcc[i] = rl[i];
-    for (int64_t t = 0; t <= nT; t++) rpp[t] = rptr[t], bp[t] = (int32_t)rp.tb_ptr[t];
-    for (int64_t l = 0; l <= nl; l++) lp[l] = rp.tlev_ptr[l];
-    T.img.upload(img);
-    T.off_pre = 0;
-    T.off_rv = (int64_t)((char *)rvv - img.data()) / 8;
-    T.lds = padded <= kTsolveMaxLds ? padded : 0;
+    T.tr_ptr.upload(rptr), T.tr_col.upload(rcol), T.tr_val.upload(rval), T.tr_slot.upload(rslot);
+    T.rec_v.upload(rv), T.rec_m.upload(rm), T.steps.upload(tab);
+    T.nrec = (int64_t)rv.size();
+    std::vector<double> pre(nT + 1, 0.0);
+    pre[nT] = 1.0;
+    T.pre.upload(pre);
+    const size_t lds = 8 * (size_t)((nT + 2) & ~1) + 12 * (size_t)T.nrec;
+    T.lds = lds <= kTsolveMaxLds ? lds : 0;
 }
 
 // payload: w of this rank's rows that separator rows read, then (rank 0) the T inputs +-x[tdof]
@@ -535,17 +696,17 @@ void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x
 void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active) {
     if (S.nT == 0) return;
     static bool lds_attr = [] {
-        return hipFuncSetAttribute((const void *)tsolve_staged_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        return hipFuncSetAttribute((const void *)tsolve_steps_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)kTsolveMaxLds) == hipSuccess;
     }();
     if (S.lds && (S.lds <= 64 * 1024 || lds_attr) && !getenv("CPK_TSOLVE_ONEPASS")) {
-        double *img = reinterpret_cast<double *>(S.img.p);
         hipLaunchKernelGGL(tprefix_kernel, dim3((unsigned)((S.nT + 3) / 4)), dim3(256), 0, c.stream, (int)S.nT,
-                           S.tk_ptr.p, S.tk_col.p, S.tk_val.p, S.tr_ptr.p, S.tr_col.p, S.tr_val.p, S.tf_src.p,
-                           S.rbuf.p, img + S.off_pre, img + S.off_rv, run, active);
-        hipLaunchKernelGGL(tsolve_staged_kernel, dim3(1), dim3(kTsolveThreads), S.lds, c.stream, (int)S.nlev,
-                           (int)S.nT, (int)S.nrest, (int)S.nbwd, (const uint4 *)S.img.p, (int)(S.lds / 16), S.tdof.p,
-                           (int)S.ntdof, wT, y, add ? 1 : 0, run, active);
+                           S.tk_ptr.p, S.tk_col.p, S.tk_val.p, S.tr_ptr.p, S.tr_col.p, S.tr_val.p, S.tr_slot.p,
+                           S.tf_src.p, S.rbuf.p, S.pre.p, S.rec_v.p, run, active);
+        hipLaunchKernelGGL(tsolve_steps_kernel, dim3(1), dim3(kTsolveThreads), S.lds, c.stream, (int)S.nT,
+                           (int)S.nsf, (int)S.nsb, (int)S.nrec, (const double *)S.rec_v.p,
+                           (const uint32_t *)S.rec_m.p, S.steps.p, (const double *)S.pre.p, (const double *)S.DT.p,
+                           S.tdof.p, (int)S.ntdof, wT, y, add ? 1 : 0, run, active);
         CPK_HIP(hipGetLastError());
         return;
     }

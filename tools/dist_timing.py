@@ -23,7 +23,12 @@ from cpkrylov_amd.synthetic import saddle_system  # noqa: E402
 torch.cuda.init()
 S = saddle_system(int(os.environ.get("N", "10000000")))
 runs = [(int(a.split(":")[0]), int(a.split(":")[1])) for a in sys.argv[1:]] or [(1, 0), (2, 0), (4, 0), (8, 0), (8, 7)]
-for P, r in runs:
+# CPK_SWEEPS="cfg1;cfg2": repeat every run under each CPK_SWEEP staging configuration
+sweeps = [x for x in os.environ.get("CPK_SWEEPS", "").split(";") if x] or [os.environ.get("CPK_SWEEP", "")]
+runs = [(P, r, sw) for sw in sweeps for P, r in runs]
+for P, r, sw in runs:
+    if sw:
+        os.environ["CPK_SWEEP"] = sw
     ctx = cpk.Context(device=0, rank=r, nranks=P) if P > 1 else cpk.Context(device=0)
     A, B, Cm, G = (cpk.Matrix(S[k], ctx) for k in ("Q", "B", "C", "G"))
     M = cpk.opLDL2(G, B, -S["C"], ctx=ctx)
@@ -53,7 +58,7 @@ for P, r in runs:
         per_it = dt / max(int(st.niters), 1) * 1e3
     except cpk.CpkError as e:
         err = str(e)[:120]
-    print(json.dumps({"P": P, "rank": r, "N_loc": len(dofs), "nrounds": M.info["nrounds"],
+    print(json.dumps({"P": P, "rank": r, "sweep": sw, "N_loc": len(dofs), "nrounds": M.info["nrounds"],
                       "spmv_us": round(p.spmv_ms * 1e3, 1), "resid_us": round(p.resid_ms * 1e3, 1),
                       "fwd_us": round(p.fwd_ms * 1e3, 1), "bwd_us": round(p.bwd_ms * 1e3, 1),
                       "apply_us": round(p.apply_ms * 1e3, 1), "niters": int(st.niters),
