@@ -53,7 +53,8 @@ struct cpk_mat_s {
         auto it = dac.find(key);
         if (it == dac.end()) {
             auto m = std::make_unique<DMat>();
-            make_dist_dmat(dist_csr(blkdiag(h, C->h), *M.dofmap, ctx->c.rank, false), ctx->c.nranks, *m);
+            make_dist_dmat(dist_csr(blkdiag(h, C->h), *M.dofmap, ctx->c.rank, false, kKrylovSpare), ctx->c.nranks,
+                           *m);
             it = dac.emplace(key, std::move(m)).first;
         }
         return *it->second;

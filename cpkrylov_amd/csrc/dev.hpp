@@ -90,9 +90,9 @@ struct DMat {
     bool is_diag = false;
     uint64_t gen = 0;   // unique per upload (keys cached solver graphs)
     // distributed rows (DistCsr): columns >= nloc read the allgathered halo buffer
-    int64_t nloc = -1, kmax = 0, nsend = 0;
+    int64_t nloc = -1, kmax = 0, kstride = 0, nsend = 0;
     DBuf<int32_t> send;         // local indices published to the other ranks
-    DBuf<double> sbuf, rbuf;    // halo payload [kmax], allgathered halo [nranks * kmax]
+    DBuf<double> sbuf, rbuf;    // halo payload [kstride], allgathered halo [nranks * kstride]
     bool halo() const { return nloc >= 0; }
     size_t bytes() const { return ptr.bytes() + col.bytes() + val.bytes() + blk.bytes(); }
 };
@@ -200,6 +200,9 @@ Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22);
 
 // The separator solve of a distributed preconditioner, device copy.
 constexpr int64_t kSepPiggy = 2;  // spare payload slots per rank in the separator exchange
+// spare slots per rank in the Krylov operator's halo exchange: the Lanczos beta partials ride
+// there with the next vector's halo (solvers.hip, cpminres)
+constexpr int64_t kKrylovSpare = 2;
 struct DSep {
     int64_t nT = 0, kt = 0, nlev = 0, nsend = 0, ntdof = 0;
     int64_t kt_data = 0;  // payload values of the plan; [kt_data, kt) are the piggyback slots

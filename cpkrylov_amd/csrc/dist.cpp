@@ -136,7 +136,7 @@ DofMap make_dofmap(const Factor &f, const TreeSplit &ts, int64_t n) {
     return dm;
 }
 
-DistCsr dist_csr(const HCsr &K, const DofMap &dm, int rank, bool rows_x_only) {
+DistCsr dist_csr(const HCsr &K, const DofMap &dm, int rank, bool rows_x_only, int64_t spare) {
     const int64_t rows_end = rows_x_only ? dm.n : dm.N;
     if (K.nrows != rows_end || K.ncols != dm.N) throw Error(CPK_ERR_DIM, "dist_csr: matrix shape does not match the dof map");
     // slot of every dof some other rank reads (per owner, ascending dof)
@@ -152,6 +152,7 @@ DistCsr dist_csr(const HCsr &K, const DofMap &dm, int rank, bool rows_x_only) {
         if (need[c]) slot[c] = (int32_t)cnt[dm.owner[c]]++;
     DistCsr d;
     d.kmax = *std::max_element(cnt.begin(), cnt.end());
+    d.kstride = d.kmax + spare;
     const int64_t nl = dm.n_loc[rank], ml = dm.m_loc[rank];
     d.nloc = nl + ml;
     for (int64_t c = 0; c < dm.N; c++)
@@ -160,7 +161,7 @@ DistCsr dist_csr(const HCsr &K, const DofMap &dm, int rank, bool rows_x_only) {
     const std::vector<int32_t> dofs = dm.dofs(rank);
     const int64_t nrows = rows_x_only ? nl : nl + ml;
     d.a.nrows = nrows;
-    d.a.ncols = d.nloc + (int64_t)dm.P * d.kmax;
+    d.a.ncols = d.nloc + (int64_t)dm.P * d.kstride;
     d.a.ptr.assign(nrows + 1, 0);
     for (int64_t i = 0; i < nrows; i++) d.a.ptr[i + 1] = d.a.ptr[i] + (K.ptr[dofs[i] + 1] - K.ptr[dofs[i]]);
     d.a.ind.resize(d.a.ptr[nrows]);
@@ -170,7 +171,7 @@ DistCsr dist_csr(const HCsr &K, const DofMap &dm, int rank, bool rows_x_only) {
         int64_t o = d.a.ptr[i];
         for (int64_t p = K.ptr[g]; p < K.ptr[g + 1]; p++, o++) {  // global column order kept
             const int32_t c = K.ind[p];
-            d.a.ind[o] = dm.owner[c] == rank ? dm.lidx[c] : (int32_t)(d.nloc + (int64_t)dm.owner[c] * d.kmax + slot[c]);
+            d.a.ind[o] = dm.owner[c] == rank ? dm.lidx[c] : (int32_t)(d.nloc + (int64_t)dm.owner[c] * d.kstride + slot[c]);
             d.a.val[o] = K.val[p];
         }
     }

@@ -40,15 +40,17 @@ DofMap make_dofmap(const Factor &f, const TreeSplit &ts, int64_t n);
 
 // A distributed CSR: rank-local rows (local vector order) with each row's entries in the
 // global matrix's column order.  Column c < N_loc is local; c >= N_loc is a ghost read from
-// the allgathered halo buffer at position c - N_loc = owner * kmax + slot.
+// the allgathered halo buffer at position c - N_loc = owner * kstride + slot.
 struct DistCsr {
     HCsr a;                     // nrows = local rows, ncols = N_loc (+ ghost space)
     int64_t nloc = 0;           // local vector length (first ghost column)
     int64_t kmax = 0;           // halo payload per rank
+    int64_t kstride = 0;        // slots per rank in the halo buffer: kmax + spare
     std::vector<int32_t> send;  // local indices this rank publishes, in slot order
 };
-// rows_x_only: only the x-part rows (the shift's [A B'] rows)
-DistCsr dist_csr(const HCsr &K, const DofMap &dm, int rank, bool rows_x_only);
+// rows_x_only: only the x-part rows (the shift's [A B'] rows); spare: extra slots per rank
+// after the halo values (a solver's partial sums ride there, solvers.hip)
+DistCsr dist_csr(const HCsr &K, const DofMap &dm, int rank, bool rows_x_only, int64_t spare = 0);
 
 // This rank's slice of the factor and the separator solve.
 struct RankPlan {

@@ -237,15 +237,16 @@ static void launch_gather(Ctx &c, const double *x, const int32_t *idx, int64_t n
 void launch_halo(Ctx &c, const DMat &A, const double *x) {
     if (!A.halo() || A.kmax == 0) return;
     launch_gather(c, x, A.send.p, A.nsend, A.sbuf.p);
-    c.comm->allgather(A.sbuf.p, A.rbuf.p, (size_t)A.kmax, c.stream);
+    c.comm->allgather(A.sbuf.p, A.rbuf.p, (size_t)A.kstride, c.stream);
 }
 
 void make_dist_dmat(const DistCsr &a, int nranks, DMat &d) {
     make_dmat(a.a, d);
-    d.nloc = a.nloc, d.kmax = a.kmax, d.nsend = (int64_t)a.send.size();
+    d.nloc = a.nloc, d.kmax = a.kmax, d.kstride = a.kstride, d.nsend = (int64_t)a.send.size();
     d.send.upload(a.send);
-    d.sbuf.alloc((size_t)std::max<int64_t>(a.kmax, 1));
-    d.rbuf.alloc((size_t)std::max<int64_t>(a.kmax * nranks, 1));
+    d.sbuf.alloc((size_t)std::max<int64_t>(a.kstride, 1));
+    d.rbuf.alloc((size_t)std::max<int64_t>(a.kstride * nranks, 1));
+    CPK_HIP(hipMemset(d.sbuf.p, 0, d.sbuf.bytes()));
     CPK_HIP(hipMemset(d.rbuf.p, 0, d.rbuf.bytes()));
 }
 

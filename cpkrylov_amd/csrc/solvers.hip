@@ -156,16 +156,64 @@ void launch_krylov_fin_sep(Ctx &c, const DSep &S, DState *st, const P &pol) {
     CPK_HIP(hipGetLastError());
 }
 
-// defer (distributed): leave the local partials in c.red for the caller to carry
+// distributed mode: publish the halo of the vector the policy selects
 template <class P>
-void launch_krylov_spmv(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n, const P &pol, bool defer = false) {
-    const bool dist = c.dist();
-    if (AC.halo() && AC.kmax > 0) {
-        if (AC.nsend > 0)
-            hipLaunchKernelGGL(krylov_pack_kernel<P>, dim3((unsigned)std::min<int64_t>((AC.nsend + 255) / 256, 1024)),
-                               dim3(256), 0, c.stream, pol, st, AC.send.p, AC.nsend, AC.sbuf.p);
-        c.comm->allgather(AC.sbuf.p, AC.rbuf.p, (size_t)AC.kmax, c.stream);
+void launch_krylov_halo(Ctx &c, const DMat &AC, DState *st, const P &pol) {
+    if (AC.nsend > 0)
+        hipLaunchKernelGGL(krylov_pack_kernel<P>, dim3((unsigned)std::min<int64_t>((AC.nsend + 255) / 256, 1024)),
+                           dim3(256), 0, c.stream, pol, st, AC.send.p, AC.nsend, AC.sbuf.p);
+    c.comm->allgather(AC.sbuf.p, AC.rbuf.p, (size_t)AC.kstride, c.stream);
+}
+
+// distributed, the Lanczos step's beta partials carried by the next vector's halo exchange:
+// pack the (not yet normalised) vector's halo plus the two partials, allgather, then one block
+// sums the partials in rank order, runs the step's epilogue and normalises the received halo
+// exactly as the owners normalise their rows (MinresUpdate: v = v / beta when beta > 0)
+template <class P>
+__global__ void krylov_pack_red_kernel(P pol, DState *st, const int32_t *__restrict__ idx, int64_t n, int64_t kmax,
+                                       const double *__restrict__ red, double *out) {
+    const double *x = pol.select(st, nullptr);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = x[idx[i]];
+    if (blockIdx.x == 0 && threadIdx.x < 2) out[kmax + threadIdx.x] = red[threadIdx.x];
+}
+template <class F>
+__global__ void lanczos_fin_halo_kernel(F f, DState *st, double *rbuf, int nranks, int64_t kstride, int64_t kmax) {
+    __shared__ int live;
+    if (threadIdx.x == 0) {
+        double tot[2] = {0.0, 0.0};
+        for (int r = 0; r < nranks; r++)
+            for (int j = 0; j < 2; j++) tot[j] += rbuf[(int64_t)r * kstride + kmax + j];
+        live = f.setup();
+        if (live) f.fin(tot);
     }
+    __syncthreads();
+    if (!live || !(st->running) || !(st->beta > 0)) return;
+    const double beta = st->beta;
+    for (int64_t i = threadIdx.x; i < (int64_t)nranks * kstride; i += blockDim.x)
+        if (i % kstride < kmax) rbuf[i] = rbuf[i] / beta;
+}
+template <class P, class F>
+void launch_lanczos_step_halo(Ctx &c, const DMat &AC, DState *st, int64_t N, const F &f, const P &pol) {
+    c.ensure_partials((size_t)ew_grid(N) * 2);
+    hipLaunchKernelGGL((ewred_kernel<2, F>), dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f,
+                       RedBuf{c.partials.p, c.counter.p, c.red.p});
+    hipLaunchKernelGGL(krylov_pack_red_kernel<P>,
+                       dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((AC.nsend + 255) / 256, 1024))), dim3(256), 0,
+                       c.stream, pol, st, AC.send.p, AC.nsend, AC.kmax, (const double *)c.red.p, AC.sbuf.p);
+    c.comm->allgather(AC.sbuf.p, AC.rbuf.p, (size_t)AC.kstride, c.stream);
+    hipLaunchKernelGGL(lanczos_fin_halo_kernel<F>, dim3(1), dim3(256), 0, c.stream, f, st, AC.rbuf.p, c.nranks,
+                       AC.kstride, AC.kmax);
+    CPK_HIP(hipGetLastError());
+}
+
+// defer (distributed): leave the local partials in c.red for the caller to carry
+// halo_ready: the input's halo is already in AC.rbuf (launch_lanczos_step_halo)
+template <class P>
+void launch_krylov_spmv(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n, const P &pol, bool defer = false,
+                        bool halo_ready = false) {
+    const bool dist = c.dist();
+    if (AC.halo() && AC.kmax > 0 && !halo_ready) launch_krylov_halo(c, AC, st, pol);
     EpiKrylov<P> e{st, nullptr, y, n, RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr}, pol};
     const unsigned grid = spmv_grid(AC.nblk, true);
     if (AC.halo())
@@ -1377,16 +1425,24 @@ void SolveCore::minres_like(int kind, const double *b, double *xy, cpk_stats *st
         // distributed: vprec = M*[u; -t] does not depend on alpha (cpminres.m:187-190), so alpha's
         // partials ride in the preconditioner's first separator allgather instead of an allreduce
         const bool piggy = c.dist() && M.piggyback_ok() && !getenv("CPK_NO_PIGGY");
+        // and beta's partials ride in the next Lanczos vector's halo exchange (spare slots)
+        const bool hmerge = piggy && AC.halo() && AC.kstride >= AC.kmax + 2 && !getenv("CPK_NO_HALO_MERGE");
+        const PolLanczosSpmv<0> pol{VQ, N, 0};
+        if (hmerge) launch_krylov_halo(c, AC, st, pol);  // v1's halo, before the first iteration
         auto body = [&]() {
             if (piggy) {
-                launch_krylov_spmv(c, AC, st, UT, n, PolLanczosSpmv<0>{VQ, N, 0}, true);
+                launch_krylov_spmv(c, AC, st, UT, n, pol, true, hmerge);
                 M.apply(UT, n, VPREC, &st->running, c.red.p);
-                launch_krylov_fin_sep(c, M.sep, st, PolLanczosSpmv<0>{VQ, N, 0});
+                launch_krylov_fin_sep(c, M.sep, st, pol);
             } else {
-                launch_krylov_spmv(c, AC, st, UT, n, PolLanczosSpmv<0>{VQ, N, 0});
+                launch_krylov_spmv(c, AC, st, UT, n, pol);
                 M.apply(UT, n, VPREC, &st->running);
             }
-            launch_ewred<2>(c, N, LanczosStep<0>{st, VQ, VPREC, UT, xy, W, n, N, 0, 2, 1});
+            const LanczosStep<0> ls{st, VQ, VPREC, UT, xy, W, n, N, 0, 2, 1};
+            if (hmerge)
+                launch_lanczos_step_halo(c, AC, st, N, ls, pol);
+            else
+                launch_ewred<2>(c, N, ls);
             launch_ew(c, N, MinresUpdate{st, VQ, W, xy, n, N});
         };
         if (print) print_hist_lines("%5lld  %9.2e\n");
@@ -1643,12 +1699,13 @@ static std::string solver_key(const Ctx &c, const Precond &M, const DMat &AC, in
     char buf[512];
     const double restart = o && o->has_restart ? o->restart : 50, mem = o && o->has_mem ? o->mem : 50;
     const double itmax = o && o->has_itmax ? o->itmax : -1;
-    snprintf(buf, sizeof buf, "%d|%llu|%p|%p|%p|%p|%p|%.17g|%.17g|%.17g|%d|%.17g|%.17g|%.17g|%s|%s", method,
+    snprintf(buf, sizeof buf, "%d|%llu|%p|%p|%p|%p|%p|%.17g|%.17g|%.17g|%d|%.17g|%.17g|%.17g|%s|%s|%d%d", method,
              (unsigned long long)AC.gen, (const void *)d_b, (const void *)d_xy, (const void *)c.partials.p,
              (const void *)c.counter.p, (const void *)c.red.p, M.nitref, M.force_itref, M.itref_tol,
              (M.residual_update != 0 && M.handle) ? 1 : 0, restart, mem,
              method == CPK_DQGMRES ? itmax : 0.0, getenv("CPK_BATCH") ? getenv("CPK_BATCH") : "",
-             getenv("CPK_NO_GRAPH") ? getenv("CPK_NO_GRAPH") : "");
+             getenv("CPK_NO_GRAPH") ? getenv("CPK_NO_GRAPH") : "", getenv("CPK_NO_PIGGY") ? 1 : 0,
+             getenv("CPK_NO_HALO_MERGE") ? 1 : 0);
     return buf;
 }
 

@@ -203,3 +203,36 @@ def test_dist_more_ranks_than_subtrees(P):
     assert sum(nl for _, _, nl, _, _ in res) == Pd["n"] + Pd["m"]
     xo, so = O.reg_cpkrylov("dqgmres", Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts, perm=perm)
     assert res[0][3] == so["niters"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [2, 3])
+def test_dist_minres_merged_exchanges(P, monkeypatch):
+    """cpminres's scalar exchanges ride in other collectives (alpha's partials in the first
+    separator allgather, beta's in the next Lanczos vector's halo allgather, which the owners'
+    normalisation is then applied to).  Each partial sum is then taken in rank order; the
+    iteration must match the plain-allreduce path to rounding."""
+    import cpkrylov_amd as cpk
+    Pd = F.load("cvxqp1_m")
+    opts = dict(F.EXPROG_OPTS)
+
+    def run():
+        def work(ctx, r):
+            x, stats, flag = cpk.reg_cpkrylov(cpk.cpminres, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts,
+                                              ctx=ctx)
+            return x, stats["residHistory"], stats["niters"]
+        return _run_ranks(P, work)[0]
+
+    variants = {}
+    for name, env in [("merged", {}), ("no_halo_merge", {"CPK_NO_HALO_MERGE": "1"}), ("plain", {"CPK_NO_PIGGY": "1"})]:
+        for k in ("CPK_NO_HALO_MERGE", "CPK_NO_PIGGY"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        variants[name] = run()
+    x0, h0, n0 = variants["plain"]
+    for name in ("merged", "no_halo_merge"):
+        x, h, n = variants[name]
+        assert n == n0, name
+        assert np.max(np.abs(h - h0)) <= 1e-10 * h0[0], name
+        assert np.linalg.norm(x - x0) <= 1e-10 * np.linalg.norm(x0), name
