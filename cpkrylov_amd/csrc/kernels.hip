@@ -377,7 +377,7 @@ constexpr int kTsMaxSteps = 256;              // the step table lives in 4 VGPRs
 constexpr int64_t kTsMaxRows = 1 << 16;
 // meta: a term lane holds its LDS column; a lead lane kTsLead | row | (length - 1) << 16 | flags
 constexpr uint32_t kTsLead = 1u << 31, kTsFirst = 1u << 30, kTsLast = 1u << 29;
-constexpr uint32_t kTsBarrier = 1u << 16;  // step table: waves | barrier after the step | longest chunk << 20
+constexpr uint32_t kTsBarrier = 1u << 16;  // step table: waves | barrier after the step
 
 __global__ __launch_bounds__(256) void tprefix_kernel(
     int nT, const int32_t *__restrict__ tk_ptr, const int32_t *__restrict__ tk_col, const double *__restrict__ tk_val,
@@ -431,23 +431,14 @@ __device__ __forceinline__ void ts_steps(int s0, int s1, const int (&tab)[kTsMax
             const bool lead = m & kTsLead;
             const double g = wt[m & 0xffffu];  // a term's column, or the lead's own row
             double x = lead ? 0.0 : v * g;
-            const int n = lead ? (int)((m >> 16) & 31u) + 1 : 0;
             if (lead && (m & kTsFirst)) acc = g;
-            // the lead subtracts the products of the next n lanes in order, shifted in one lane
-            // at a time (no LDS traffic: 16 waves reading each other's products through LDS
-            // cost more LDS-array cycles than the whole chain)
-            // (past its own chunk a lead subtracts +0.0, which leaves acc unchanged: the select
-            // stays off the chain of subtractions)
-            const int nmax = (e >> 20) & 63;
-            for (int k0 = 1; k0 <= nmax; k0 += 8) {  // the shifts of a group run ahead of its chain
-                double xs[8];
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    x = ts_next_lane(x);
-                    xs[k] = k0 + k <= n ? x : 0.0;
-                }
-#pragma unroll
-                for (int k = 0; k < 8; k++) acc -= xs[k];
+            // each lead subtracts the products of the next nw lanes in order, shifted to it one
+            // lane at a time (no LDS traffic).  Lane 0 leads the wave's first chunk, and every
+            // chunk of a wave is padded to the same length nw, so no lane needs a select.
+            const int nw = (int)((__builtin_amdgcn_readfirstlane(m) >> 16) & 31u) + 1;
+            for (int k = 0; k < nw; k++) {
+                x = ts_next_lane(x);
+                acc -= x;
             }
             if (lead && (m & kTsLast)) wt[m & 0xffffu] = acc;
         }
@@ -466,7 +457,7 @@ __global__ __launch_bounds__(kTsolveThreads) void tsolve_steps_kernel(
     const int tid = threadIdx.x, lane = tid % kWave;
     double *wt = tsw, *rv = wt + ((nT + 2) & ~1);
     uint32_t *rm = reinterpret_cast<uint32_t *>(rv + nrec);
-    int tab[kTsMaxSteps / kWave];  // lane i of tab[k]: step 64k + i (waves | barrier | longest chunk)
+    int tab[kTsMaxSteps / kWave];  // lane i of tab[k]: step 64k + i (waves | barrier)
 #pragma unroll
     for (int k = 0; k < kTsMaxSteps / kWave; k++) {
         const int s = k * kWave + lane;
@@ -522,8 +513,8 @@ struct StepPacker {
     };
     std::vector<std::vector<Lane>> steps;  // kTsolveThreads lanes each
     std::vector<int> used_waves;           // 1 + the last wave holding a chunk
-    std::vector<int> longest;              // the step's longest chunk
     std::vector<bool> barrier;
+    uint32_t one_col = 0;                  // LDS column of the 1.0 slot (nT)
     // terms(t): (value, LDS column, term id) of row t in order
     template <class Terms>
     void level(const std::vector<int32_t> &rows, Terms terms) {
@@ -535,21 +526,24 @@ struct StepPacker {
                 used.push_back({});
                 steps.emplace_back(kTsolveThreads);
                 used_waves.push_back(0);
-                longest.push_back(0);
                 barrier.push_back(false);
             }
         };
+        // a chunk of n terms padded to npad (the wave's chunk length): pad lanes hold 0.0
+        // against the 1.0 slot, so subtracting their products leaves the sum unchanged
         auto put = [&](int32_t t, size_t k, int w, int lane0, const std::vector<std::tuple<double, int32_t, int64_t>> &tv,
-                       size_t j0, size_t n, bool fst, bool lst) {
+                       size_t j0, size_t n, bool fst, bool lst, size_t npad) {
             auto &st = steps[first + k];
             Lane &ld = st[(size_t)(w * kWave + lane0)];
-            ld.m = kTsLead | (uint32_t)t | ((uint32_t)(n - 1) << 16) | (fst ? kTsFirst : 0u) | (lst ? kTsLast : 0u);
-            for (size_t j = 0; j < n; j++) {
+            ld.m = kTsLead | (uint32_t)t | ((uint32_t)(npad - 1) << 16) | (fst ? kTsFirst : 0u) | (lst ? kTsLast : 0u);
+            for (size_t j = 0; j < npad; j++) {
                 Lane &l = st[(size_t)(w * kWave + lane0 + 1) + j];
-                l.v = std::get<0>(tv[j0 + j]), l.m = (uint32_t)std::get<1>(tv[j0 + j]), l.term = std::get<2>(tv[j0 + j]);
+                if (j < n)
+                    l.v = std::get<0>(tv[j0 + j]), l.m = (uint32_t)std::get<1>(tv[j0 + j]), l.term = std::get<2>(tv[j0 + j]);
+                else
+                    l.v = 0.0, l.m = one_col;
             }
             used_waves[first + k] = std::max(used_waves[first + k], w + 1);
-            longest[first + k] = std::max(longest[first + k], (int)n);
         };
         std::vector<std::pair<size_t, int32_t>> single;
         for (int32_t t : rows) {
@@ -571,24 +565,29 @@ struct StepPacker {
                 if (w == kWaves) continue;
                 for (size_t j = 0; j < k; j++) {
                     used[s + j][w] = kWave;
-                    put(t, s + j, w, 0, tv, j * kTsChunk, std::min<size_t>(kTsChunk, n - j * kTsChunk), j == 0, j == k - 1);
+                    const size_t nj = std::min<size_t>(kTsChunk, n - j * kTsChunk);
+                    put(t, s + j, w, 0, tv, j * kTsChunk, nj, j == 0, j == k - 1, nj);
                 }
                 break;
             }
         }
+        // the other rows longest first, a wave at a time: every chunk of a wave is padded to the
+        // wave's first (longest) one, so the wave's chain length is uniform (kernel: no selects)
         std::stable_sort(single.begin(), single.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
-        for (const auto &rn : single) {
-            const auto tv = terms(rn.second);
-            const int need = (int)rn.first + 1;
-            bool placed = false;
-            for (size_t s = 0; !placed; s++) {
-                ensure(s);
-                for (int w = 0; w < kWaves && !placed; w++)
-                    if (kWave - used[s][w] >= need) {
-                        put(rn.second, s, w, used[s][w], tv, 0, rn.first, true, true);
-                        used[s][w] += need;
-                        placed = true;
-                    }
+        size_t i = 0;
+        for (size_t s = 0; i < single.size(); s++) {
+            ensure(s);
+            for (int w = 0; w < kWaves && i < single.size(); w++) {
+                if (used[s][w]) continue;
+                const size_t L = single[i].first;
+                int lane = 0;
+                while (i < single.size() && lane + (int)L + 1 <= kWave) {
+                    const int32_t t = single[i].second;
+                    put(t, s, w, lane, terms(t), 0, single[i].first, true, true, L);
+                    lane += (int)L + 1;
+                    i++;
+                }
+                used[s][w] = kWave;
             }
         }
         barrier.back() = true;
@@ -611,6 +610,7 @@ void dsep_stage(DSep &T, const RankPlan &rp) {
         rest0[t] = e;
     }
     StepPacker P;
+    P.one_col = (uint32_t)nT;
     using TV = std::vector<std::tuple<double, int32_t, int64_t>>;
     auto rows_of = [&](int64_t l, bool bwd) {
         std::vector<int32_t> r;
@@ -645,7 +645,7 @@ void dsep_stage(DSep &T, const RankPlan &rp) {
     std::vector<int32_t> tab;
     std::vector<int64_t> pay_slot(rp.tf_col.size(), -1);
     for (size_t s = 0; s < P.steps.size(); s++) {
-        tab.push_back(P.used_waves[s] | (P.barrier[s] ? (int32_t)kTsBarrier : 0) | (P.longest[s] << 20));
+        tab.push_back(P.used_waves[s] | (P.barrier[s] ? (int32_t)kTsBarrier : 0));
         for (int i = 0; i < P.used_waves[s] * kWave; i++) {
             const auto &l = P.steps[s][(size_t)i];
             if (l.term >= 0) pay_slot[(size_t)l.term] = (int64_t)rv.size();
