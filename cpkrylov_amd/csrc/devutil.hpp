@@ -81,7 +81,7 @@ __device__ __forceinline__ bool arrive_last(unsigned *counter) {
 // Reduce v over the whole grid.  Returns true in every thread of the last-arriving
 // workgroup, where tot[] (thread 0) holds the grid-wide sums in a fixed summation order.
 template <int NV>
-__device__ __forceinline__ bool grid_sum(double (&v)[NV], RedBuf rb, double (&tot)[NV]) {
+__device__ __forceinline__ bool grid_sum(double (&v)[NV], RedBuf rb, double (&tot)[NV], bool *was_last = nullptr) {
     __shared__ int s_last;
     block_sum<NV>(v);
     if (threadIdx.x == 0) {
@@ -91,6 +91,7 @@ __device__ __forceinline__ bool grid_sum(double (&v)[NV], RedBuf rb, double (&to
         s_last = arrive_last(rb.counter);
     }
     __syncthreads();
+    if (was_last) *was_last = s_last != 0;
     if (!s_last) return false;
     double acc[NV];
 #pragma unroll

@@ -165,17 +165,25 @@ void launch_krylov_halo(Ctx &c, const DMat &AC, DState *st, const P &pol) {
     c.comm->allgather(AC.sbuf.p, AC.rbuf.p, (size_t)AC.kstride, c.stream);
 }
 
-// distributed, the Lanczos step's beta partials carried by the next vector's halo exchange:
-// pack the (not yet normalised) vector's halo plus the two partials, allgather, then one block
-// sums the partials in rank order, runs the step's epilogue and normalises the received halo
-// exactly as the owners normalise their rows (MinresUpdate: v = v / beta when beta > 0)
-template <class P>
-__global__ void krylov_pack_red_kernel(P pol, DState *st, const int32_t *__restrict__ idx, int64_t n, int64_t kmax,
-                                       const double *__restrict__ red, double *out) {
-    const double *x = pol.select(st, nullptr);
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = x[idx[i]];
-    if (blockIdx.x == 0 && threadIdx.x < 2) out[kmax + threadIdx.x] = red[threadIdx.x];
+// distributed, the Lanczos step's beta partials carried by the next vector's halo exchange: the
+// step's reduction leaves the two local sums in the payload's spare slots, and its last
+// workgroup recomputes the new vector's halo entries with the step's own formula (the other
+// workgroups' stores are not yet visible across XCDs) into the payload.  After the allgather
+// one block sums the partials in rank order, runs the step's epilogue and normalises the
+// received halo exactly as the owners normalise their rows (MinresUpdate: v = v / beta when
+// beta > 0).
+template <class F>
+__global__ __launch_bounds__(kBlock) void lanczos_step_halo_kernel(int64_t N, F f, RedBuf rb,
+                                                                   const int32_t *__restrict__ idx, int64_t nsend,
+                                                                   double *sbuf) {
+    if (!f.setup()) return;
+    double acc[2] = {0.0, 0.0};
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) f(i, acc);
+    double tot[2];
+    bool last = false;
+    grid_sum<2>(acc, rb, tot, &last);  // rb.defer: the payload's spare slots
+    if (!last) return;
+    for (int64_t j = threadIdx.x; j < nsend; j += kBlock) sbuf[j] = f.value(idx[j]);
 }
 template <class F>
 __global__ void lanczos_fin_halo_kernel(F f, DState *st, double *rbuf, int nranks, int64_t kstride, int64_t kmax) {
@@ -193,14 +201,12 @@ __global__ void lanczos_fin_halo_kernel(F f, DState *st, double *rbuf, int nrank
     for (int64_t i = threadIdx.x; i < (int64_t)nranks * kstride; i += blockDim.x)
         if (i % kstride < kmax) rbuf[i] = rbuf[i] / beta;
 }
-template <class P, class F>
-void launch_lanczos_step_halo(Ctx &c, const DMat &AC, DState *st, int64_t N, const F &f, const P &pol) {
+template <class F>
+void launch_lanczos_step_halo(Ctx &c, const DMat &AC, DState *st, int64_t N, const F &f) {
     c.ensure_partials((size_t)ew_grid(N) * 2);
-    hipLaunchKernelGGL((ewred_kernel<2, F>), dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f,
-                       RedBuf{c.partials.p, c.counter.p, c.red.p});
-    hipLaunchKernelGGL(krylov_pack_red_kernel<P>,
-                       dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((AC.nsend + 255) / 256, 1024))), dim3(256), 0,
-                       c.stream, pol, st, AC.send.p, AC.nsend, AC.kmax, (const double *)c.red.p, AC.sbuf.p);
+    hipLaunchKernelGGL((lanczos_step_halo_kernel<F>), dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f,
+                       RedBuf{c.partials.p, c.counter.p, AC.sbuf.p + AC.kmax}, (const int32_t *)AC.send.p, AC.nsend,
+                       AC.sbuf.p);
     c.comm->allgather(AC.sbuf.p, AC.rbuf.p, (size_t)AC.kstride, c.stream);
     hipLaunchKernelGGL(lanczos_fin_halo_kernel<F>, dim3(1), dim3(256), 0, c.stream, f, st, AC.rbuf.p, c.nranks,
                        AC.kstride, AC.kmax);
@@ -257,15 +263,18 @@ struct LanczosStep {
         vkp1 = VQ + ((kk + skp1) % 3) * N;
         return true;
     }
+    // the new (not yet normalised) Lanczos vector's entry i
+    __device__ double value(int64_t i) const {
+        if (i < n) return vprec[i] - alpha * vk[i] - beta * vkm1[i];
+        const double v = vk[i] - vprec[i];
+        return v - alpha * vk[i] - beta * vkm1[i];
+    }
     __device__ void operator()(int64_t i, double *acc) {
-        double v;
+        const double v = value(i);
         if (i < n) {
-            v = vprec[i] - alpha * vk[i] - beta * vkm1[i];
             acc[0] += ut[i] * v;
             if (KIND == 1) xy[i] = xy[i] + zeta * W[i];  // cpcglanczos.m:607 x = x + zeta*wv
         } else {
-            v = vk[i] - vprec[i];
-            v = v - alpha * vk[i] - beta * vkm1[i];
             acc[1] += ut[i] * v;
             if (KIND == 1) xy[i] = xy[i] - zeta * W[i];  // y = y - zeta*wq
         }
@@ -1440,7 +1449,7 @@ void SolveCore::minres_like(int kind, const double *b, double *xy, cpk_stats *st
             }
             const LanczosStep<0> ls{st, VQ, VPREC, UT, xy, W, n, N, 0, 2, 1};
             if (hmerge)
-                launch_lanczos_step_halo(c, AC, st, N, ls, pol);
+                launch_lanczos_step_halo(c, AC, st, N, ls);
             else
                 launch_ewred<2>(c, N, ls);
             launch_ew(c, N, MinresUpdate{st, VQ, W, xy, n, N});
