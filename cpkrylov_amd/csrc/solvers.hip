@@ -252,10 +252,23 @@ struct LanczosStep {
     double alpha, beta, zeta;
     const double *vk, *vkm1;
     double *vkp1;
+    // distributed cpminres: alpha's partials ride in the separator exchange (sep: its allgathered
+    // payload) and every workgroup sums them itself, in rank order (the α epilogue of
+    // krylov_fin_sep_kernel, without its dispatch); fin commits alpha and the iteration count
+    const double *sep = nullptr;
+    int sep_ranks = 0;
+    int64_t sep_kt = 0, sep_data = 0, kk = 0;
     __device__ bool setup() {
         if (!st->running) return false;
-        const int64_t kk = st->k;
+        kk = st->k;
         alpha = st->alpha;
+        if (sep) {
+            double tot[2] = {0.0, 0.0};
+            for (int r = 0; r < sep_ranks; r++)
+                for (int j = 0; j < 2; j++) tot[j] += sep[(int64_t)r * sep_kt + sep_data + j];
+            alpha = tot[0] + tot[1];
+            kk += 1;
+        }
         beta = st->beta;
         zeta = st->zeta;
         vk = VQ + ((kk + sk) % 3) * N;
@@ -297,6 +310,7 @@ __device__ inline bool check_beta(DState *st, double raw, int64_t kk) {
 // cpminres.m:195-235
 template <>
 __device__ void LanczosStep<0>::fin(const double *tot) {
+    if (sep) st->alpha = alpha, st->k = kk;  // PolLanczosSpmv<0>::fin's part
     const double raw = tot[0] + tot[1];
     const int64_t kk = st->k;
     if (!check_beta(st, raw, kk)) return;
@@ -1442,16 +1456,18 @@ void SolveCore::minres_like(int kind, const double *b, double *xy, cpk_stats *st
             if (piggy) {
                 launch_krylov_spmv(c, AC, st, UT, n, pol, true, hmerge);
                 M.apply(UT, n, VPREC, &st->running, c.red.p);
-                launch_krylov_fin_sep(c, M.sep, st, pol);
+                if (!hmerge) launch_krylov_fin_sep(c, M.sep, st, pol);  // else in the Lanczos step
             } else {
                 launch_krylov_spmv(c, AC, st, UT, n, pol);
                 M.apply(UT, n, VPREC, &st->running);
             }
-            const LanczosStep<0> ls{st, VQ, VPREC, UT, xy, W, n, N, 0, 2, 1};
-            if (hmerge)
+            LanczosStep<0> ls{st, VQ, VPREC, UT, xy, W, n, N, 0, 2, 1};
+            if (hmerge) {
+                ls.sep = M.sep.rbuf.p, ls.sep_ranks = c.nranks, ls.sep_kt = M.sep.kt, ls.sep_data = M.sep.kt_data;
                 launch_lanczos_step_halo(c, AC, st, N, ls);
-            else
+            } else {
                 launch_ewred<2>(c, N, ls);
+            }
             launch_ew(c, N, MinresUpdate{st, VQ, W, xy, n, N});
         };
         if (print) print_hist_lines("%5lld  %9.2e\n");
