@@ -367,8 +367,8 @@ __global__ __launch_bounds__(256) void tsolve_kernel(
 //      the next lanes of the same wave; each lane forms its product, and the lead subtracts the
 //      chunk's products in the row's order.  No index is looked up at run time: a step costs
 //      one record read, one gather, the chain, one store and, at the end of a level, a barrier.
-//      (A level loop that looked its rows up in LDS spent ~1500 cycles per level on dependent
-//      index loads.)
+//      The forward chains (up to 31 dependent subtractions per row, in the factor's order)
+//      bound it: VALU issue, with up to four waves per SIMD in the wide levels.
 // Row sums keep the exported factor's order: bit-identical.
 constexpr int kTsolveThreads = 1024;
 constexpr size_t kTsolveMaxLds = 160 * 1024;  // gfx950: 160 KB of LDS per workgroup
