@@ -1,6 +1,7 @@
 // dist.cpp -- host plan of the distributed solve (see dist.hpp).  Every rank runs the same
 // deterministic analysis and builds the same global plan, so no setup communication is
 // needed beyond the RCCL communicator itself.
+#include <cstdlib>
 #include "dist.hpp"
 
 #include <algorithm>
@@ -20,6 +21,7 @@ TreeSplit split_tree(const Factor &f, int P, double tol, int64_t tmax) {
     ts.node_rank.assign(N, 0);
     if (ts.P == 1 || N == 0) return ts;
     if (tmax < 0) tmax = std::max<int64_t>(256, N / 100);
+    if (const char *e = getenv("CPK_SPLIT_TOL")) tol = atof(e);  // diagnostic
     // work weight of a row: its forward and backward entries plus the row itself
     std::vector<double> W(N, 1.0);
     for (int32_t i : f.Li) W[i] += 1.0;
