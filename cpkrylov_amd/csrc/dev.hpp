@@ -217,7 +217,8 @@ struct DSep {
     DBuf<double> tk_val, tr_val, pre, rec_v;
     DBuf<uint32_t> rec_m;
     int64_t nsf = 0, nsb = 0, nrec = 0;
-    size_t lds = 0;  // LDS bytes of the stepped solve, 0 = not staged (one-pass global kernel)
+    size_t lds = 0;    // LDS bytes of the stepped solve with its records staged, 0 = too large
+    size_t lds_g = 0;  // LDS bytes with the records left in HBM; 0 (or no records): one-pass kernel
 };
 struct RankPlan;
 // Split the forward rows of T and build the steps of the separator level solve.

@@ -447,16 +447,20 @@ __device__ __forceinline__ void ts_steps(int s0, int s1, const int (&tab)[kTsMax
     }
 }
 
+// GREC: the records stay in HBM (a separator whose records do not fit in LDS); each step then
+// waits for its record loads, which is still several times faster than the one-pass kernel
+template <bool GREC>
 __global__ __launch_bounds__(kTsolveThreads) void tsolve_steps_kernel(
     int nT, int nsf, int nsb, int nrec, const double *__restrict__ rec_v, const uint32_t *__restrict__ rec_m,
     const int32_t *__restrict__ steps, const double *__restrict__ pre, const double *__restrict__ DT,
     const int32_t *__restrict__ tdof, int ntdof, double *wT, double *y, int add, const int *run, const int *active) {
-    // LDS: wt[nT + 1, even] | rv[nrec] | rm[nrec]
+    // LDS: wt[nT + 1, even] | rv[nrec] | rm[nrec] (the records: staged unless GREC)
     extern __shared__ __attribute__((aligned(16))) double tsw[];
     if (skip(run, active)) return;
     const int tid = threadIdx.x, lane = tid % kWave;
-    double *wt = tsw, *rv = wt + ((nT + 2) & ~1);
-    uint32_t *rm = reinterpret_cast<uint32_t *>(rv + nrec);
+    double *wt = tsw;
+    const double *rv = GREC ? rec_v : wt + ((nT + 2) & ~1);
+    const uint32_t *rm = GREC ? rec_m : reinterpret_cast<const uint32_t *>(rv + nrec);
     int tab[kTsMaxSteps / kWave];  // lane i of tab[k]: step 64k + i (waves | barrier)
 #pragma unroll
     for (int k = 0; k < kTsMaxSteps / kWave; k++) {
@@ -466,7 +470,9 @@ __global__ __launch_bounds__(kTsolveThreads) void tsolve_steps_kernel(
     {  // stage: every load in flight at once
         constexpr int U = 8;
         for (int i0 = tid; i0 <= nT; i0 += kTsolveThreads) wt[i0] = pre[i0];  // pre[nT] = 1.0
-        for (int i0 = tid; i0 < nrec; i0 += U * kTsolveThreads) {
+        double *srv = wt + ((nT + 2) & ~1);
+        uint32_t *srm = reinterpret_cast<uint32_t *>(srv + nrec);
+        for (int i0 = tid; i0 < (GREC ? 0 : nrec); i0 += U * kTsolveThreads) {
             double a[U];
             uint32_t b[U];
 #pragma unroll
@@ -478,7 +484,7 @@ __global__ __launch_bounds__(kTsolveThreads) void tsolve_steps_kernel(
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const int i = i0 + u * kTsolveThreads;
-                if (i < nrec) rv[i] = a[u], rm[i] = b[u];
+                if (i < nrec) srv[i] = a[u], srm[i] = b[u];
             }
         }
     }
@@ -666,6 +672,7 @@ void dsep_stage(DSep &T, const RankPlan &rp) {
     T.pre.upload(pre);
     const size_t lds = 8 * (size_t)((nT + 2) & ~1) + 12 * (size_t)T.nrec;
     T.lds = lds <= kTsolveMaxLds ? lds : 0;
+    T.lds_g = 8 * (size_t)((nT + 2) & ~1) <= kTsolveMaxLds ? 8 * (size_t)((nT + 2) & ~1) : 0;
 }
 
 // payload: w of this rank's rows that separator rows read, then (rank 0) the T inputs +-x[tdof]
@@ -696,18 +703,29 @@ void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x
 
 void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active) {
     if (S.nT == 0) return;
-    static bool lds_attr = [] {
-        return hipFuncSetAttribute((const void *)tsolve_steps_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    static const bool lds_attr = [] {
+        return hipFuncSetAttribute((const void *)tsolve_steps_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)kTsolveMaxLds) == hipSuccess &&
+               hipFuncSetAttribute((const void *)tsolve_steps_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)kTsolveMaxLds) == hipSuccess;
     }();
-    if (S.lds && (S.lds <= 64 * 1024 || lds_attr) && !getenv("CPK_TSOLVE_ONEPASS")) {
+    auto fits = [&](size_t b) { return b && (b <= 64 * 1024 || lds_attr); };
+    const bool grec = getenv("CPK_TSOLVE_GLOBAL") != nullptr || !fits(S.lds);  // diagnostic override
+    const size_t lds = grec ? S.lds_g : S.lds;
+    if (S.nrec > 0 && fits(lds) && !getenv("CPK_TSOLVE_ONEPASS")) {
         hipLaunchKernelGGL(tprefix_kernel, dim3((unsigned)((S.nT + 3) / 4)), dim3(256), 0, c.stream, (int)S.nT,
                            S.tk_ptr.p, S.tk_col.p, S.tk_val.p, S.tr_ptr.p, S.tr_col.p, S.tr_val.p, S.tr_slot.p,
                            S.tf_src.p, S.rbuf.p, S.pre.p, S.rec_v.p, run, active);
-        hipLaunchKernelGGL(tsolve_steps_kernel, dim3(1), dim3(kTsolveThreads), S.lds, c.stream, (int)S.nT,
-                           (int)S.nsf, (int)S.nsb, (int)S.nrec, (const double *)S.rec_v.p,
-                           (const uint32_t *)S.rec_m.p, S.steps.p, (const double *)S.pre.p, (const double *)S.DT.p,
-                           S.tdof.p, (int)S.ntdof, wT, y, add ? 1 : 0, run, active);
+        if (grec)
+            hipLaunchKernelGGL(tsolve_steps_kernel<true>, dim3(1), dim3(kTsolveThreads), lds, c.stream, (int)S.nT,
+                               (int)S.nsf, (int)S.nsb, (int)S.nrec, (const double *)S.rec_v.p,
+                               (const uint32_t *)S.rec_m.p, S.steps.p, (const double *)S.pre.p, (const double *)S.DT.p,
+                               S.tdof.p, (int)S.ntdof, wT, y, add ? 1 : 0, run, active);
+        else
+            hipLaunchKernelGGL(tsolve_steps_kernel<false>, dim3(1), dim3(kTsolveThreads), lds, c.stream, (int)S.nT,
+                               (int)S.nsf, (int)S.nsb, (int)S.nrec, (const double *)S.rec_v.p,
+                               (const uint32_t *)S.rec_m.p, S.steps.p, (const double *)S.pre.p, (const double *)S.DT.p,
+                               S.tdof.p, (int)S.ntdof, wT, y, add ? 1 : 0, run, active);
         CPK_HIP(hipGetLastError());
         return;
     }

@@ -236,3 +236,28 @@ def test_dist_minres_merged_exchanges(P, monkeypatch):
         assert n == n0, name
         assert np.max(np.abs(h - h0)) <= 1e-10 * h0[0], name
         assert np.linalg.norm(x - x0) <= 1e-10 * np.linalg.norm(x0), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["CPK_TSOLVE_GLOBAL", "CPK_TSOLVE_ONEPASS"])
+@pytest.mark.parametrize("P", [2, 4])
+def test_dist_apply_separator_fallbacks_bitexact(P, path, monkeypatch):
+    """The separator solve's fallbacks (records left in HBM for a separator too large for LDS;
+    the one-pass global kernel) give the same bits as the staged solve and the oracle."""
+    import cpkrylov_amd as cpk
+    S = _system("synthetic20k")
+    z = np.random.default_rng(7).standard_normal(S["n"] + S["m"])
+    monkeypatch.setenv(path, "1")
+
+    def work(ctx, r):
+        M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+        M.nitref, M.force_itref = 1, True
+        return M * z, M.export_factors() if r == 0 else None
+
+    res = _run_ranks(P, work)
+    L, D, perm = res[0][1]
+    Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=(L, D, perm))
+    Mo.set(nitref=1.0, force_itref=1.0)
+    yo = Mo @ z
+    for y, _ in res:
+        assert np.array_equal(y, yo), np.max(np.abs(y - yo))
