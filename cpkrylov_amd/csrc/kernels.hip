@@ -379,40 +379,39 @@ constexpr int64_t kTsMaxRows = 1 << 16;
 constexpr uint32_t kTsLead = 1u << 31, kTsFirst = 1u << 30, kTsLast = 1u << 29;
 constexpr uint32_t kTsBarrier = 1u << 16;  // step table: waves | barrier after the step
 
-__global__ __launch_bounds__(256) void tprefix_kernel(
-    int nT, const int32_t *__restrict__ tk_ptr, const int32_t *__restrict__ tk_col, const double *__restrict__ tk_val,
-    const int32_t *__restrict__ tr_ptr, const int32_t *__restrict__ tr_col, const double *__restrict__ tr_val,
-    const int32_t *__restrict__ tr_slot, const int32_t *__restrict__ tf_src, const double *__restrict__ rbuf,
-    double *__restrict__ pre, double *__restrict__ rec_v, const int *run, const int *active) {
-    __shared__ double prod[4][kWave];
-    if (skip(run, active)) return;
-    const int wv = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-    const int t = blockIdx.x * 4 + wv;
-    if (t >= nT) return;
-    double acc = rbuf[tf_src[t]];
-    const int k1 = tk_ptr[t + 1];
-    for (int e = tk_ptr[t]; e < k1; e += kWave) {
-        const int q = e + lane;
-        double p = 0.0;
-        if (q < k1) p = tk_val[q] * rbuf[tk_col[q]];
-        prod[wv][lane] = p;
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {
-            const int n = min(kWave, k1 - e);
-            for (int u = 0; u < n; u++) acc -= prod[wv][u];
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-    if (lane == 0) pre[t] = acc;
-    for (int q = tr_ptr[t] + lane; q < tr_ptr[t + 1]; q += kWave) rec_v[tr_slot[q]] = tr_val[q] * rbuf[tr_col[q]];
-}
-
 // x of lane i + 1 (wave shift; the last lane gets 0)
 __device__ __forceinline__ double ts_next_lane(double x) {
     const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x130, 0xf, 0xf, true);  // wave_shl:1
     const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x130, 0xf, 0xf, true);
     return __hiloint2double(hi, lo);
 }
+
+__global__ __launch_bounds__(256) void tprefix_kernel(
+    int nT, const int32_t *__restrict__ tk_ptr, const int32_t *__restrict__ tk_col, const double *__restrict__ tk_val,
+    const int32_t *__restrict__ tr_ptr, const int32_t *__restrict__ tr_col, const double *__restrict__ tr_val,
+    const int32_t *__restrict__ tr_slot, const int32_t *__restrict__ tf_src, const double *__restrict__ rbuf,
+    double *__restrict__ pre, double *__restrict__ rec_v, const int *run, const int *active) {
+    if (skip(run, active)) return;
+    const int wv = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    const int t = blockIdx.x * 4 + wv;
+    if (t >= nT) return;  // whole waves: the shifts below need every lane
+    double acc = rbuf[tf_src[t]];
+    const int k1 = tk_ptr[t + 1];
+    for (int e = tk_ptr[t]; e < k1; e += kWave) {
+        const int q = e + lane;
+        double x = q < k1 ? tk_val[q] * rbuf[tk_col[q]] : 0.0;
+        // lane 0 subtracts the wave's products in order, shifted to it one lane at a time
+        const int n = min(kWave, k1 - e);
+        acc -= x;
+        for (int u = 1; u < n; u++) {
+            x = ts_next_lane(x);
+            acc -= x;
+        }
+    }
+    if (lane == 0) pre[t] = acc;
+    for (int q = tr_ptr[t] + lane; q < tr_ptr[t + 1]; q += kWave) rec_v[tr_slot[q]] = tr_val[q] * rbuf[tr_col[q]];
+}
+
 
 // steps [s0, s1); woff: the first record of step s0 (in waves) on entry, of step s1 on exit
 __device__ __forceinline__ void ts_steps(int s0, int s1, const int (&tab)[kTsMaxSteps / kWave], int &woff,
