@@ -10,8 +10,8 @@ Metric (BASELINE.json): "Krylov iters/sec + SpMV GB/s (% HBM peak), cpminres 10M
   value     Krylov iterations completed by all ranks / max over ranks of the timed wall time.
   roofline  the saddle-point SpMV r = x - Kp*y (the refinement residual inside every M*z):
             algorithmic bytes per launch / its HIP-event-timed average duration, vs 8 TB/s.
-  cpu_baseline  the C restatement (oracle/) of the same solve on one host core, timed on a
-            bounded sample of the same workload.
+  cpu_baseline  the C restatement (oracle/) of the same solve on the host, timed on a
+            bounded sample of the same workload: one core, and OpenMP on the cores the box grants.
 Multi-GPU (torchrun, one process per GPU): ONE solve of the same S10 system row-block
 partitioned over the ranks (strong scaling): RCCL allreduce for the inner
 products, allgathered halos for the SpMVs and the separator exchange of the distributed LDL'
@@ -107,8 +107,12 @@ def main():
     # N > 1 (or --dist): one distributed solve over all ranks (strong scaling), RCCL collectives
     # and halo exchanges inside the solver; every rank holds its row block
     distributed = world > 1 or args.dist
-    dist_error = None
+    dev = torch.device("cuda", local)
     if distributed:
+        # every rank must finish its setup before any rank enters a collective: a rank that fails
+        # (e.g. out of memory) would otherwise leave the others waiting in RCCL.  No fallback to
+        # replicas: a failed distributed setup ends the job with a non-zero exit on every rank.
+        err = None
         try:
             uid = [cpk.get_unique_id() if rank == 0 else None]
             if dist:
@@ -117,11 +121,18 @@ def main():
                 ctx = cpk.Context(device=local, rank=rank, nranks=world, unique_id=uid[0])
             A, B, Cm, G = (cpk.Matrix(S[k], ctx) for k in ("Q", "B", "C", "G"))
             M = cpk.opLDL2(G, B, -S["C"], ctx=ctx)
-        except cpk.CpkError as e:  # reported in the line; the run falls back to replicas
-            dist_error = str(e)
-            print(f"bench: distributed setup failed ({e}); running independent replicas", file=sys.stderr)
-            distributed = False
-    if not distributed:
+        except Exception as e:  # noqa: BLE001  (reported, then every rank exits)
+            err = f"{type(e).__name__}: {e}"
+        ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
+        if dist:
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            print(f"bench: distributed setup failed on rank {rank}: {err or 'another rank failed'}",
+                  file=sys.stderr, flush=True)
+            if dist:
+                dist.destroy_process_group()
+            sys.exit(3)
+    else:
         ctx = cpk.Context(device=local)
         A, B, Cm, G = (cpk.Matrix(S[k], ctx) for k in ("Q", "B", "C", "G"))
         M = cpk.opLDL2(G, B, -S["C"], ctx=ctx)
@@ -129,7 +140,6 @@ def main():
     M.residual_update, M.force_itref = EXPROG_OPTS["residual_update"], EXPROG_OPTS["force_itref"]
     dofs, n_loc = M.local_dofs()
     N_loc = len(dofs)
-    dev = torch.device("cuda", local)
     b = torch.from_numpy(np.ascontiguousarray(S["rhs"][dofs])).to(dev)
     b1 = torch.empty(max(n_loc, 1), dtype=torch.float64, device=dev)
     xy0 = torch.empty(max(N_loc, 1), dtype=torch.float64, device=dev)
@@ -175,9 +185,8 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    # one solve over all ranks: its iterations are the job's iterations (strong scaling);
-    # replicas (fallback) each solve the whole system
-    total_iters = float(iters) * (1 if distributed else world)
+    # one solve over all ranks: its iterations are the job's iterations (strong scaling)
+    total_iters = float(iters)
 
     prof = _lib.Profile()
     _lib.check(_lib.lib.cpk_profile_kernels(ctx.h, A.h, Cm.h, M.h, args.profile_reps, C.byref(prof)))
@@ -210,7 +219,7 @@ def main():
                        "Krylov iters/sec, cpdqgmres(40) 50M-dof nonsymmetric 3x3-block"),
             "value": round(value, 2), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "strong" if distributed or world == 1 else "weak", "vs_baseline": None, "dtype": "f64",
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": (f"S10 synthetic symmetric saddle-point system, cp{args.method} to convergence "
                                     "(cpk_exprog1 options), step = one method call" if args.config == "s10" else
@@ -219,7 +228,7 @@ def main():
                                     "(cpk_exprog1 tolerances)"),
                        "N": N, "n": n, "m": m, "nnz_kp": M.info["nnz_kp"], "nnz_l": M.info["nnz_l"],
                        "sweep_launches": M.info["nrounds"], "elim_tree_depth": M.info["depth"],
-                       "parallelism": f"rowblock{world}" if distributed else ("single" if world == 1 else f"replicas{world}"),
+                       "parallelism": f"rowblock{world}" if distributed else "single",
                        "seed": S["seed"],
                        "rows_local_rank0": N_loc},
             "iters_per_step": round(float(iters) / args.steps, 2), "solved": solved,
@@ -232,7 +241,6 @@ def main():
             "setup_s": round(setup_s, 2),
             "cpu_baseline": cpu,
             "pmc": pmc,
-            "dist_error": dist_error,
             "parity": parity,
         }
         print(json.dumps(line), flush=True)
@@ -240,31 +248,92 @@ def main():
         dist.destroy_process_group()
 
 
+def host_cpu():
+    """Model name (lscpu / /proc/cpuinfo), logical CPUs of the machine (nproc --all) and of this
+    process's affinity mask, and the thread budget the box grants (OMP_NUM_THREADS)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = max(1, min(aff or 1, int(omp) if omp and omp.isdigit() else (aff or 1)))
+    return {"model": model, "nproc_all": os.cpu_count(), "affinity": aff, "omp_num_threads": omp,
+            "threads": threads}
+
+
 def cpu_baseline(S, b1, M_gpu, args, hist_gpu, niters_gpu):
-    """The oracle's cpminres on the same system and shifted rhs, one host core."""
+    """The oracle's solve of the same system and shifted rhs on the host:
+    one core (the serial restatement, MATLAB's sparse kernels being single-threaded) and OpenMP
+    on the cores this process may use.  Both legs run the same pivot order as the GPU and the
+    reference's work, including the dead residual-update SpMVs.  The serial leg, run to
+    convergence, is also the parity reference of the GPU's histories; the OpenMP leg and two
+    1e-15-perturbed rhs give the problem's own sensitivity band (tests/sensitivity.py)."""
     from oracle import oracle as O
+    host = host_cpu()
     L, D, perm = M_gpu.export_factors()
+    t = time.perf_counter()
     Mo = O.LDL2(S["G"], S["B"], -S["C"], perm=perm)  # the oracle's own factorization, same pivot order
+    t_factor = time.perf_counter() - t
     Mo.set(nitref=args.opts["nitref"], itref_tol=args.opts["itref_tol"],
            force_itref=1.0, residual_update=1.0)
-    # probe two iterations to size a 10-30 s sample
-    t = time.perf_counter()
-    O.method(args.method, b1, S["Q"], S["C"], Mo, dict(args.opts, itmax=2))
-    per_iter = (time.perf_counter() - t) / 3.0  # init M-apply + 2 iterations
-    itmax = int(max(2, min(args.opts["itmax"], args.cpu_seconds / max(per_iter, 1e-9))))
-    t = time.perf_counter()
-    x, y, st = O.method(args.method, b1, S["Q"], S["C"], Mo, dict(args.opts, itmax=itmax))
-    dt = time.perf_counter() - t
-    it = int(st["niters"])
-    cpu = {"value": round(it / dt, 4), "unit": "iters/s", "cores": 1, "kind": "port",
-           "sample": f"oracle cp{args.method} on {args.config.upper()} (same b1, same pivot order), {it} iterations "
-                     f"(itmax {itmax}, solved {bool(st['solved'])}), {dt:.1f} s, gcc -O2 single thread"}
+
+    def leg(threads, budget_s, opts_extra=None, rhs=None):
+        got = O.set_threads(threads)
+        try:
+            rhs_ = b1 if rhs is None else rhs
+            t = time.perf_counter()  # probe two iterations to size a bounded sample
+            O.method(args.method, rhs_, S["Q"], S["C"], Mo, dict(args.opts, itmax=2))
+            per_iter = (time.perf_counter() - t) / 3.0  # init M-apply + 2 iterations
+            itmax = int(max(2, min(args.opts["itmax"], budget_s / max(per_iter, 1e-9))))
+            if opts_extra is not None:
+                itmax = int(args.opts["itmax"])
+            t = time.perf_counter()
+            x, y, st = O.method(args.method, rhs_, S["Q"], S["C"], Mo, dict(args.opts, itmax=itmax))
+            return got, itmax, time.perf_counter() - t, x, st
+        finally:
+            O.set_threads(1)
+
+    half = args.cpu_seconds / 2
+    _, it1max, dt1, x1, st1 = leg(1, half)
+    T, itTmax, dtT, xT, stT = leg(host["threads"], half)
+    it1, itT = int(st1["niters"]), int(stT["niters"])
+    cpu = {"value": round(it1 / dt1, 4), "unit": "iters/s", "cores": 1, "kind": "port",
+           "sample": f"oracle cp{args.method} on {args.config.upper()} (same b1, same pivot order, dead "
+                     f"residual-update SpMVs included), {it1} iterations (itmax {it1max}, solved "
+                     f"{bool(st1['solved'])}) in {dt1:.1f} s, gcc -O3 -ffp-contract=off, one thread",
+           "omp": {"value": round(itT / dtT, 4), "unit": "iters/s", "cores": T,
+                   "sample": f"same solve, OpenMP on {T} threads (row-parallel SpMV and updates, "
+                             f"level-scheduled sweeps), {itT} iterations (itmax {itTmax}) in {dtT:.1f} s"},
+           "host": host, "oracle_factor_s": round(t_factor, 2)}
     parity = None
-    if st["solved"]:
-        h = st["residHistory"]
-        parity = {"niters_gpu": niters_gpu, "niters_oracle": it, "niters_equal": niters_gpu == it,
-                  "max_hist_dev_over_h0": float(np.max(np.abs(h - hist_gpu[:len(h)])) / h[0])
-                  if len(h) == len(hist_gpu) else None}
+    if st1["solved"]:
+        h = st1["residHistory"]
+        h0 = h[0]
+        dev = float(np.max(np.abs(h - hist_gpu[:len(h)])) / h0) if len(h) == len(hist_gpu) else None
+        # sensitivity band: the OpenMP leg (different dot rounding) and two perturbed rhs
+        band = 0.0
+        if stT["solved"] and len(stT["residHistory"]) == len(h):
+            band = float(np.max(np.abs(stT["residHistory"] - h)) / h0)
+        rng = np.random.default_rng(12345)
+        for _ in range(2):
+            bp = b1 * (1 + 1e-15 * rng.standard_normal(b1.shape[0]))
+            _, _, _, _, sp_ = leg(host["threads"], 0, opts_extra={}, rhs=bp)
+            hp = sp_["residHistory"]
+            L_ = min(len(hp), len(h))
+            band = max(band, float(np.max(np.abs(hp[:L_] - h[:L_])) / h0))
+        tol = max(1e-8, 10 * band)
+        parity = {"niters_gpu": niters_gpu, "niters_oracle": it1, "niters_equal": niters_gpu == it1,
+                  "max_hist_dev_over_h0": dev, "band_over_h0": band, "tolerance_over_h0": tol,
+                  "pass": bool(niters_gpu == it1 and dev is not None and dev <= tol),
+                  "method": "serial oracle run to convergence = reference; band = max history deviation of "
+                            "the OpenMP leg and of two rhs perturbed by 1e-15 relative; tolerance = "
+                            "max(1e-8, 10 x band) (tests/test_gpu_parity.py)"}
     return cpu, parity
 
 

@@ -97,7 +97,10 @@ def get_unique_id():
 class Matrix:
     """A sparse matrix handle (host copy + lazily uploaded HBM copy)."""
 
-    def __init__(self, M, ctx=None, host_only=False):
+    def __init__(self, M, ctx=None, host_only=False, csc=False):
+        """csc=True hands the matrix over as MATLAB stores it (mxGetJc / mxGetIr / mxGetPr:
+        0-based, size_t column pointers and row indices), through cpk_mat_create_csc -- the
+        entry the MEX gateway uses (matlab/cpk_mex.c)."""
         if isinstance(M, Matrix):
             raise TypeError("already a Matrix")
         if not sp.issparse(M):
@@ -105,18 +108,29 @@ class Matrix:
             if M.ndim != 2:
                 raise CpkError(_lib.CPK_ERR_ARGS, "matrix expected")
             M = sp.csr_matrix(M)
-        M = sp.csr_matrix(M, dtype=np.float64)
-        M.sum_duplicates()
-        M.sort_indices()
-        self.shape = M.shape
-        self._ptr = np.ascontiguousarray(M.indptr, dtype=np.int64)
-        self._ind = np.ascontiguousarray(M.indices, dtype=np.int32)
-        self._val = np.ascontiguousarray(M.data, dtype=np.float64)
         self.ctx = None if host_only else (ctx or default_context())
         h = C.c_void_p()
-        check(lib.cpk_mat_create_csr(self.ctx.h if self.ctx else None, M.shape[0], M.shape[1],
-                                     self._ptr.ctypes.data_as(_P(C.c_int64)),
-                                     self._ind.ctypes.data_as(_P(C.c_int32)), _dptr(self._val), C.byref(h)))
+        cx = self.ctx.h if self.ctx else None
+        if csc:
+            M = sp.csc_matrix(M, dtype=np.float64)
+            M.sum_duplicates()
+            M.sort_indices()
+            self.shape = M.shape
+            self._ptr = np.ascontiguousarray(M.indptr, dtype=np.uintp)
+            self._ind = np.ascontiguousarray(M.indices, dtype=np.uintp)
+            self._val = np.ascontiguousarray(M.data, dtype=np.float64)
+            check(lib.cpk_mat_create_csc(cx, M.shape[0], M.shape[1], self._ptr.ctypes.data_as(_P(C.c_size_t)),
+                                         self._ind.ctypes.data_as(_P(C.c_size_t)), _dptr(self._val), C.byref(h)))
+        else:
+            M = sp.csr_matrix(M, dtype=np.float64)
+            M.sum_duplicates()
+            M.sort_indices()
+            self.shape = M.shape
+            self._ptr = np.ascontiguousarray(M.indptr, dtype=np.int64)
+            self._ind = np.ascontiguousarray(M.indices, dtype=np.int32)
+            self._val = np.ascontiguousarray(M.data, dtype=np.float64)
+            check(lib.cpk_mat_create_csr(cx, M.shape[0], M.shape[1], self._ptr.ctypes.data_as(_P(C.c_int64)),
+                                         self._ind.ctypes.data_as(_P(C.c_int32)), _dptr(self._val), C.byref(h)))
         self.h = h
 
     def __matmul__(self, x):
@@ -252,7 +266,7 @@ class opLDL2:
 
 def analyze(A, B, Cm):
     """Host-only half of opLDL2(A, B, C) (no GPU): ordering, LDL', sweep schedule."""
-    mats = [Matrix(M, host_only=True) for M in (A, B, Cm)]
+    mats = [M if isinstance(M, Matrix) else Matrix(M, host_only=True) for M in (A, B, Cm)]
     h = C.c_void_p()
     check(lib.cpk_analyze(mats[0].h, mats[1].h, mats[2].h, C.byref(h)))
     try:

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -44,25 +45,25 @@ struct cpk_mat_s {
         }
         return *d;
     }
-    // distributed rows, keyed by the preconditioner whose dof map they follow
-    std::map<std::pair<uint64_t, const void *>, std::unique_ptr<DMat>> dac;
-    std::map<const void *, std::unique_ptr<DMat>> dax, dbtx;
-    const DMat &krylov_op(cpk_mat_s *C, const Precond &M) {
+    // distributed rows follow the preconditioner's dof map, so they are
+    // cached in the Precond itself (Precond::dist_ops), keyed by the matrices' generations: they
+    // die with the preconditioner, and a new preconditioner never sees an old one's rows
+    const DMat &krylov_op(cpk_mat_s *C, Precond &M) {
         if (!M.dist) return blkdiag_with(C);
-        auto key = std::make_pair(C->gen, (const void *)&M);
-        auto it = dac.find(key);
-        if (it == dac.end()) {
+        auto &slot = M.dist_ops[{'K', gen, C->gen}];
+        if (!slot) {
             auto m = std::make_unique<DMat>();
             make_dist_dmat(dist_csr(blkdiag(h, C->h), *M.dofmap, ctx->c.rank, false, kKrylovSpare), ctx->c.nranks,
                            *m);
-            it = dac.emplace(key, std::move(m)).first;
+            slot = std::move(m);
         }
-        return *it->second;
+        return *slot;
     }
     // shift rows of a distributed preconditioner: A*xy0(1:n) and B'*xy0(n+1:N), x-part rows
-    std::pair<const DMat *, const DMat *> shift_ops(const Precond &M) {
-        auto it = dax.find(&M);
-        if (it == dax.end()) {
+    std::pair<const DMat *, const DMat *> shift_ops(Precond &M) {
+        auto &sa = M.dist_ops[{'A', gen, 0}];
+        auto &sb = M.dist_ops[{'B', gen, 0}];
+        if (!sa || !sb) {
             const int64_t n = M.gn, N = M.gN;
             HCsr a = h, bt;
             a.ncols = N;
@@ -76,10 +77,9 @@ struct cpk_mat_s {
             auto ma = std::make_unique<DMat>(), mb = std::make_unique<DMat>();
             make_dist_dmat(dist_csr(a, *M.dofmap, ctx->c.rank, true), ctx->c.nranks, *ma);
             make_dist_dmat(dist_csr(bt, *M.dofmap, ctx->c.rank, true), ctx->c.nranks, *mb);
-            it = dax.emplace(&M, std::move(ma)).first;
-            dbtx[&M] = std::move(mb);
+            sa = std::move(ma), sb = std::move(mb);
         }
-        return {it->second.get(), dbtx[&M].get()};
+        return {sa.get(), sb.get()};
     }
     const DMat &blkdiag_with(cpk_mat_s *C) {
         if (!ctx) throw Error(CPK_ERR_ARGS, "host-only matrix (created with ctx == NULL) used on the device");
@@ -111,7 +111,7 @@ struct cpk_pc_s {
 };
 
 static thread_local std::string g_err;
-static uint64_t g_gen = 1;
+static std::atomic<uint64_t> g_gen{1};
 
 #define API_BEGIN try {
 #define API_END                                                  \
@@ -426,7 +426,7 @@ int cpk_pc_export(cpk_pc M, int64_t *Lcolptr, int32_t *Lrowind, double *Lval, do
     API_END
 }
 
-static void check_method_dims(cpk_mat A, cpk_mat C, cpk_pc M) {
+static void check_method_dims(cpk_mat A, cpk_mat C, const cpk_pc_s *M) {
     need(A && C && M, "NULL argument");
     if (A->h.nrows != A->h.ncols || C->h.nrows != C->h.ncols) throw Error(CPK_ERR_DIM, "A and C must be square");
     if (A->h.nrows != M->p->gn || C->h.nrows != M->p->gm) throw Error(CPK_ERR_DIM, "A, C and M dimensions disagree");
@@ -633,7 +633,7 @@ int cpk_analysis_plan(cpk_analysis a, cpk_mat A, cpk_mat C, int nranks, int rank
          "A and C must match the analysis' n and m");
     auto p = std::make_unique<cpk_plan_s>();
     p->n = an.n, p->m = an.m;
-    p->ts = split_tree(an.F0, nranks);
+    p->ts = split_tree(an.F0, nranks, split_tol_option());
     p->dm = make_dofmap(an.F0, p->ts, an.n);
     p->rp = make_rank_plan(an.F0, p->ts, p->dm, rank);
     p->kp = dist_csr(an.Kp, p->dm, rank, false);

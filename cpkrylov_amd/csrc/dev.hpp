@@ -4,7 +4,9 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
+#include <map>
 #include <memory>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -251,6 +253,9 @@ struct Precond {
     double ptime = 0;
     // cached solvers (workspace + captured iteration graphs), keyed; see solvers.hip
     std::vector<std::pair<std::string, std::shared_ptr<void>>> solvers;
+    // distributed rows of the Krylov operator and the shift products, which follow this
+    // preconditioner's dof map (capi.cpp): keyed by (kind, matrix generation(s)); they die with it
+    std::map<std::tuple<char, uint64_t, uint64_t>, std::unique_ptr<DMat>> dist_ops;
     // y = M*x  (opLDL2.multiply); all pointers on the device, enqueued on ctx->stream
     // piggy_src (distributed only, piggyback_ok()): kSepPiggy device values appended to the first
     // separator exchange's payload, e.g. a solver's deferred inner-product partials; after the

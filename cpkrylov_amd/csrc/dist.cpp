@@ -14,6 +14,16 @@
 
 namespace cpk {
 
+double split_tol_option() {
+    const char *e = getenv("CPK_SPLIT_TOL");
+    if (!e) return kSplitTol;
+    char *end = nullptr;
+    const double v = strtod(e, &end);
+    if (end == e || *end != '\0' || !std::isfinite(v) || !(v > 0 && v < 1))
+        throw Error(CPK_ERR_ARGS, std::string("CPK_SPLIT_TOL must be a number in (0, 1), got '") + e + "'");
+    return v;
+}
+
 TreeSplit split_tree(const Factor &f, int P, double tol, int64_t tmax) {
     const int64_t N = f.N;
     TreeSplit ts;
@@ -21,7 +31,7 @@ TreeSplit split_tree(const Factor &f, int P, double tol, int64_t tmax) {
     ts.node_rank.assign(N, 0);
     if (ts.P == 1 || N == 0) return ts;
     if (tmax < 0) tmax = std::max<int64_t>(256, N / 100);
-    if (const char *e = getenv("CPK_SPLIT_TOL")) tol = atof(e);  // diagnostic
+    if (!(tol > 0 && tol < 1)) throw Error(CPK_ERR_ARGS, "split_tree: load tolerance must lie in (0, 1)");
     // work weight of a row: its forward and backward entries plus the row itself
     std::vector<double> W(N, 1.0);
     for (int32_t i : f.Li) W[i] += 1.0;

@@ -24,7 +24,12 @@ struct TreeSplit {
     std::vector<int32_t> T;          // separator rows, ascending
 };
 // tol: accepted load imbalance (max/avg - 1); T grows until it is met or T reaches tmax rows.
-TreeSplit split_tree(const Factor &f, int P, double tol = 0.03, int64_t tmax = -1);
+// Every rank must pass the same tol (each builds the same global plan independently).
+constexpr double kSplitTol = 0.03;
+TreeSplit split_tree(const Factor &f, int P, double tol = kSplitTol, int64_t tmax = -1);
+// the diagnostic override CPK_SPLIT_TOL, validated: a finite number in
+// (0, 1), else CPK_ERR_ARGS; kSplitTol when unset.  Read by the callers of split_tree.
+double split_tol_option();
 
 // Dof ownership.  Rank r's local vectors are [owned x-part dofs ascending; owned y-part dofs
 // ascending], so the solvers' [x; y] index ranges keep their meaning locally.

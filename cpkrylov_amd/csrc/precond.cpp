@@ -88,7 +88,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an) {
     pc->dist = true;
     pc->gn = an.n, pc->gm = an.m, pc->gN = an.N;
     pc->ordering = an.ordering;
-    const TreeSplit ts = split_tree(an.F0, c.nranks);
+    const TreeSplit ts = split_tree(an.F0, c.nranks, split_tol_option());
     auto dm = std::make_shared<DofMap>(make_dofmap(an.F0, ts, an.n));
     RankPlan rp = make_rank_plan(an.F0, ts, *dm, c.rank);
     pc->n = dm->n_loc[c.rank], pc->m = dm->m_loc[c.rank], pc->N = pc->n + pc->m;

@@ -40,7 +40,7 @@ struct PolStart {  // starts an iteration: decides `running` from `stop`
     }
 };
 
-// cpminres.m:187-189 / cpcglanczos.m:601-606 / cpsymmlq.m:231-268 : u = A*vk; t = C*qk; alpha
+// cpminres.m:187-189 / cpcglanczos.m:232-234 / cpsymmlq.m:231-268 : u = A*vk; t = C*qk; alpha
 template <int KIND>
 struct PolLanczosSpmv {
     const double *VQ;
@@ -79,7 +79,7 @@ struct PolLanczosSpmv {
     }
 };
 
-// cpcg.m:405-408 : Ap = A*p; pAp; Cq = C*q; qCq; alpha = residNorm2/(pAp+qCq)
+// cpcg.m:151-154 : Ap = A*p; pAp; Cq = C*q; qCq; alpha = residNorm2/(pAp+qCq)
 struct PolCgSpmv {
     const double *PQ;
     __device__ bool skip(DState *st) { return PolStart::start(st); }
@@ -286,7 +286,7 @@ struct LanczosStep {
         const double v = value(i);
         if (i < n) {
             acc[0] += ut[i] * v;
-            if (KIND == 1) xy[i] = xy[i] + zeta * W[i];  // cpcglanczos.m:607 x = x + zeta*wv
+            if (KIND == 1) xy[i] = xy[i] + zeta * W[i];  // cpcglanczos.m:238 x = x + zeta*wv
         } else {
             acc[1] += ut[i] * v;
             if (KIND == 1) xy[i] = xy[i] - zeta * W[i];  // y = y - zeta*wq
@@ -332,7 +332,7 @@ __device__ void LanczosStep<0>::fin(const double *tot) {
     st->stop = !(st->residNorm > st->stopTol && kk < st->itmax);
 }
 
-// cpcglanczos.m:616-664
+// cpcglanczos.m:247-295
 template <>
 __device__ void LanczosStep<1>::fin(const double *tot) {
     const double raw = tot[0] + tot[1];
@@ -433,7 +433,7 @@ struct InitLanczos {
             st->stopTol = st->atol + st->rtol * st->residNorm;
             push(st->hist, st->nh, st->hcap, st->residNorm);
             st->stop = !(st->residNorm > st->stopTol && 0 < st->itmax);
-        } else if (KIND == 1) {  // cpcglanczos.m:534-567
+        } else if (KIND == 1) {  // cpcglanczos.m:154-198
             st->beta = b1;
             st->beta1 = b1;
             st->residNorm = b1;
@@ -506,7 +506,7 @@ struct MinresUpdate {
     }
 };
 
-// cpcglanczos.m:626-637 : normalise vkp1; wv = vkp1 - low*wv
+// cpcglanczos.m:256-268 : normalise vkp1; wv = vkp1 - low*wv
 struct CglUpdate {
     DState *st;
     double *VQ, *W;
@@ -658,7 +658,7 @@ struct CgInit0 {  // g = -b ; w = 0 ; x = 0 ; a = 0
         XA[i] = 0.0;
     }
 };
-struct CgInit1 {  // p = -r; q = -u; residNorm2 = g'*r   (cpcg.m:380-387)
+struct CgInit1 {  // p = -r; q = -u; residNorm2 = g'*r   (cpcg.m:126-133)
     DState *st;
     const double *RU, *GW;
     double *PQ;
@@ -682,7 +682,7 @@ struct CgInit1 {  // p = -r; q = -u; residNorm2 = g'*r   (cpcg.m:380-387)
         st->stop = !(st->residNorm > st->stopTol && 0 < st->itmax);
     }
 };
-struct CgStep {  // x += alpha p; a += alpha q; g += alpha Ap; w += alpha Cq   (cpcg.m:415-418)
+struct CgStep {  // x += alpha p; a += alpha q; g += alpha Ap; w += alpha Cq   (cpcg.m:161-164)
     DState *st;
     double *XA, *GW;
     const double *PQ, *APCQ;
@@ -697,7 +697,7 @@ struct CgStep {  // x += alpha p; a += alpha q; g += alpha Ap; w += alpha Cq   (
         GW[i] = GW[i] + alpha * APCQ[i];
     }
 };
-struct CgResid {  // t = a + u; residNorm2_new = g'*r + t'*w   (cpcg.m:421-429)
+struct CgResid {  // t = a + u; residNorm2_new = g'*r + t'*w   (cpcg.m:166-176)
     DState *st;
     const double *XA, *RU, *GW;
     double *TT;
@@ -749,7 +749,7 @@ struct ArnoldiStart {
     double *v1;
     int64_t n;
     int restart_cycle;  // outer > 1 (cpgmres.m:166-171)
-    int dq;             // DQGMRES: dot(u, V1) only (cpdqgmres.m:428)
+    int dq;             // DQGMRES: dot(u, V1) only (cpdqgmres.m:157)
     int first;          // first cycle: sets stopTol and pushes the history
     __device__ bool setup() { return true; }
     __device__ void operator()(int64_t i, double *acc) {
@@ -816,7 +816,7 @@ __device__ inline double &Hd(DState *st, int64_t j, int64_t kk) {  // H(j, kk), 
 }
 
 // V(:,k+1) = w(1:n) ; Q(:,k+1) = Q(:,k) - w(n+1:N) ; H(j,k) = dot(V_j,u) + dot(Q_j,t) for the window
-// (cpgmres.m:212-215, cpdqgmres.m:479-484).  All window dots in one streaming pass.
+// (cpgmres.m:212-215, cpdqgmres.m:208-213).  All window dots in one streaming pass.
 constexpr int kDotGroup = 16;
 __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double *V, const double *w,
                                                               const double *ut, int64_t n, int64_t N, int64_t ring,
@@ -937,7 +937,7 @@ static void launch_arnoldi_dots(Ctx &c, DState *st, double *V, const double *w, 
 }
 
 // V(:,k+1) -= H(j,k) V(:,j) for the window in order; H(k+1,k) = sqrt(dot(u,V_{k+1}) + dot(t,Q_{k+1}));
-// then rotations, SymGivens and the g update (cpgmres.m:214-247, cpdqgmres.m:481-521).
+// then rotations, SymGivens and the g update (cpgmres.m:214-247, cpdqgmres.m:214-250).
 // Window coefficients and basis pointers of one step, tabulated in LDS once per workgroup:
 // the per-element loops then read (h_j, V_j) from LDS instead of recomputing ring slots and
 // H indices (64-bit divisions) for every element.
@@ -1010,7 +1010,7 @@ struct ArnoldiOrth {
             st->residNorm = fabs(st->g[kk]);
             push(st->hist, st->nh, st->hcap, st->residNorm);
             st->stop = !(st->residNorm > st->stopTol && kk < st->restart);
-        } else {  // cpdqgmres.m:489-539
+        } else {  // cpdqgmres.m:218-269
             const int64_t mem = st->mem, M1 = mem + 1;
             const int64_t kpos = (kk - 1) % M1, kp1pos = kk % M1, rotpos = (kk - 1) % mem;
             Hd(st, kk, 1) = hk1;
@@ -1052,7 +1052,7 @@ struct GmresNormalize {
 };
 
 // DQGMRES: normalise V(:,kp1pos); PV(:,kpos) = (V(:,kpos) - sum H(j,kk) PV(:,jpos)) / H(k,2);
-// x = x + g(kpos)*PV(:,kpos); y = y - g(kpos)*PQ(:,kpos)   (cpdqgmres.m:493-536)
+// x = x + g(kpos)*PV(:,kpos); y = y - g(kpos)*PQ(:,kpos)   (cpdqgmres.m:222-265)
 struct DqgmresDirection {
     DState *st;
     double *V, *PV, *xy;
@@ -1689,7 +1689,7 @@ void SolveCore::dqgmres(const double *b, double *xy, cpk_stats *stats) {
     CPK_HIP(hipMemsetAsync(xy, 0, N * sizeof(double), c.stream));
     if (print) printf("\n**** Constraint-preconditioned version of DQGMRES - mem = %lld ****\n\n", (long long)Mm);
     launch_set_concat(c, UT, b, n, m);
-    M.apply(UT, N, Wv, nullptr);  // M * [u; t], t = 0 (cpdqgmres.m:425)
+    M.apply(UT, N, Wv, nullptr);  // M * [u; t], t = 0 (cpdqgmres.m:154)
     launch_ewred<2>(c, N, ArnoldiStart{st, Wv, UT, xy, V, n, 0, 1, 1});
     launch_ew(c, N, NormalizeCopy{st, V, nullptr, 1, 0.0});
     CPK_HIP(hipGetLastError());

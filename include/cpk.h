@@ -63,7 +63,7 @@ typedef struct {
     int has_nitref, has_itref_tol, has_force_itref, has_residual_update;
 } cpk_opts;
 
-/* stats / flag outputs (cpminres.m:250-252, cpsymmlq.m:363-367, cpcglanczos.m:681-694,
+/* stats / flag outputs (cpminres.m:250-252, cpsymmlq.m:363-367, cpcglanczos.m:311-325,
  * reg_cpkrylov.m:177-178).  History buffers are caller-allocated with capacity hist_cap
  * (itmax + 2 suffices for every method); a NULL buffer is skipped. */
 typedef struct {

@@ -37,6 +37,35 @@ static double now_s(void) {
 
 #define EPS 2.220446049250313e-16 /* MATLAB eps */
 
+/* Threads of the CPU-baseline leg (orc_set_threads; default 1 = the plain serial restatement).
+ * With T > 1 the row-parallel parts run under OpenMP -- SpMV rows, elementwise updates and the
+ * triangular sweeps by elimination-tree levels (every unknown still subtracts its terms in the
+ * serial order, so these stay bit-identical) -- and the dot products sum per-thread chunks,
+ * which changes their rounding (timing leg only; parity uses T = 1). */
+static int g_threads = 1;
+void orc_set_threads(int t) { g_threads = t < 1 ? 1 : t; }
+int orc_get_threads(void) {
+#ifdef _OPENMP
+    return g_threads;
+#else
+    return 1;
+#endif
+}
+#ifdef _OPENMP
+#define PLOOP(i, lo, hi, ...)                                                                  \
+    do {                                                                                       \
+        const int64_t lo_ = (lo), hi_ = (hi);                                                  \
+        if (g_threads > 1 && hi_ - lo_ > 4096) {                                               \
+            _Pragma("omp parallel for schedule(static) num_threads(g_threads)")                \
+            for (int64_t i = lo_; i < hi_; i++) { __VA_ARGS__ }                                \
+        } else {                                                                               \
+            for (int64_t i = lo_; i < hi_; i++) { __VA_ARGS__ }                                \
+        }                                                                                      \
+    } while (0)
+#else
+#define PLOOP(i, lo, hi, ...) for (int64_t i = (lo); i < (hi); i++) { __VA_ARGS__ }
+#endif
+
 /* ------------------------------------------------------------------------------------ */
 /* owned CSR                                                                             */
 /* ------------------------------------------------------------------------------------ */
@@ -89,15 +118,22 @@ static int csr_transpose(const orc_csr *a, csr *t) {
 
 /* y = A*x  (MATLAB sparse mtimes: per row, 0 + a1*x1 + a2*x2 + ... in column order) */
 static void spmv(const orc_csr *a, const double *x, double *y) {
-    for (int64_t i = 0; i < a->nrows; i++) {
+    PLOOP(i, 0, a->nrows,
         double acc = 0.0;
         for (int64_t p = a->ptr[i]; p < a->ptr[i + 1]; p++) acc += a->val[p] * x[a->ind[p]];
         y[i] = acc;
-    }
+    );
 }
 
 static double dot(int64_t n, const double *a, const double *b) {
     double s = 0.0;
+#ifdef _OPENMP
+    if (g_threads > 1 && n > 4096) {
+        _Pragma("omp parallel for schedule(static) num_threads(g_threads) reduction(+ : s)")
+        for (int64_t i = 0; i < n; i++) s += a[i] * b[i];
+        return s;
+    }
+#endif
     for (int64_t i = 0; i < n; i++) s += a[i] * b[i];
     return s;
 }
@@ -156,6 +192,10 @@ struct orc_ldl2 {
      * intend; off (the default) restates MATLAB's value-object semantics, where they stay zero */
     int handle;
     double *ghn;
+    /* threaded sweeps (g_threads > 1): rows by forward / backward level, built on first use */
+    int64_t nlf, nlb;
+    int64_t *lf_ptr, *lb_ptr;
+    int32_t *lf_rows, *lb_rows;
 };
 
 static int assemble_kp(const orc_csr *A, const orc_csr *B, const orc_csr *C, csr *Kp) {
@@ -403,6 +443,7 @@ void orc_ldl2_destroy(orc_ldl2 *op) {
     free(op->w2);
     free(op->w3);
     free(op->ghn);
+    free(op->lf_ptr), free(op->lb_ptr), free(op->lf_rows), free(op->lb_rows);
     free(op);
 }
 
@@ -429,10 +470,65 @@ void orc_ldl2_get_perm(const orc_ldl2 *op, int32_t *perm) {
     memcpy(perm, op->perm, (size_t)op->N * sizeof(int32_t));
 }
 
+/* rows grouped by level: lev[i] = 1 + max lev of the rows it reads (counting sort); fwd
+ * visits rows in increasing order (rows of L read lower rows), else decreasing (columns of L) */
+static void level_sets(int64_t N, const int64_t *ptr, const int32_t *ind, int fwd, int64_t *nl,
+                       int64_t **lptr, int32_t **lrows) {
+    int32_t *lev = calloc((size_t)(N > 0 ? N : 1), sizeof(int32_t));
+    int32_t mx = -1;
+    for (int64_t s = 0; s < N; s++) {
+        const int64_t i = fwd ? s : N - 1 - s;
+        int32_t l = 0;
+        for (int64_t p = ptr[i]; p < ptr[i + 1]; p++)
+            if (lev[ind[p]] + 1 > l) l = lev[ind[p]] + 1;
+        lev[i] = l;
+        if (l > mx) mx = l;
+    }
+    *nl = mx + 1;
+    *lptr = calloc((size_t)mx + 2, sizeof(int64_t));
+    *lrows = malloc((size_t)(N > 0 ? N : 1) * sizeof(int32_t));
+    for (int64_t i = 0; i < N; i++) (*lptr)[lev[i] + 1]++;
+    for (int64_t l = 0; l <= mx; l++) (*lptr)[l + 1] += (*lptr)[l];
+    int64_t *nx = malloc((size_t)(mx + 1 > 0 ? mx + 1 : 1) * sizeof(int64_t));
+    for (int64_t l = 0; l <= mx; l++) nx[l] = (*lptr)[l];
+    for (int64_t i = 0; i < N; i++) (*lrows)[nx[lev[i]]++] = (int32_t)i;
+    free(nx);
+    free(lev);
+}
+
 /* y = op.LDL * x = P * (L' \ (D \ (L \ (P' * x))))   (opLDL2.m:86) */
-static void ldl_apply(const struct orc_ldl2 *op, const double *x, double *y) {
+static void ldl_apply(struct orc_ldl2 *op, const double *x, double *y) {
     int64_t N = op->N;
     double *z = op->w3;
+#ifdef _OPENMP
+    if (g_threads > 1) {
+        /* the same sweeps in row ("pull") form by levels: unknown i subtracts L(i,j)*z(j) in
+         * increasing j (forward) and L(j,i)*z(j) in decreasing j (backward), as the column
+         * sweeps below do, so the result is bit-identical */
+        if (!op->lf_ptr) {
+            level_sets(N, op->Lrow.ptr, op->Lrow.ind, 1, &op->nlf, &op->lf_ptr, &op->lf_rows);
+            level_sets(N, op->Lp, op->Li, 0, &op->nlb, &op->lb_ptr, &op->lb_rows);
+        }
+        PLOOP(k, 0, N, z[k] = x[op->perm[k]];);
+        for (int64_t l = 0; l < op->nlf; l++)
+            PLOOP(q, op->lf_ptr[l], op->lf_ptr[l + 1],
+                const int32_t i = op->lf_rows[q];
+                double acc = z[i];
+                for (int64_t p = op->Lrow.ptr[i]; p < op->Lrow.ptr[i + 1]; p++) acc -= op->Lrow.val[p] * z[op->Lrow.ind[p]];
+                z[i] = acc;
+            );
+        PLOOP(j, 0, N, z[j] = z[j] / op->D[j];);
+        for (int64_t l = 0; l < op->nlb; l++)
+            PLOOP(q, op->lb_ptr[l], op->lb_ptr[l + 1],
+                const int32_t i = op->lb_rows[q];
+                double acc = z[i];
+                for (int64_t p = op->Lp[i + 1] - 1; p >= op->Lp[i]; p--) acc -= op->Lx[p] * z[op->Li[p]];
+                z[i] = acc;
+            );
+        PLOOP(k, 0, N, y[op->perm[k]] = z[k];);
+        return;
+    }
+#endif
     for (int64_t k = 0; k < N; k++) z[k] = x[op->perm[k]]; /* P' * x */
     /* L \ z, column-oriented (unit diagonal: z_j / 1 is exact) */
     for (int64_t j = 0; j < N; j++) {
@@ -457,7 +553,7 @@ int orc_ldl2_apply(orc_ldl2 *op, const double *x, double *y) {
     int64_t n = op->nA, N = op->N;
     double *r = op->w1, *t = op->w2;
     if (op->residual_update != 0) {
-        for (int64_t i = 0; i < N; i++) t[i] = x[i] - op->ghn[i]; /* [x(1:n) - op.Aty; x(n+1:N) - op.Cy] */
+        PLOOP(i, 0, N, t[i] = x[i] - op->ghn[i];); /* [x(1:n) - op.Aty; x(n+1:N) - op.Cy] */
         ldl_apply(op, t, y);
         /* op.Aty = op.A(1:n, n+1:n+m) * y2; op.Cy = op.A(n+1:N, n+1:N) * y2 (opLDL2.m:169-171) */
         orc_csr k12 = view(&op->K12), k22 = view(&op->K22);
@@ -470,15 +566,15 @@ int orc_ldl2_apply(orc_ldl2 *op, const double *x, double *y) {
     if (op->nitref > 0) {
         orc_csr kp = view(&op->Kp);
         spmv(&kp, y, r);
-        for (int64_t i = 0; i < N; i++) r[i] = x[i] - r[i];
+        PLOOP(i, 0, N, r[i] = x[i] - r[i];);
         double rNorm = nrm2(N, r);
         double xNorm = nrm2(N, x);
         double nit = 0;
         while (nit < op->nitref && (rNorm >= op->itref_tol * xNorm || op->force_itref != 0)) {
             ldl_apply(op, r, t); /* dy = op.LDL * r */
-            for (int64_t i = 0; i < N; i++) y[i] = y[i] + t[i];
+            PLOOP(i, 0, N, y[i] = y[i] + t[i];);
             spmv(&kp, y, r);
-            for (int64_t i = 0; i < N; i++) r[i] = x[i] - r[i];
+            PLOOP(i, 0, N, r[i] = x[i] - r[i];);
             rNorm = nrm2(N, r);
             nit = nit + 1;
         }
@@ -546,8 +642,8 @@ static int run_minres(int64_t n, int64_t m, const double *b, const orc_csr *A, c
     if (s.print) printf("\n**** Constraint-preconditioned version of MINRES ****\n\n");
     memcpy(in, u, (size_t)n * sizeof(double)); /* [u; t], t = 0 */
     orc_ldl2_apply(M, in, vprec);
-    for (int64_t i = 0; i < n; i++) vkp1[i] = vprec[i];
-    for (int64_t i = 0; i < m; i++) qkp1[i] = -vprec[n + i];
+    PLOOP(i, 0, n, vkp1[i] = vprec[i];);
+    PLOOP(i, 0, m, qkp1[i] = -vprec[n + i];);
     double beta = dot(n, u, vkp1);
     const double eps100 = 100 * EPS;
     if (beta < -eps100) {
@@ -556,8 +652,8 @@ static int run_minres(int64_t n, int64_t m, const double *b, const orc_csr *A, c
     }
     beta = sqrt(fabs(beta));
     if (beta > 0) {
-        for (int64_t i = 0; i < n; i++) vkp1[i] = vkp1[i] / beta;
-        for (int64_t i = 0; i < m; i++) qkp1[i] = qkp1[i] / beta;
+        PLOOP(i, 0, n, vkp1[i] = vkp1[i] / beta;);
+        PLOOP(i, 0, m, qkp1[i] = qkp1[i] / beta;);
     }
     memcpy(wv, vkp1, (size_t)n * sizeof(double));
     memcpy(wq, qkp1, (size_t)m * sizeof(double));
@@ -580,12 +676,12 @@ static int run_minres(int64_t n, int64_t m, const double *b, const orc_csr *A, c
         spmv(A, vk, u);
         spmv(C, qk, t);
         double alpha = dot(n, u, vk) + dot(m, t, qk);
-        for (int64_t i = 0; i < n; i++) in[i] = u[i];
-        for (int64_t i = 0; i < m; i++) in[n + i] = -t[i];
+        PLOOP(i, 0, n, in[i] = u[i];);
+        PLOOP(i, 0, m, in[n + i] = -t[i];);
         orc_ldl2_apply(M, in, vprec);
-        for (int64_t i = 0; i < n; i++) vkp1[i] = vprec[i] - alpha * vk[i] - beta * vkm1[i];
-        for (int64_t i = 0; i < m; i++) qkp1[i] = qk[i] - vprec[n + i];
-        for (int64_t i = 0; i < m; i++) qkp1[i] = qkp1[i] - alpha * qk[i] - beta * qkm1[i];
+        PLOOP(i, 0, n, vkp1[i] = vprec[i] - alpha * vk[i] - beta * vkm1[i];);
+        PLOOP(i, 0, m, qkp1[i] = qk[i] - vprec[n + i];);
+        PLOOP(i, 0, m, qkp1[i] = qkp1[i] - alpha * qk[i] - beta * qkm1[i];);
         beta = dot(n, u, vkp1) + dot(m, t, qkp1);
         if (beta < -eps100) {
             char where[64];
@@ -595,8 +691,8 @@ static int run_minres(int64_t n, int64_t m, const double *b, const orc_csr *A, c
         }
         beta = sqrt(fabs(beta));
         if (beta > 0) {
-            for (int64_t i = 0; i < n; i++) vkp1[i] = vkp1[i] / beta;
-            for (int64_t i = 0; i < m; i++) qkp1[i] = qkp1[i] / beta;
+            PLOOP(i, 0, n, vkp1[i] = vkp1[i] / beta;);
+            PLOOP(i, 0, m, qkp1[i] = qkp1[i] / beta;);
         }
         double oldeps = epsln;
         double delta = cs * deltabar + sn * alpha;
@@ -610,10 +706,10 @@ static int run_minres(int64_t n, int64_t m, const double *b, const orc_csr *A, c
         taubar = sn * taubar;
         tmp = wv1, wv1 = wv2, wv2 = wv, wv = tmp;
         tmp = wq1, wq1 = wq2, wq2 = wq, wq = tmp;
-        for (int64_t i = 0; i < n; i++) wv[i] = (vk[i] - oldeps * wv1[i] - delta * wv2[i]) / gamma;
-        for (int64_t i = 0; i < m; i++) wq[i] = (qk[i] - oldeps * wq1[i] - delta * wq2[i]) / gamma;
-        for (int64_t i = 0; i < n; i++) x[i] = x[i] + tau * wv[i];
-        for (int64_t i = 0; i < m; i++) y[i] = y[i] - tau * wq[i];
+        PLOOP(i, 0, n, wv[i] = (vk[i] - oldeps * wv1[i] - delta * wv2[i]) / gamma;);
+        PLOOP(i, 0, m, wq[i] = (qk[i] - oldeps * wq1[i] - delta * wq2[i]) / gamma;);
+        PLOOP(i, 0, n, x[i] = x[i] + tau * wv[i];);
+        PLOOP(i, 0, m, y[i] = y[i] - tau * wq[i];);
         residNorm = taubar;
         if ((rc = hist_push(st, &st->hist, &st->hist_len, residNorm))) goto done;
         if (s.print) printf("%5lld  %9.2e\n", (long long)k, residNorm);
@@ -628,7 +724,7 @@ done:
 }
 
 /* ------------------------------------------------------------------------------------ */
-/* cpcg (kernels/cpcg.m:348-449)                                                         */
+/* cpcg (kernels/cpcg.m:94-195)                                                          */
 /* ------------------------------------------------------------------------------------ */
 static int run_cg(int64_t n, int64_t m, const double *b, const orc_csr *A, const orc_csr *C, orc_ldl2 *M,
                   const orc_opts *o, double *x, double *y, orc_stats *st) {
@@ -848,7 +944,7 @@ done:
 }
 
 /* ------------------------------------------------------------------------------------ */
-/* cpdqgmres (kernels/cpdqgmres.m:368-553)                                               */
+/* cpdqgmres (kernels/cpdqgmres.m:97-282)                                                */
 /* ------------------------------------------------------------------------------------ */
 static int run_dqgmres(int64_t n, int64_t m, const double *b, const orc_csr *A, const orc_csr *C, orc_ldl2 *M,
                        const orc_opts *o, double *x, double *y, orc_stats *st) {
@@ -1155,7 +1251,7 @@ done:
 }
 
 /* ------------------------------------------------------------------------------------ */
-/* cpcglanczos (kernels/cpcglanczos.m:476-695)                                           */
+/* cpcglanczos (kernels/cpcglanczos.m:107-326)                                           */
 /* ------------------------------------------------------------------------------------ */
 static int run_cglanczos(int64_t n, int64_t m, const double *b, const orc_csr *A, const orc_csr *C, orc_ldl2 *M,
                          const orc_opts *o, double *x, double *y, orc_stats *st) {
@@ -1226,7 +1322,7 @@ static int run_cglanczos(int64_t n, int64_t m, const double *b, const orc_csr *A
         for (int64_t i = 0; i < n; i++) vkp1[i] = vprec[i] - alpha * vk[i] - beta * vkm1[i];
         for (int64_t i = 0; i < m; i++) qkp1[i] = qk[i] - vprec[n + i];
         for (int64_t i = 0; i < m; i++) qkp1[i] = qkp1[i] - alpha * qk[i] - beta * qkm1[i];
-        /* bb1, bb2 (cpcglanczos.m:615) are never used */
+        /* bb1, bb2 (cpcglanczos.m:246) are never used */
         beta = dot(n, u, vkp1) + dot(m, t, qkp1);
         if (beta < -eps100) {
             rc = set_err(ORC_ERR_INDEFINITE,

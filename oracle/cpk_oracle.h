@@ -102,6 +102,11 @@ void orc_symgivens(double a, double b, double *c, double *s, double *d);
 
 const char *orc_last_error(void);
 
+/* Threads of the CPU-baseline timing leg (default 1).  T > 1 runs SpMV, elementwise updates and
+ * level-scheduled sweeps under OpenMP (bit-identical) and chunked dot products (not). */
+void orc_set_threads(int t);
+int orc_get_threads(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,6 +72,8 @@ def lib():
         L.orc_reg_cpkrylov.argtypes = [C.c_int, P(C.c_double), P(_Csr), P(_Csr), P(_Csr), P(_Csr), P(_Opts),
                                        C.c_int, P(C.c_int32), P(C.c_double), P(_Stats), P(C.c_void_p)]
         L.orc_symgivens.argtypes = [C.c_double, C.c_double] + [P(C.c_double)] * 3
+        L.orc_set_threads.argtypes = [C.c_int]
+        L.orc_get_threads.restype = C.c_int
         L.orc_last_error.restype = C.c_char_p
         _lib = L
     return _lib
@@ -232,6 +234,13 @@ def reg_cpkrylov(name, b, A, B, Cm, G, opts=None, order="rcm", perm=None, hist_c
         name, cap, _ptr(x, C.c_double))
     stats["ptime"], stats["stime"] = st.ptime, st.stime
     return x, stats
+
+
+def set_threads(t):
+    """Threads of the CPU-baseline timing leg (1 = the serial restatement); returns the count
+    actually in effect (1 when the oracle was built without OpenMP)."""
+    lib().orc_set_threads(int(t))
+    return lib().orc_get_threads()
 
 
 def symgivens(a, b):

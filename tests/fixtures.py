@@ -1,7 +1,7 @@
 """Loads the reference's example systems (tests/golden/*.npz, data only) and cuts the blocks
 exactly as the examples do: Q = K(1:n,1:n); G = diag(diag(Q)); A = K(n+1:end,1:n);
-C = -K(n+1:end,n+1:end)  (examples/cpk_exprog1.m:59-64, cpk_exprog2.m:179-184), and the
-options of the examples (cpk_exprog1.m:79-90, cpk_exprog2.m:188-208)."""
+C = -K(n+1:end,n+1:end)  (examples/cpk_exprog1.m:59-63, cpk_exprog2.m:61-65), and the
+options of the examples (cpk_exprog1.m:79-90, cpk_exprog2.m:69-90)."""
 import os
 
 import numpy as np

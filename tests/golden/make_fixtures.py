@@ -2,7 +2,7 @@
 
 Source (read as DATA only, never executed): /root/reference/examples/
   cvxqp1_m_2x2_symm_iter10.mat      (used by examples/cpk_exprog1.m:45-49, n = nH, m = nJ)
-  cvxqp2_s_3x3_nonsymm_perm_iter10.mat (used by examples/cpk_exprog2.m:165-169, n = nH + nZ, m = nJ)
+  cvxqp2_s_3x3_nonsymm_perm_iter10.mat (used by examples/cpk_exprog2.m:47-50, n = nH + nZ, m = nJ)
 
 Each .npz holds K (CSR: K_indptr int64, K_indices int32, K_data f64), rhs (f64), n, m,
 and x_direct = K \\ rhs computed here with scipy's SuperLU (the examples' own check,

@@ -1,8 +1,8 @@
 """Golden vectors of the CPU oracle on the reference's example systems (committed data).
 
 Runs oracle/ (the C restatement, reverse Cuthill-McKee ordering -- independent of the
-product's ordering) with the examples' options (cpk_exprog1.m:79-90, cpk_exprog2.m:188-208)
-for every method the examples name (cpk_exprog1.m:67-74, cpk_exprog2.m:187-192) and saves
+product's ordering) with the examples' options (cpk_exprog1.m:79-90, cpk_exprog2.m:69-90)
+for every method the examples name (cpk_exprog1.m:67-74, cpk_exprog2.m:69-74) and saves
 niters, solved, the histories and x to tests/golden/oracle_<system>_<method>[_<param>].npz.
 Run: python tests/golden/make_golden.py
 """

@@ -1,5 +1,5 @@
 """GPU parity: the HIP path (through the C ABI) against the CPU oracle on the reference's
-example systems with the examples' options (cpk_exprog1.m:79-90, cpk_exprog2.m:188-208).
+example systems with the examples' options (cpk_exprog1.m:79-90, cpk_exprog2.m:69-90).
 
 Parity bar:
   - bit-exact: niters, len(history), flag.solved; and the preconditioner apply given identical

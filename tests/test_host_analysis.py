@@ -113,3 +113,32 @@ def test_zero_pivot_reported():
     with pytest.raises(cpk.CpkError) as e:
         cpk.analyze(G0, P["B"], -P["C"])
     assert e.value.code == 6
+
+
+def test_csc_boundary_matches_csr():
+    """cpk_mat_create_csc -- MATLAB's own sparse storage (0-based size_t jc / ir, the MEX
+    gateway's entry, matlab/cpk_mex.c) -- yields the same analysis as the CSR entry: identical
+    ordering, factor, D and schedule."""
+    P = F.load("cvxqp1_m")
+    mats_csc = [cpk.Matrix(M, host_only=True, csc=True) for M in (P["G"], P["B"], -P["C"])]
+    a = cpk.analyze(*mats_csc)
+    b = cpk.analyze(P["G"], P["B"], -P["C"])
+    for k in ("D", "perm", "round_ptr", "blk_lvl", "lvl_row", "order"):
+        assert np.array_equal(a[k], b[k]), k
+    assert (a["L"] != b["L"]).nnz == 0
+    assert a["info"] == b["info"]
+
+
+def test_split_tol_option_validated(monkeypatch):
+    """CPK_SPLIT_TOL (a diagnostic of the distributed plan) must be a finite number in (0, 1):
+    every rank builds the same plan from it, so a malformed value is an error, not a default."""
+    S = saddle_system(N=20000, seed=3)
+    for bad in ("abc", "0", "1.5", "nan", "-0.1", "0.03x"):
+        monkeypatch.setenv("CPK_SPLIT_TOL", bad)
+        with pytest.raises(cpk.CpkError):
+            cpk.dist_plan(S["G"], S["B"], -S["C"], S["Q"], S["C"], 2, 0)
+    monkeypatch.setenv("CPK_SPLIT_TOL", "0.06")
+    p6 = cpk.dist_plan(S["G"], S["B"], -S["C"], S["Q"], S["C"], 2, 0)
+    monkeypatch.delenv("CPK_SPLIT_TOL")
+    p3 = cpk.dist_plan(S["G"], S["B"], -S["C"], S["Q"], S["C"], 2, 0)
+    assert p6["nT"] <= p3["nT"]

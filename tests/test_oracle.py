@@ -153,3 +153,29 @@ def test_indefinite_error():
     with pytest.raises(O.OracleError) as e:
         O.reg_cpkrylov("minres", P["rhs"], P["Q"], P["B"], P["C"], Gneg, dict(F.EXPROG_OPTS), order="rcm")
     assert "does not behave as a spd matrix" in str(e.value)
+
+
+def test_threaded_leg_sweeps_bitexact():
+    """The OpenMP CPU-baseline leg (orc_set_threads) sweeps by elimination-tree levels in row
+    form; every unknown subtracts its terms in the serial column sweep's order, so M*z is
+    bit-identical to the serial restatement.  Its cpminres differs only through the chunked
+    dot products: same niters, histories within the 1e-8·h0 parity floor."""
+    from cpkrylov_amd.synthetic import saddle_system
+    S = saddle_system(N=40000, seed=7)
+    M = O.LDL2(S["G"], S["B"], -S["C"], order="rcm")
+    M.set(nitref=2, force_itref=0, itref_tol=1e-14)
+    z = np.random.default_rng(1).standard_normal(S["n"] + S["m"])
+    y1 = M @ z
+    opts = dict(F.EXPROG_OPTS)
+    x1, _, s1 = O.method("minres", S["rhs"][:S["n"]], S["Q"], S["C"], M, opts)
+    try:
+        assert O.set_threads(4) == 4
+        y4 = M @ z
+        x4, _, s4 = O.method("minres", S["rhs"][:S["n"]], S["Q"], S["C"], M, opts)
+    finally:
+        O.set_threads(1)
+    assert np.array_equal(y1, y4)
+    assert s1["niters"] == s4["niters"]
+    h1, h4 = s1["residHistory"], s4["residHistory"]
+    assert np.max(np.abs(h1 - h4)) <= 1e-8 * h1[0]
+    assert np.linalg.norm(x1 - x4) <= 1e-8 * np.linalg.norm(x1)
