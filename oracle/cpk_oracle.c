@@ -18,6 +18,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 static char g_err[512];
 static int set_err(int code, const char *fmt, ...) {
@@ -943,6 +946,117 @@ done:
     return rc;
 }
 
+#ifdef _OPENMP
+/* Timing-leg (g_threads > 1) forms of cpdqgmres's three window loops (cpdqgmres.m:210-216 the
+ * H column against the fixed (u,t) and the V/Q update, :218-225 the new basis vector's norm,
+ * :254-265 the direction vector and the x/y update).  The serial restatement runs each loop as
+ * the reference writes it, one full pass per window column; here every element still takes the
+ * same operations in the same order (so V, Q, PV, PQ, x, y are bit-identical given equal
+ * scalars), but rows are processed in blocks that keep a block of every window column in cache,
+ * so the window streams from memory once per pass instead of once per column.  Dot products sum
+ * per-thread partials, combined in thread order (deterministic for a given thread count). */
+enum { DQ_ROWS = 2048 };
+
+/* hj[q] = dot(V(:,jpos), u) + dot(Q(:,jpos), t) for window columns j = j0 .. j0+nj-1 */
+static void dq_window_dots(int64_t n, int64_t m, const double *V, const double *Q, int64_t M1, int64_t j0,
+                           int64_t nj, const double *u, const double *t, double *hj) {
+    const int T = g_threads;
+    double *part = calloc((size_t)(2 * T * (nj > 0 ? nj : 1)), sizeof(double));
+    _Pragma("omp parallel num_threads(T)") {
+        const int th = omp_get_thread_num();
+        double *pv = part + (size_t)th * 2 * nj, *pq = pv + nj;
+        _Pragma("omp for schedule(static)") for (int64_t b = 0; b < n; b += DQ_ROWS) {
+            const int64_t e = b + DQ_ROWS < n ? b + DQ_ROWS : n;
+            for (int64_t q = 0; q < nj; q++) {
+                const double *v = V + ((j0 + q - 1) % M1) * n;
+                double s = pv[q];
+                for (int64_t i = b; i < e; i++) s += v[i] * u[i];
+                pv[q] = s;
+            }
+        }
+        _Pragma("omp for schedule(static)") for (int64_t b = 0; b < m; b += DQ_ROWS) {
+            const int64_t e = b + DQ_ROWS < m ? b + DQ_ROWS : m;
+            for (int64_t q = 0; q < nj; q++) {
+                const double *v = Q + ((j0 + q - 1) % M1) * m;
+                double s = pq[q];
+                for (int64_t i = b; i < e; i++) s += v[i] * t[i];
+                pq[q] = s;
+            }
+        }
+    }
+    for (int64_t q = 0; q < nj; q++) {
+        double sv = 0.0, sq = 0.0;
+        for (int th = 0; th < T; th++) sv += part[(size_t)th * 2 * nj + q], sq += part[(size_t)th * 2 * nj + nj + q];
+        hj[q] = sv + sq;
+    }
+    free(part);
+}
+
+/* V(:,kp1) -= hj[q] V(:,jpos) in window order (likewise Q), then returns
+ * dot(u, V(:,kp1)) + dot(t, Q(:,kp1)) */
+static double dq_window_orth(int64_t n, int64_t m, double *V, double *Q, int64_t M1, int64_t j0, int64_t nj,
+                             const double *hj, int64_t kp1pos, const double *u, const double *t) {
+    const int T = g_threads;
+    double *part = calloc((size_t)(2 * T), sizeof(double));
+    double *vk = V + (kp1pos - 1) * n, *qk = Q + (kp1pos - 1) * m;
+    _Pragma("omp parallel num_threads(T)") {
+        const int th = omp_get_thread_num();
+        double sv = 0.0, sq = 0.0;
+        _Pragma("omp for schedule(static)") for (int64_t b = 0; b < n; b += DQ_ROWS) {
+            const int64_t e = b + DQ_ROWS < n ? b + DQ_ROWS : n;
+            for (int64_t q = 0; q < nj; q++) {
+                const double *v = V + ((j0 + q - 1) % M1) * n, h = hj[q];
+                for (int64_t i = b; i < e; i++) vk[i] = vk[i] - h * v[i];
+            }
+            for (int64_t i = b; i < e; i++) sv += u[i] * vk[i];
+        }
+        _Pragma("omp for schedule(static)") for (int64_t b = 0; b < m; b += DQ_ROWS) {
+            const int64_t e = b + DQ_ROWS < m ? b + DQ_ROWS : m;
+            for (int64_t q = 0; q < nj; q++) {
+                const double *v = Q + ((j0 + q - 1) % M1) * m, h = hj[q];
+                for (int64_t i = b; i < e; i++) qk[i] = qk[i] - h * v[i];
+            }
+            for (int64_t i = b; i < e; i++) sq += t[i] * qk[i];
+        }
+        part[2 * th] = sv, part[2 * th + 1] = sq;
+    }
+    double sv = 0.0, sq = 0.0;
+    for (int th = 0; th < T; th++) sv += part[2 * th], sq += part[2 * th + 1];
+    free(part);
+    return sv + sq;
+}
+
+/* PV(:,kpos) = (V(:,kpos) - sum_q hj[q] PV(:,jpos)) / hkk, x += gk PV(:,kpos); likewise PQ with
+ * y -= gk PQ(:,kpos) */
+static void dq_window_dir(int64_t n, int64_t m, const double *V, const double *Q, double *PV, double *PQ,
+                          int64_t M1, int64_t j0, int64_t nj, const double *hj, int64_t kpos, double hkk, double gk,
+                          double *x, double *y) {
+    const int T = g_threads;
+    const double *vk = V + (kpos - 1) * n, *qk = Q + (kpos - 1) * m;
+    double *pvk = PV + (kpos - 1) * n, *pqk = PQ + (kpos - 1) * m;
+    _Pragma("omp parallel num_threads(T)") {
+        _Pragma("omp for schedule(static)") for (int64_t b = 0; b < n; b += DQ_ROWS) {
+            const int64_t e = b + DQ_ROWS < n ? b + DQ_ROWS : n;
+            for (int64_t i = b; i < e; i++) pvk[i] = vk[i];
+            for (int64_t q = 0; q < nj; q++) {
+                const double *v = PV + ((j0 + q - 1) % M1) * n, h = hj[q];
+                for (int64_t i = b; i < e; i++) pvk[i] = pvk[i] - h * v[i];
+            }
+            for (int64_t i = b; i < e; i++) pvk[i] = pvk[i] / hkk, x[i] = x[i] + gk * pvk[i];
+        }
+        _Pragma("omp for schedule(static)") for (int64_t b = 0; b < m; b += DQ_ROWS) {
+            const int64_t e = b + DQ_ROWS < m ? b + DQ_ROWS : m;
+            for (int64_t i = b; i < e; i++) pqk[i] = qk[i];
+            for (int64_t q = 0; q < nj; q++) {
+                const double *v = PQ + ((j0 + q - 1) % M1) * m, h = hj[q];
+                for (int64_t i = b; i < e; i++) pqk[i] = pqk[i] - h * v[i];
+            }
+            for (int64_t i = b; i < e; i++) pqk[i] = pqk[i] / hkk, y[i] = y[i] - gk * pqk[i];
+        }
+    }
+}
+#endif
+
 /* ------------------------------------------------------------------------------------ */
 /* cpdqgmres (kernels/cpdqgmres.m:97-282)                                                */
 /* ------------------------------------------------------------------------------------ */
@@ -1012,6 +1126,26 @@ static int run_dqgmres(int64_t n, int64_t m, const double *b, const orc_csr *A, 
         orc_ldl2_apply(M, in, w);
         for (int64_t i = 0; i < n; i++) VV(kp1pos)[i] = w[i];
         for (int64_t i = 0; i < m; i++) QQ(kp1pos)[i] = QQ(kpos)[i] - w[n + i];
+#ifdef _OPENMP
+        if (g_threads > 1) { /* timing leg: the same window passes, row-blocked (see dq_window_*) */
+            int64_t j0 = k - mem + 1 > 1 ? k - mem + 1 : 1, nj = k - j0 + 1;
+            double hj[nj > 0 ? nj : 1];
+            dq_window_dots(n, m, V, Q, M1, j0, nj, u, t, hj);
+            for (int64_t q = 0; q < nj; q++) HH(j0 + q, 2 + k - (j0 + q)) = hj[q];
+            double hn2 = dq_window_orth(n, m, V, Q, M1, j0, nj, hj, kp1pos, u, t);
+            if (hn2 < 0) {
+                rc = set_err(ORC_ERR_INDEFINITE, "Iter %lld: H(k,1)^2 = %g < 0: complex norm", (long long)k, hn2);
+                goto done;
+            }
+            HH(k, 1) = sqrt(hn2);
+            if (HH(k, 1) != 0) {
+                double h = HH(k, 1);
+                PLOOP(i, 0, n, VV(kp1pos)[i] = VV(kp1pos)[i] / h;);
+                PLOOP(i, 0, m, QQ(kp1pos)[i] = QQ(kp1pos)[i] / h;);
+            }
+            goto rotations;
+        }
+#endif
         for (int64_t j = (k - mem + 1 > 1 ? k - mem + 1 : 1); j <= k; j++) {
             int64_t jpos = (j - 1) % M1 + 1, kk = 2 + k - j;
             double h = dot(n, VV(jpos), u) + dot(m, QQ(jpos), t);
@@ -1030,6 +1164,9 @@ static int run_dqgmres(int64_t n, int64_t m, const double *b, const orc_csr *A, 
             for (int64_t i = 0; i < n; i++) VV(kp1pos)[i] = VV(kp1pos)[i] / h;
             for (int64_t i = 0; i < m; i++) QQ(kp1pos)[i] = QQ(kp1pos)[i] / h;
         }
+#ifdef _OPENMP
+    rotations:
+#endif
         for (int64_t j = (k - mem > 1 ? k - mem : 1); j <= k - 1; j++) {
             int64_t jrot = (j - 1) % mem + 1, kk = k - j + 1, kk1 = kk + 1;
             double Hjk = c[jrot - 1] * HH(j, kk1) + sv[jrot - 1] * HH(j + 1, kk);
@@ -1042,6 +1179,15 @@ static int run_dqgmres(int64_t n, int64_t m, const double *b, const orc_csr *A, 
         HH(k, 1) = 0;
         g[kp1pos - 1] = sv[rotpos - 1] * g[kpos - 1];
         g[kpos - 1] = c[rotpos - 1] * g[kpos - 1];
+#ifdef _OPENMP
+        if (g_threads > 1) {
+            int64_t j0 = k - mem > 1 ? k - mem : 1, nj = k - j0;
+            double hj[nj > 0 ? nj : 1];
+            for (int64_t q = 0; q < nj; q++) hj[q] = HH(j0 + q, 2 + k - (j0 + q));
+            dq_window_dir(n, m, V, Q, PV, PQ, M1, j0, nj, hj, kpos, HH(k, 2), g[kpos - 1], x, y);
+            goto pushed;
+        }
+#endif
         memcpy(PVV(kpos), VV(kpos), (size_t)n * sizeof(double));
         memcpy(PQQ(kpos), QQ(kpos), (size_t)m * sizeof(double));
         for (int64_t j = (k - mem > 1 ? k - mem : 1); j <= k - 1; j++) {
@@ -1056,6 +1202,9 @@ static int run_dqgmres(int64_t n, int64_t m, const double *b, const orc_csr *A, 
         double gk = g[kpos - 1];
         for (int64_t i = 0; i < n; i++) x[i] = x[i] + gk * PVV(kpos)[i];
         for (int64_t i = 0; i < m; i++) y[i] = y[i] - gk * PQQ(kpos)[i];
+#ifdef _OPENMP
+    pushed:
+#endif
         residNorm = fabs(g[kp1pos - 1]);
         if ((rc = hist_push(st, &st->hist, &st->hist_len, residNorm))) goto done;
         if (s.print) printf("%5lld  %14.7e\n", (long long)k, residNorm);

@@ -1,0 +1,215 @@
+"""Parity at the headline sizes (BASELINE.json configs[3] and configs[4]), on one MI355X:
+
+  S10  10M dofs, symmetric saddle point, cpminres with the exprog1 options (the bench's workload)
+  S50  50M dofs, nonsymmetric 3x3 block, cpdqgmres(40), at most CPK_S50_ITMAX iterations
+
+each solved on one GPU and as 8 ranks (the elimination-tree split of DESIGN.md section 7 at
+P = 8, exchanging through SimComm because RCCL refuses two ranks on one device), and compared
+with the CPU oracle run with the product's pivot order:
+
+  * bit-exact: niters, len(residHistory), flag.solved, and M*z against the oracle's
+    opLDL2.multiply given the same factors (1 GPU and every one of the 8 ranks);
+  * fp64 tolerance: histories and x within max(1e-8, 10 x band) (tests/test_gpu_parity.py),
+    band = the problem's own sensitivity at this size: the largest history / x deviation of the
+    oracle under a different summation order of its inner products (the OpenMP leg) and under
+    1e-15 relative rhs perturbations.
+
+The reference of S10 is the serial oracle (the restatement as written); at S50 the serial
+oracle's window loops take ~10 s per iteration, so the reference is the OpenMP leg (the same
+arithmetic per element, inner products summed per thread) and the band comes from one
+perturbed rhs and a run on a different thread count.
+"""
+import functools
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from cpkrylov_amd.synthetic import nonsym_system, saddle_system
+from oracle import oracle as O
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+FLOOR = 1e-8
+SAFETY = 10.0
+P_RANKS = 8
+S10_N = int(os.environ.get("CPK_S10_N", 10_000_000))
+S50_N = int(os.environ.get("CPK_S50_N", 50_000_000))
+S50_ITMAX = int(os.environ.get("CPK_S50_ITMAX", 120))
+EXPROG_OPTS = dict(print=False, atol=1.0e-6, rtol=1.0e-6, itmax=500,
+                   residual_update=True, nitref=1, force_itref=True, itref_tol=1.0e-8)
+S50_OPTS = dict(EXPROG_OPTS, mem=40, itmax=S50_ITMAX)
+
+
+def _log(msg):
+    print(f"[scale {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def _threads():
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    aff = len(os.sched_getaffinity(0))
+    return max(2, min(aff, int(omp) if omp.isdigit() else aff, 16))
+
+
+@functools.lru_cache(maxsize=None)
+def _system(which):
+    t = time.perf_counter()
+    S = saddle_system(N=S10_N) if which == "s10" else nonsym_system(N=S50_N)
+    _log(f"{which}: generated N={S['N']} in {time.perf_counter() - t:.1f} s")
+    return S
+
+
+def _run_ranks(P, fn):
+    import cpkrylov_amd as cpk
+    g = cpk.SimGroup(P)
+
+    def one(r):
+        ctx = cpk.Context(device=0, rank=r, nranks=P, simgroup=g)
+        try:
+            return fn(ctx, r)
+        finally:
+            ctx.close()
+
+    with ThreadPoolExecutor(P) as ex:
+        futs = [ex.submit(one, r) for r in range(P)]
+        return [f.result(timeout=900) for f in futs]
+
+
+def _hist_dev(h, ho, h0):
+    L = min(len(h), len(ho))
+    return float(np.max(np.abs(np.asarray(h[:L]) - np.asarray(ho[:L]))) / h0)
+
+
+def _oracle_solve(method, S, opts, perm, threads, rhs=None):
+    """reg_cpkrylov on the oracle with the product's pivot order and its own factorization."""
+    O.set_threads(threads)
+    try:
+        t = time.perf_counter()
+        x, st = O.reg_cpkrylov(method, S["rhs"] if rhs is None else rhs, S["Q"], S["B"], S["C"], S["G"], opts,
+                               perm=perm)
+        _log(f"oracle {method} threads={threads}: {st['niters']} iterations in {time.perf_counter() - t:.1f} s")
+        return x, st
+    finally:
+        O.set_threads(1)
+
+
+@functools.lru_cache(maxsize=None)
+def _reference(which, perm_bytes):
+    """(x, stats) of the reference oracle solve and the sensitivity band {hist, x}."""
+    S = _system(which)
+    perm = np.frombuffer(perm_bytes, dtype=np.int32)
+    method, opts = ("minres", EXPROG_OPTS) if which == "s10" else ("dqgmres", S50_OPTS)
+    T = _threads()
+    rng = np.random.default_rng(12345)
+    if which == "s10":
+        x_ref, s_ref = _oracle_solve(method, S, opts, perm, 1)
+        others = [_oracle_solve(method, S, opts, perm, T)]
+        for _ in range(2):
+            rhs = S["rhs"] * (1 + 1e-15 * rng.standard_normal(S["N"]))
+            others.append(_oracle_solve(method, S, opts, perm, T, rhs))
+    else:
+        x_ref, s_ref = _oracle_solve(method, S, opts, perm, T)
+        rhs = S["rhs"] * (1 + 1e-15 * rng.standard_normal(S["N"]))
+        others = [_oracle_solve(method, S, opts, perm, max(2, T // 2)), _oracle_solve(method, S, opts, perm, T, rhs)]
+    h_ref = s_ref["residHistory"]
+    bd = {"hist": 0.0, "x": 0.0}
+    for x, st in others:
+        bd["hist"] = max(bd["hist"], _hist_dev(st["residHistory"], h_ref, h_ref[0]))
+        bd["x"] = max(bd["x"], float(np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref)))
+    _log(f"{which}: band hist {bd['hist']:.3e} x {bd['x']:.3e}")
+    return x_ref, s_ref, bd
+
+
+def _check_solve(which, x, stats, flag, perm):
+    x_ref, s_ref, bd = _reference(which, np.ascontiguousarray(perm, np.int32).tobytes())
+    h, ho = stats["residHistory"], s_ref["residHistory"]
+    assert stats["niters"] == s_ref["niters"]
+    assert flag["solved"] == s_ref["solved"]
+    assert len(h) == len(ho)
+    dev = _hist_dev(h, ho, ho[0])
+    dx = float(np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref))
+    _log(f"{which}: niters {stats['niters']} solved {flag['solved']} hist dev {dev:.3e} "
+         f"(tol {max(FLOOR, SAFETY * bd['hist']):.3e}) x dev {dx:.3e} (tol {max(FLOOR, SAFETY * bd['x']):.3e})")
+    assert dev <= max(FLOOR, SAFETY * bd["hist"]), (dev, bd)
+    assert dx <= max(FLOOR, SAFETY * bd["x"]), (dx, bd)
+
+
+def _set_props(M):
+    M.nitref, M.itref_tol = EXPROG_OPTS["nitref"], EXPROG_OPTS["itref_tol"]
+    M.residual_update, M.force_itref = EXPROG_OPTS["residual_update"], EXPROG_OPTS["force_itref"]
+
+
+def _apply_oracle(S, factors, z):
+    Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=factors)
+    Mo.set(nitref=1.0, itref_tol=1e-8, force_itref=1.0, residual_update=1.0)
+    return Mo @ z
+
+
+_FACTORS = {}
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("which", ["s10", "s50"])
+def test_headline_one_gpu(which):
+    import cpkrylov_amd as cpk
+    S = _system(which)
+    method, opts = ("minres", EXPROG_OPTS) if which == "s10" else ("dqgmres", S50_OPTS)
+    t = time.perf_counter()
+    x, stats, flag = cpk.reg_cpkrylov(getattr(cpk, "cp" + method), S["rhs"], S["Q"], S["B"], S["C"], S["G"], opts)
+    _log(f"{which}: GPU reg_cpkrylov {stats['niters']} iterations, ptime {stats['ptime']:.1f} s, "
+         f"stime {stats['stime']:.2f} s, total {time.perf_counter() - t:.1f} s")
+    M = stats["M"]
+    L, D, perm = M.export_factors()
+    _FACTORS[which] = (L, D, perm)
+    # M*z with the exprog1 properties against the oracle's multiply with the same factors
+    _set_props(M)
+    z = np.random.default_rng(31).standard_normal(S["N"])
+    y = M * z
+    yo = _apply_oracle(S, (L, D, perm), z)
+    assert np.array_equal(y, yo), np.max(np.abs(y - yo))
+    del M, stats["M"]
+    _check_solve(which, x, stats, flag, perm)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("which", ["s10", "s50"])
+def test_headline_eight_ranks(which):
+    """The P = 8 split of the same system: every rank's M*z equals the 1-GPU apply (and so the
+    oracle's) bit for bit; the distributed solve matches the oracle reference."""
+    import cpkrylov_amd as cpk
+    S = _system(which)
+    method, opts = ("minres", EXPROG_OPTS) if which == "s10" else ("dqgmres", S50_OPTS)
+    z = np.random.default_rng(31).standard_normal(S["N"])
+
+    def work(ctx, r):
+        M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+        _set_props(M)
+        y = M * z
+        info = {"rows": len(M.local_dofs()[0])}
+        del M
+        x, stats, flag = cpk.reg_cpkrylov(getattr(cpk, "cp" + method), S["rhs"], S["Q"], S["B"], S["C"], S["G"],
+                                          opts, ctx=ctx)
+        perm = stats["M"].export_factors()[2] if r == 0 else None
+        return y, info, x, {k: v for k, v in stats.items() if k != "M"}, flag, perm
+
+    t = time.perf_counter()
+    res = _run_ranks(P_RANKS, work)
+    _log(f"{which}: {P_RANKS} ranks done in {time.perf_counter() - t:.1f} s; rows per rank "
+         f"{[r[1]['rows'] for r in res]}")
+    perm = res[0][5]
+    if which in _FACTORS and np.array_equal(_FACTORS[which][2], perm):
+        factors = _FACTORS[which]
+    else:
+        ref = cpk.opLDL2(S["G"], S["B"], -S["C"])
+        factors = ref.export_factors()
+        del ref
+    yo = _apply_oracle(S, factors, z)
+    for y, *_ in res:
+        assert np.array_equal(y, yo), np.max(np.abs(y - yo))
+    y, info, x, stats, flag, _ = res[0]
+    for _, _, xr, sr, fr, _ in res[1:]:  # every rank returns the same global answer
+        assert np.array_equal(xr, x) and sr["niters"] == stats["niters"] and fr == flag
+    _check_solve(which, x, stats, flag, perm)
