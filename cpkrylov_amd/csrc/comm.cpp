@@ -87,8 +87,8 @@ struct SimGroup {
     std::condition_variable cv;
     int arrived = 0;
     uint64_t gen = 0;
-    DBuf<double> shared;
-    static constexpr size_t kCap = size_t(16) << 20;  // doubles
+    DBuf<double> shared;  // grown on demand to the largest collective (every rank asks the same n)
+    static constexpr size_t kCap0 = size_t(16) << 20;  // doubles
     explicit SimGroup(int p) : P(p) {}
     void barrier() {
         std::unique_lock<std::mutex> lk(mu);
@@ -109,7 +109,12 @@ struct SimComm : Comm {
     int rank;
     SimComm(SimGroup *gg, int r) : g(gg), rank(r) {}
     void check(size_t n) const {
-        if (n * (size_t)g->P > SimGroup::kCap) throw Error(CPK_ERR_UNSUPPORTED, "simulated collective too large");
+        if (n * (size_t)g->P <= g->shared.n) return;
+        // every rank of a collective passes the same n: all arrive, rank 0 grows the buffer
+        // while the others wait, then all continue with the new one
+        g->barrier();
+        if (rank == 0) g->shared.alloc(n * (size_t)g->P);
+        g->barrier();
     }
     void allreduce_sum(double *buf, size_t n, hipStream_t s) override {
         check(n);
@@ -135,7 +140,7 @@ struct SimComm : Comm {
 
 SimGroup *simgroup_create(int nranks) {
     auto *g = new SimGroup(nranks);
-    g->shared.alloc(SimGroup::kCap);
+    g->shared.alloc(SimGroup::kCap0);
     return g;
 }
 void simgroup_destroy(SimGroup *g) { delete g; }

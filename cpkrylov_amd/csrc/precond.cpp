@@ -20,6 +20,20 @@
 
 namespace cpk {
 
+// CPK_TIMING=1: per-phase wall times of the host analysis on stderr (diagnostic)
+struct PhaseClock {
+    const char *what;
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    explicit PhaseClock(const char *w) : what(w), on(getenv("CPK_TIMING") != nullptr), t(std::chrono::steady_clock::now()) {}
+    void lap(const char *phase) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[cpk] %s: %-32s %8.3f s\n", what, phase, std::chrono::duration<double>(now - t).count());
+        t = now;
+    }
+};
+
 SweepConfig sweep_config() {
     SweepConfig cfg;
     if (const char *e = getenv("CPK_SWEEP")) {
@@ -40,21 +54,28 @@ SweepConfig sweep_config() {
 
 Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22) {
     auto t0 = std::chrono::steady_clock::now();
+    PhaseClock pc("analyze");
     Analysis an;
     an.Kp = assemble_kp(A11, B, C22);  // dimension checks of opLDL2.m:61-75
     an.n = A11.nrows, an.m = C22.nrows, an.N = an.n + an.m;
+    pc.lap("assemble");
     std::vector<int32_t> perm = order_kp(an.Kp, an.n, &an.ordering);
+    pc.lap("order");
     Factor f0 = ldl_factor(an.Kp, perm, 1);
+    pc.lap("factor");
     an.sweep = sweep_config();
     an.S = build_schedule(f0, an.sweep.rows[0], an.sweep.cap[0], an.sweep.rows[1], an.sweep.cap[1], an.sweep.sub0);
+    pc.lap("schedule");
     an.F = relabel(f0, an.S);
     an.F0 = std::move(f0);
+    pc.lap("relabel");
     an.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return an;
 }
 
 Precond *precond_create(Ctx &c, Analysis &&an) {
     auto t0 = std::chrono::steady_clock::now();
+    PhaseClock clk("precond_create");
     auto pc = std::make_unique<Precond>();
     pc->ctx = &c;
     pc->n = an.n, pc->m = an.m, pc->N = an.N;
@@ -70,6 +91,7 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
         const std::vector<int64_t> key(pc->S.order.begin(), pc->S.order.end());
         make_dfactor(an.F, pc->S, pc->dF, &key);
     }
+    clk.lap("device factor layout + upload");
     an.F = Factor();
     pc->F = std::move(an.F0);
     pc->w.alloc(pc->N);

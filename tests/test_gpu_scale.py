@@ -14,10 +14,13 @@ with the CPU oracle run with the product's pivot order:
     oracle under a different summation order of its inner products (the OpenMP leg) and under
     1e-15 relative rhs perturbations.
 
-The reference of S10 is the serial oracle (the restatement as written); at S50 the serial
-oracle's window loops take ~10 s per iteration, so the reference is the OpenMP leg (the same
-arithmetic per element, inner products summed per thread) and the band comes from one
-perturbed rhs and a run on a different thread count.
+The reference of S10 is the serial oracle (the restatement as written) and its band comes from
+oracle runs.  At S50 the serial oracle's window loops take ~10 s per iteration and one OpenMP
+run ~90 s, so the reference is the OpenMP leg (the same arithmetic per element, inner products
+summed per thread) and the band comes from the GPU itself: two solves whose shifted rhs is
+perturbed by 1e-15 relative, against the unperturbed one.  The band measures the problem's
+sensitivity, not the instrument, so any deterministic defect of the GPU path still shows as a
+deviation from the oracle reference.
 """
 import functools
 import os
@@ -98,33 +101,65 @@ def _oracle_solve(method, S, opts, perm, threads, rhs=None):
 
 @functools.lru_cache(maxsize=None)
 def _reference(which, perm_bytes):
-    """(x, stats) of the reference oracle solve and the sensitivity band {hist, x}."""
+    """(x, stats) of the reference oracle solve, and for S10 the oracle's sensitivity band."""
     S = _system(which)
     perm = np.frombuffer(perm_bytes, dtype=np.int32)
     method, opts = ("minres", EXPROG_OPTS) if which == "s10" else ("dqgmres", S50_OPTS)
     T = _threads()
-    rng = np.random.default_rng(12345)
-    if which == "s10":
-        x_ref, s_ref = _oracle_solve(method, S, opts, perm, 1)
-        others = [_oracle_solve(method, S, opts, perm, T)]
-        for _ in range(2):
-            rhs = S["rhs"] * (1 + 1e-15 * rng.standard_normal(S["N"]))
-            others.append(_oracle_solve(method, S, opts, perm, T, rhs))
-    else:
+    if which != "s10":
         x_ref, s_ref = _oracle_solve(method, S, opts, perm, T)
+        return x_ref, s_ref, None
+    rng = np.random.default_rng(12345)
+    x_ref, s_ref = _oracle_solve(method, S, opts, perm, 1)
+    others = [_oracle_solve(method, S, opts, perm, T)]
+    for _ in range(2):
         rhs = S["rhs"] * (1 + 1e-15 * rng.standard_normal(S["N"]))
-        others = [_oracle_solve(method, S, opts, perm, max(2, T // 2)), _oracle_solve(method, S, opts, perm, T, rhs)]
+        others.append(_oracle_solve(method, S, opts, perm, T, rhs))
     h_ref = s_ref["residHistory"]
     bd = {"hist": 0.0, "x": 0.0}
     for x, st in others:
         bd["hist"] = max(bd["hist"], _hist_dev(st["residHistory"], h_ref, h_ref[0]))
         bd["x"] = max(bd["x"], float(np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref)))
-    _log(f"{which}: band hist {bd['hist']:.3e} x {bd['x']:.3e}")
+    _log(f"{which}: oracle band hist {bd['hist']:.3e} x {bd['x']:.3e}")
     return x_ref, s_ref, bd
 
 
-def _check_solve(which, x, stats, flag, perm):
+_GPU_BAND = {}
+
+
+def _gpu_band(which, M=None):
+    """Sensitivity band from GPU solves of the method with the shifted rhs perturbed by 1e-15
+    relative (reg_cpkrylov.m:152-160 shift computed once with M)."""
+    if which in _GPU_BAND:
+        return _GPU_BAND[which]
+    import cpkrylov_amd as cpk
+    S = _system(which)
+    method, opts = ("minres", EXPROG_OPTS) if which == "s10" else ("dqgmres", S50_OPTS)
+    if M is None:
+        M = cpk.opLDL2(S["G"], S["B"], -S["C"])
+    _set_props(M)
+    n = S["n"]
+    xy0 = M * np.concatenate([np.zeros(n), S["rhs"][n:]])
+    b1 = S["rhs"][:n] - S["Q"] @ xy0[:n] - S["B"].T @ xy0[n:]
+    fn = getattr(cpk, "cp" + method)
+    x0, y0, s0 = fn(b1, S["Q"], S["C"], M, opts)[:3]
+    xy_0 = np.concatenate([x0, y0])
+    h0 = s0["residHistory"]
+    rng = np.random.default_rng(4242)
+    bd = {"hist": 0.0, "x": 0.0}
+    for _ in range(2):
+        x, y, st = fn(b1 * (1 + 1e-15 * rng.standard_normal(n)), S["Q"], S["C"], M, opts)[:3]
+        bd["hist"] = max(bd["hist"], _hist_dev(st["residHistory"], h0, h0[0]))
+        bd["x"] = max(bd["x"], float(np.linalg.norm(np.concatenate([x, y]) - xy_0) / np.linalg.norm(xy_0)))
+    _log(f"{which}: GPU band hist {bd['hist']:.3e} x {bd['x']:.3e}")
+    _GPU_BAND[which] = bd
+    return bd
+
+
+def _check_solve(which, x, stats, flag, perm, M=None):
     x_ref, s_ref, bd = _reference(which, np.ascontiguousarray(perm, np.int32).tobytes())
+    if bd is None:
+        bd = _gpu_band(which, M)
     h, ho = stats["residHistory"], s_ref["residHistory"]
     assert stats["niters"] == s_ref["niters"]
     assert flag["solved"] == s_ref["solved"]
@@ -170,8 +205,8 @@ def test_headline_one_gpu(which):
     y = M * z
     yo = _apply_oracle(S, (L, D, perm), z)
     assert np.array_equal(y, yo), np.max(np.abs(y - yo))
-    del M, stats["M"]
-    _check_solve(which, x, stats, flag, perm)
+    del stats["M"]
+    _check_solve(which, x, stats, flag, perm, M)
 
 
 @pytest.mark.timeout(900)
