@@ -174,11 +174,22 @@ class opLDL2:
             pt = C.c_double()
             check(lib.cpk_pc_create(self.ctx.h, mats[0].h, mats[1].h, mats[2].h, C.byref(pt), C.byref(h)))
             self.h = h
+            self.ptime = pt.value
         info = _lib.PcInfo()
         check(lib.cpk_pc_get_info(self.h, C.byref(info)))
         self.info = {k: getattr(info, k) for k, _ in _lib.PcInfo._fields_}
         self.nA, self.nC, self.n = info.n, info.m, info.N
         self.shape = (info.N, info.N)
+
+    def refactor(self, A, B, Cm):
+        """New values of (A, B, C) with the sparsity this operator was built with: the factors
+        of opLDL2(A, B, C) recomputed on the device, symbolic analysis reused (cpk_pc_refactor;
+        an IPM outer iteration's rebuild of opLDL2, opLDL2.m:60-92).  Returns the seconds taken."""
+        mats = [_as_matrix(M, self.ctx) for M in (A, B, Cm)]
+        pt = C.c_double()
+        check(lib.cpk_pc_refactor(self.h, mats[0].h, mats[1].h, mats[2].h, C.byref(pt)))
+        self.ptime = pt.value
+        return pt.value
 
     # ---- properties --------------------------------------------------------------------------
     def _get(self):

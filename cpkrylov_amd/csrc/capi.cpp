@@ -313,6 +313,19 @@ int cpk_pc_create(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptim
     API_END
 }
 
+int cpk_pc_refactor(cpk_pc M, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptime) {
+    API_BEGIN
+    need(M && A11 && B && C22, "opLDL2: Invalid number of arguments.");
+    Precond &p = *M->p;
+    if (A11->h.nrows != p.gn || C22->h.nrows != p.gm || B->h.nrows != p.gm || B->h.ncols != p.gn)
+        throw Error(CPK_ERR_DIM, "Incompatible dimensions.");
+    if (pattern_hash(A11->h, B->h, C22->h) != p.pattern_hash)
+        throw Error(CPK_ERR_ARGS, "refactor: the sparsity of A11, B or C22 differs from the factored one");
+    const double s = precond_refactor(p, A11->dev(), B->dev(), C22->dev());
+    if (ptime) *ptime = s;
+    API_END
+}
+
 int cpk_pc_destroy(cpk_pc M) {
     API_BEGIN
     delete M;
@@ -417,11 +430,17 @@ int cpk_pc_get_info(cpk_pc M, cpk_pc_info *info) {
 int cpk_pc_export(cpk_pc M, int64_t *Lcolptr, int32_t *Lrowind, double *Lval, double *D, int32_t *perm) {
     API_BEGIN
     need(M, "NULL argument");
-    const Factor &f = M->p->F;
+    const Precond &p = *M->p;
+    const Factor &f = p.F;
     if (Lcolptr) std::memcpy(Lcolptr, f.Lp.data(), f.Lp.size() * sizeof(int64_t));
     if (Lrowind) std::memcpy(Lrowind, f.Li.data(), f.Li.size() * sizeof(int32_t));
-    if (Lval) std::memcpy(Lval, f.Lx.data(), f.Lx.size() * sizeof(double));
-    if (D) std::memcpy(D, f.D.data(), f.D.size() * sizeof(double));
+    if (p.dl.ready) {  // values computed on the device (ldl.hip): CSC order, pivot order
+        if (Lval && !f.Li.empty()) CPK_HIP(hipMemcpy(Lval, p.dl.Lx.p, f.Li.size() * sizeof(double), hipMemcpyDeviceToHost));
+        if (D && f.N) CPK_HIP(hipMemcpy(D, p.dl.D.p, (size_t)f.N * sizeof(double), hipMemcpyDeviceToHost));
+    } else {
+        if (Lval) std::memcpy(Lval, f.Lx.data(), f.Lx.size() * sizeof(double));
+        if (D) std::memcpy(D, f.D.data(), f.D.size() * sizeof(double));
+    }
     if (perm) std::memcpy(perm, f.perm.data(), f.perm.size() * sizeof(int32_t));
     API_END
 }

@@ -133,8 +133,11 @@ struct BwdExtra {
     int64_t key;
     double val;
 };
+// fsrc / bsrc (optional): the f.Li / f.Lx slot of every forward / backward device entry (the
+// device numeric factorization fills fval / bval through them); f.Lx may be empty (zeros)
 void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vector<int64_t> *key = nullptr,
-                  const std::vector<std::vector<BwdExtra>> *extra = nullptr);
+                  const std::vector<std::vector<BwdExtra>> *extra = nullptr, std::vector<int32_t> *fsrc = nullptr,
+                  std::vector<int32_t> *bsrc = nullptr);
 size_t sweep_lds_bytes(int R, int CAP);
 // Sweep configuration: rows and entries staged per block, threads per block.
 // CPK_SWEEP="rows,cap,threads" overrides the default.
@@ -186,6 +189,25 @@ void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x
 // redundant separator solve into wT (= w + nsub); rank 0 writes (add: accumulates) y at the T dofs
 void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active);
 
+// ---- device numeric LDL' (ldl.hip) --------------------------------------------------------
+struct DLdl {
+    int64_t N = 0, nnz = 0, nf = 0, nb = 0;
+    std::vector<int32_t> lev_ptr;  // host: rows by elimination-tree height
+    DBuf<int32_t> lev_rows, Rp, Rc, Rcsc, Lp, Li, kp_ptr, kp_tgt, fsrc, bsrc, dsrc;
+    DBuf<uint32_t> kp_src;
+    DBuf<int64_t> kp_from;  // Kp entry -> (block << 40 | entry) of A11 / B / C22 (refactorization)
+    DBuf<double> Lx, D, Y;  // L in CSC order, D in pivot order, per-row-entry scratch
+    DBuf<int> bad;
+    bool ready = false;
+};
+void dldl_setup(DLdl &d, const LdlSymbolic &sym, const Factor &f, const std::vector<int32_t> &fsrc,
+                const std::vector<int32_t> &bsrc, const std::vector<int32_t> &order);
+// numeric factorization from the device Kp values, then DFactor's sweep values and D;
+// throws CPK_ERR_FACTOR on a zero or NaN pivot
+void dldl_factor(Ctx &c, DLdl &d, const double *kpv, DFactor &dF);
+// Kp values from the device values of A11, B, C22 through d.kp_from
+void dldl_assemble_kp(Ctx &c, const DLdl &d, const double *a, const double *b, const double *cc, double *kpv);
+
 // ---- preconditioner (precond.cpp) --------------------------------------------------------
 // Host analysis of opLDL2's constructor: Kp assembly, ordering, LDL', sweep schedule.
 struct Analysis {
@@ -197,8 +219,13 @@ struct Analysis {
     int ordering = 0;
     double seconds = 0;
     SweepConfig sweep;
+    // device_numeric: the host computed structure only (F0.Lx, F0.D empty); sym and rsrc feed
+    // the device numeric phase (ldl.hip)
+    bool device_numeric = false;
+    LdlSymbolic sym;
+    std::vector<int32_t> rsrc;  // F's entry t came from F0's entry rsrc[t]
 };
-Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22);
+Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, bool device_numeric = false);
 
 // The separator solve of a distributed preconditioner, device copy.
 constexpr int64_t kSepPiggy = 2;  // spare payload slots per rank in the separator exchange
@@ -242,6 +269,8 @@ struct Precond {
     DMat dKp;
     DFactor dF;
     DBuf<double> w, r;   // permuted work vector, refinement residual
+    DLdl dl;             // device numeric factorization (single GPU); dl.ready: F.Lx / F.D live on the device
+    uint64_t pattern_hash = 0;  // sparsity of (A11, B, C22): a refactorization must keep it
     DBuf<int> active;    // refinement predicate
     // public properties of opLDL2 (opLDL2.m:45-50)
     double nitref = 3, itref_tol = 1.0e-8, force_itref = 0, residual_update = 0;
@@ -269,6 +298,10 @@ struct Precond {
     double apply_bytes() const;
 };
 Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22);
+// new values of A11, B, C22 (device CSR copies) with the sparsity the preconditioner was built
+// with: Kp and the numeric factorization on the device, symbolic analysis reused; returns seconds
+double precond_refactor(Precond &p, const DMat &A11, const DMat &B, const DMat &C22);
+uint64_t pattern_hash(const HCsr &A11, const HCsr &B, const HCsr &C22);
 Precond *precond_create(Ctx &c, Analysis &&an);
 // distributed preconditioner of rank c.rank out of c.nranks
 Precond *precond_create_dist(Ctx &c, Analysis &&an);

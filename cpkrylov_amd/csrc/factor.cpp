@@ -10,8 +10,13 @@
 namespace cpk {
 
 // Up-looking (row-by-row) LDL': row k of L is the solution of a sparse triangular system
-// whose pattern is the reach of row k's entries in the elimination tree.
-Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int /*nthreads*/) {
+// whose pattern is the reach of row k's entries in the elimination tree (the up-looking
+// algorithm of T. A. Davis, "Direct Methods for Sparse Linear Systems", SIAM 2006, sec. 4.7 /
+// LDL: ldl_symbolic, ldl_numeric).  Here the reach of each row is visited in ascending column
+// order (a topological order of the row's triangular solve) instead of the stack order, so a
+// device thread walking the sorted row pattern performs the same operations in the same order.
+Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int /*nthreads*/, LdlSymbolic *sym,
+                  bool numeric) {
     const int64_t N = Kp.nrows;
     Factor f;
     f.N = N;
@@ -38,12 +43,24 @@ Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int /*nthrea
     f.Lp.assign(N + 1, 0);
     for (int64_t k = 0; k < N; k++) f.Lp[k + 1] = f.Lp[k] + lnz[k];
     if (f.Lp[N] > INT32_MAX) throw Error(CPK_ERR_NOMEM, "factor too large for 32-bit entry offsets");
-    f.Li.resize(f.Lp[N]);
-    f.Lx.resize(f.Lp[N]);
-    f.D.resize(N);
-    std::vector<double> y(N, 0.0);
-    std::vector<int32_t> pattern(N);
+    const int64_t nnz = f.Lp[N];
+    f.Li.resize(nnz);
+    if (numeric) f.Lx.resize(nnz), f.D.resize(N);
+    if (sym) {
+        sym->N = N;
+        sym->Rp.assign(N + 1, 0);
+        sym->Rc.resize(nnz);
+        sym->Rcsc.resize(nnz);
+        sym->kp_ptr.assign(N + 1, 0);
+        sym->kp_tgt.clear();
+        sym->kp_src.clear();
+        sym->kp_tgt.reserve((size_t)(Kp.nnz() / 2 + N));
+        sym->kp_src.reserve((size_t)(Kp.nnz() / 2 + N));
+    }
+    std::vector<double> y(numeric ? N : 0, 0.0);
+    std::vector<int32_t> pattern(N), slot(sym ? N : 0);
     std::fill(lnz.begin(), lnz.end(), 0);
+    int64_t rpos = 0;
     for (int64_t k = 0; k < N; k++) {
         int64_t top = N;
         flag[k] = (int32_t)k;
@@ -51,7 +68,7 @@ Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int /*nthrea
         for (int64_t p = Kp.ptr[r]; p < Kp.ptr[r + 1]; p++) {
             int32_t i = pinv[Kp.ind[p]];
             if (i > k) continue;
-            y[i] += Kp.val[p];
+            if (numeric) y[i] += Kp.val[p];
             int64_t len = 0;
             for (; flag[i] != k; i = f.parent[i]) {
                 pattern[len++] = i;
@@ -59,24 +76,56 @@ Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int /*nthrea
             }
             while (len > 0) pattern[--top] = pattern[--len];
         }
-        double d = y[k];
-        y[k] = 0.0;
+        std::sort(pattern.begin() + top, pattern.end());
+        if (sym) {
+            for (int64_t q = top; q < N; q++) slot[pattern[q]] = (int32_t)(rpos + (q - top));
+            for (int64_t p = Kp.ptr[r]; p < Kp.ptr[r + 1]; p++) {
+                const int32_t i = pinv[Kp.ind[p]];
+                if (i > k) continue;
+                sym->kp_tgt.push_back(i == k ? -1 : slot[i]);
+                sym->kp_src.push_back((uint32_t)p);
+            }
+            sym->kp_ptr[k + 1] = (int32_t)sym->kp_tgt.size();
+        }
+        double d = numeric ? y[k] : 0.0;
+        if (numeric) y[k] = 0.0;
         for (; top < N; top++) {
             const int32_t i = pattern[top];
-            const double yi = y[i];
-            y[i] = 0.0;
             const int64_t p2 = f.Lp[i] + lnz[i];
-            for (int64_t p = f.Lp[i]; p < p2; p++) y[f.Li[p]] -= f.Lx[p] * yi;
-            const double lki = yi / f.D[i];
-            d -= lki * yi;
+            if (numeric) {
+                const double yi = y[i];
+                y[i] = 0.0;
+                for (int64_t p = f.Lp[i]; p < p2; p++) y[f.Li[p]] -= f.Lx[p] * yi;
+                const double lki = yi / f.D[i];
+                d -= lki * yi;
+                f.Lx[p2] = lki;
+            }
             f.Li[p2] = (int32_t)k;
-            f.Lx[p2] = lki;
+            if (sym) sym->Rc[rpos] = i, sym->Rcsc[rpos] = (int32_t)p2, rpos++;
             lnz[i]++;
         }
+        if (sym) sym->Rp[k + 1] = (int32_t)rpos;
+        if (!numeric) continue;
         if (d == 0.0 || !(d == d))
             throw Error(CPK_ERR_FACTOR, "ldl: zero or NaN pivot at position " + std::to_string(k) +
                                             " (static 1x1 pivoting needs G > 0 on the nullspace and C > 0)");
         f.D[k] = d;
+    }
+    if (sym) {
+        if (sym->kp_tgt.size() > (size_t)INT32_MAX) throw Error(CPK_ERR_NOMEM, "too many Kp entries for the device factorization");
+        // rows by elimination-tree height: a row depends only on its descendants
+        std::vector<int32_t> h(N, 0);
+        int32_t hmax = 0;
+        for (int64_t v = 0; v < N; v++) {
+            if (f.parent[v] >= 0) h[f.parent[v]] = std::max(h[f.parent[v]], h[v] + 1);
+            hmax = std::max(hmax, h[v]);
+        }
+        sym->lev_ptr.assign((size_t)hmax + 2, 0);
+        for (int64_t v = 0; v < N; v++) sym->lev_ptr[h[v] + 1]++;
+        for (int32_t l = 0; l <= hmax; l++) sym->lev_ptr[l + 1] += sym->lev_ptr[l];
+        sym->lev_rows.resize(N);
+        std::vector<int32_t> nx(sym->lev_ptr.begin(), sym->lev_ptr.end() - 1);
+        for (int64_t v = 0; v < N; v++) sym->lev_rows[nx[h[v]]++] = (int32_t)v;
     }
     return f;
 }
@@ -252,7 +301,7 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     return s;
 }
 
-Factor relabel(const Factor &f, const Schedule &s) {
+Factor relabel(const Factor &f, const Schedule &s, std::vector<int32_t> *src) {
     const int64_t N = f.N;
     std::vector<int32_t> pos(N);
     for (int64_t q = 0; q < N; q++) pos[s.order[q]] = (int32_t)q;
@@ -273,17 +322,20 @@ Factor relabel(const Factor &f, const Schedule &s) {
         g.Lp[q + 1] = g.Lp[q] + (f.Lp[old + 1] - f.Lp[old]);
     }
     g.Li.resize(f.Li.size());
-    g.Lx.resize(f.Lx.size());
-    std::vector<std::pair<int32_t, double>> col;
+    const bool vals = !f.Lx.empty();
+    if (vals) g.Lx.resize(f.Lx.size());
+    if (src) src->resize(f.Li.size());
+    std::vector<std::pair<int32_t, int64_t>> col;
     for (int64_t q = 0; q < N; q++) {
         int32_t old = s.order[q];
         col.clear();
-        for (int64_t p = f.Lp[old]; p < f.Lp[old + 1]; p++) col.emplace_back(pos[f.Li[p]], f.Lx[p]);
+        for (int64_t p = f.Lp[old]; p < f.Lp[old + 1]; p++) col.emplace_back(pos[f.Li[p]], p);
         std::sort(col.begin(), col.end(), [](auto &a, auto &b) { return a.first < b.first; });
         for (size_t t = 0; t < col.size(); t++) {
             if (col[t].first <= q) throw Error(CPK_ERR_FACTOR, "internal: relabel is not topological");
             g.Li[g.Lp[q] + t] = col[t].first;
-            g.Lx[g.Lp[q] + t] = col[t].second;
+            if (vals) g.Lx[g.Lp[q] + t] = f.Lx[col[t].second];
+            if (src) (*src)[g.Lp[q] + t] = (int32_t)col[t].second;
         }
     }
     return g;

@@ -28,6 +28,9 @@ HCsr csr_from_csc(int64_t nr, int64_t nc, const size_t *jc, const size_t *ir, co
 HCsr transpose(const HCsr &a);
 // Kp = [A B'; B C]  (opLDL2.m:81)
 HCsr assemble_kp(const HCsr &A, const HCsr &B, const HCsr &C);
+// source of every Kp entry: (block << 40) | entry index, block 0 = A, 1 = B (B and B' entries),
+// 2 = C, in assemble_kp's entry order
+std::vector<int64_t> kp_value_sources(const HCsr &A, const HCsr &B, const HCsr &C);
 // blkdiag(A, C): the Krylov operator's diagonal blocks, used to fuse u = A*v and t = C*q.
 HCsr blkdiag(const HCsr &A, const HCsr &C);
 bool is_diagonal(const HCsr &a);
@@ -51,7 +54,26 @@ struct Factor {
     std::vector<double> D;
     std::vector<int32_t> parent; // elimination tree
 };
-Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int nthreads);
+// Symbolic data of the up-looking factorization, for its numeric phase on the device
+// (ldl.hip): row patterns of L (ascending), each row entry's CSC slot, the Kp entries that seed
+// each row, and the rows grouped by elimination-tree height (rows of one height are independent).
+struct LdlSymbolic {
+    int64_t N = 0;
+    std::vector<int32_t> Rp;      // row k of strict L: columns Rc[Rp[k] .. Rp[k+1]), ascending
+    std::vector<int32_t> Rc;
+    std::vector<int32_t> Rcsc;    // CSC slot (index into Factor::Li / Lx) of row entry t
+    std::vector<int32_t> kp_ptr;  // seeds of row k: [kp_ptr[k], kp_ptr[k+1]) in Kp's entry order
+    std::vector<int32_t> kp_tgt;  // row-entry slot t, or -1 for the pivot (diagonal) itself
+    std::vector<uint32_t> kp_src; // Kp entry index of the seed
+    std::vector<int32_t> lev_ptr; // rows of height h: lev_rows[lev_ptr[h] .. lev_ptr[h+1])
+    std::vector<int32_t> lev_rows;
+};
+// Up-looking LDL'.  Row k's pattern (the reach of its Kp entries in the elimination tree) is
+// processed in ascending column order, so the device numeric phase (ldl.hip), which walks the
+// same pattern in the same order, reproduces L and D bit for bit.  numeric = false: structure
+// only (Lx, D left empty); sym: also return the symbolic data of the device phase.
+Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int nthreads, LdlSymbolic *sym = nullptr,
+                  bool numeric = true);
 
 // ---- SpTRSV schedule ---------------------------------------------------------------------
 // The elimination tree is cut into blocks: sets of whole subtrees of at most R rows and at
@@ -78,6 +100,7 @@ struct Schedule {
 Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1, int64_t SUB0 = 0,
                         const std::vector<int64_t> *extra_bwd = nullptr);
 // Apply the schedule's relabel to the factor (values unchanged, exact data movement).
-Factor relabel(const Factor &f, const Schedule &s);
+// src (optional): src[t] = index into f.Li / f.Lx of the relabelled factor's entry t.
+Factor relabel(const Factor &f, const Schedule &s, std::vector<int32_t> *src = nullptr);
 
 }  // namespace cpk

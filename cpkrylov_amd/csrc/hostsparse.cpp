@@ -125,6 +125,29 @@ HCsr assemble_kp(const HCsr &A, const HCsr &B, const HCsr &C) {
     return K;
 }
 
+std::vector<int64_t> kp_value_sources(const HCsr &A, const HCsr &B, const HCsr &C) {
+    const int64_t n = A.nrows, m = C.nrows;
+    // B' rows with B's entry index of each entry (the order transpose() produces: rows of B ascending)
+    std::vector<int64_t> tp(n + 1, 0);
+    for (int64_t p = 0; p < B.nnz(); p++) tp[B.ind[p] + 1]++;
+    for (int64_t j = 0; j < n; j++) tp[j + 1] += tp[j];
+    std::vector<int64_t> ti(B.nnz()), nx(tp.begin(), tp.end() - 1);
+    for (int64_t i = 0; i < m; i++)
+        for (int64_t p = B.ptr[i]; p < B.ptr[i + 1]; p++) ti[nx[B.ind[p]]++] = p;
+    const int64_t kB = int64_t(1) << 40, kC = int64_t(2) << 40;
+    std::vector<int64_t> src;
+    src.reserve(A.nnz() + 2 * B.nnz() + C.nnz());
+    for (int64_t i = 0; i < n; i++) {
+        for (int64_t p = A.ptr[i]; p < A.ptr[i + 1]; p++) src.push_back(p);
+        for (int64_t q = tp[i]; q < tp[i + 1]; q++) src.push_back(kB | ti[q]);
+    }
+    for (int64_t i = 0; i < m; i++) {
+        for (int64_t p = B.ptr[i]; p < B.ptr[i + 1]; p++) src.push_back(kB | p);
+        for (int64_t p = C.ptr[i]; p < C.ptr[i + 1]; p++) src.push_back(kC | p);
+    }
+    return src;
+}
+
 HCsr blkdiag(const HCsr &A, const HCsr &C) {
     const int64_t n = A.nrows, m = C.nrows;
     HCsr K;

@@ -61,57 +61,71 @@ void make_dmat(const HCsr &a, DMat &d) {
 // relabelled factor still sums in the exported factor's order); extra[q] are backward entries
 // of row q that refer to rows outside this factor (distributed separators).
 void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vector<int64_t> *key,
-                  const std::vector<std::vector<BwdExtra>> *extra) {
+                  const std::vector<std::vector<BwdExtra>> *extra, std::vector<int32_t> *fsrc,
+                  std::vector<int32_t> *bsrc) {
     const int64_t N = f.N;
     auto K = [&](int64_t q) { return key ? (*key)[q] : q; };
     int64_t nextra = 0;
     if (extra)
         for (const auto &e : *extra) nextra += (int64_t)e.size();
+    if (extra && bsrc) throw Error(CPK_ERR_UNSUPPORTED, "internal: entry sources with extra backward entries");
+    const bool vals = !f.Lx.empty();  // structure-only factor: values come from the device numeric phase
     d.N = N;
     d.nnz = (int64_t)f.Li.size() + nextra;
     if (d.nnz > (int64_t)INT32_MAX) throw Error(CPK_ERR_UNSUPPORTED, "factor has more than 2^31 entries");
-    // forward rows: transpose of the CSC, then each row ordered by the key of its columns
+    // forward rows: transpose of the CSC, then each row ordered by the key of its columns;
+    // fidx[q] = the CSC slot of forward entry q
     std::vector<uint32_t> fptr(N + 1, 0);
     for (int32_t i : f.Li) fptr[i + 1]++;
     for (int64_t i = 0; i < N; i++) fptr[i + 1] += fptr[i];
     const int64_t nf = (int64_t)f.Li.size();
-    std::vector<int32_t> fcol(nf);
-    std::vector<double> fval(nf);
+    std::vector<int32_t> fcol(nf), fidx(nf);
     {
         std::vector<uint32_t> nx(fptr.begin(), fptr.end() - 1);
         for (int64_t j = 0; j < N; j++)
             for (int64_t p = f.Lp[j]; p < f.Lp[j + 1]; p++) {
                 uint32_t q = nx[f.Li[p]]++;
                 fcol[q] = (int32_t)j;
-                fval[q] = f.Lx[p];
+                fidx[q] = (int32_t)p;
             }
         if (key) {
-            std::vector<std::pair<int64_t, std::pair<int32_t, double>>> row;
+            std::vector<std::pair<int64_t, std::pair<int32_t, int32_t>>> row;
             for (int64_t i = 0; i < N; i++) {
                 row.clear();
-                for (uint32_t q = fptr[i]; q < fptr[i + 1]; q++) row.push_back({K(fcol[q]), {fcol[q], fval[q]}});
+                for (uint32_t q = fptr[i]; q < fptr[i + 1]; q++) row.push_back({K(fcol[q]), {fcol[q], fidx[q]}});
                 std::sort(row.begin(), row.end(), [](auto &x, auto &y) { return x.first < y.first; });
-                for (size_t t = 0; t < row.size(); t++) fcol[fptr[i] + t] = row[t].second.first, fval[fptr[i] + t] = row[t].second.second;
+                for (size_t t = 0; t < row.size(); t++) fcol[fptr[i] + t] = row[t].second.first, fidx[fptr[i] + t] = row[t].second.second;
             }
         }
     }
-    // backward rows: L's columns (plus extra entries), keys descending
+    std::vector<double> fval(nf, 0.0);
+    if (vals)
+        for (int64_t q = 0; q < nf; q++) fval[q] = f.Lx[fidx[q]];
+    // backward rows: L's columns (plus extra entries), keys descending; bidx[q] = CSC slot
     std::vector<uint32_t> bptr(N + 1, 0);
     for (int64_t j = 0; j < N; j++)
         bptr[j + 1] = bptr[j] + (uint32_t)(f.Lp[j + 1] - f.Lp[j]) + (uint32_t)(extra ? (*extra)[j].size() : 0);
-    std::vector<int32_t> bcol(d.nnz);
-    std::vector<double> bval(d.nnz);
+    std::vector<int32_t> bcol(d.nnz), bidx(bsrc ? d.nnz : 0);
+    std::vector<double> bval(d.nnz, 0.0);
     {
-        std::vector<std::pair<int64_t, std::pair<int32_t, double>>> row;
+        std::vector<std::pair<int64_t, std::pair<int32_t, int64_t>>> row;  // (key, (col, CSC slot | ~extra))
         for (int64_t j = 0; j < N; j++) {
             row.clear();
-            for (int64_t p = f.Lp[j]; p < f.Lp[j + 1]; p++) row.push_back({K(f.Li[p]), {f.Li[p], f.Lx[p]}});
+            for (int64_t p = f.Lp[j]; p < f.Lp[j + 1]; p++) row.push_back({K(f.Li[p]), {f.Li[p], p}});
             if (extra)
-                for (const BwdExtra &e : (*extra)[j]) row.push_back({e.key, {e.col, e.val}});
+                for (size_t t = 0; t < (*extra)[j].size(); t++) row.push_back({(*extra)[j][t].key, {(*extra)[j][t].col, ~(int64_t)t}});
             std::sort(row.begin(), row.end(), [](auto &x, auto &y) { return x.first > y.first; });
-            for (size_t t = 0; t < row.size(); t++) bcol[bptr[j] + t] = row[t].second.first, bval[bptr[j] + t] = row[t].second.second;
+            for (size_t t = 0; t < row.size(); t++) {
+                const int64_t src = row[t].second.second;
+                bcol[bptr[j] + t] = row[t].second.first;
+                if (src < 0) bval[bptr[j] + t] = (*extra)[j][~src].val;
+                else if (vals) bval[bptr[j] + t] = f.Lx[src];
+                if (bsrc) bidx[bptr[j] + t] = (int32_t)src;
+            }
         }
     }
+    if (fsrc) *fsrc = std::move(fidx);
+    if (bsrc) *bsrc = std::move(bidx);
     // rounds whose blocks all fit the upper-round staging image (sptrsv_upper_kernel)
     d.round_fits.assign(s.round_ptr.empty() ? 0 : s.round_ptr.size() - 1, 1);
     for (size_t r = 0; r < d.round_fits.size(); r++)
@@ -130,7 +144,8 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     d.bptr.upload(bptr);
     d.bcol.upload(bcol);
     d.bval.upload(bval);
-    d.D.upload(f.D);
+    if (vals) d.D.upload(f.D);
+    else d.D.alloc((size_t)N);
     d.perm.upload(f.perm);
     d.nblk = (int64_t)s.blk_row.size() - 1;
     d.nlvl = (int64_t)s.lvl_row.size() - 1;

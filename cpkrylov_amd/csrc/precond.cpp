@@ -52,7 +52,7 @@ SweepConfig sweep_config() {
     return cfg;
 }
 
-Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22) {
+Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, bool device_numeric) {
     auto t0 = std::chrono::steady_clock::now();
     PhaseClock pc("analyze");
     Analysis an;
@@ -61,12 +61,13 @@ Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22) {
     pc.lap("assemble");
     std::vector<int32_t> perm = order_kp(an.Kp, an.n, &an.ordering);
     pc.lap("order");
-    Factor f0 = ldl_factor(an.Kp, perm, 1);
-    pc.lap("factor");
+    an.device_numeric = device_numeric;
+    Factor f0 = ldl_factor(an.Kp, perm, 1, device_numeric ? &an.sym : nullptr, !device_numeric);
+    pc.lap(device_numeric ? "factor (symbolic)" : "factor");
     an.sweep = sweep_config();
     an.S = build_schedule(f0, an.sweep.rows[0], an.sweep.cap[0], an.sweep.rows[1], an.sweep.cap[1], an.sweep.sub0);
     pc.lap("schedule");
-    an.F = relabel(f0, an.S);
+    an.F = relabel(f0, an.S, device_numeric ? &an.rsrc : nullptr);
     an.F0 = std::move(f0);
     pc.lap("relabel");
     an.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -89,9 +90,21 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
         pc->dF.sweep_threads[i] = an.sweep.threads[i];
     {
         const std::vector<int64_t> key(pc->S.order.begin(), pc->S.order.end());
-        make_dfactor(an.F, pc->S, pc->dF, &key);
+        if (an.device_numeric) {
+            std::vector<int32_t> fsrc, bsrc;
+            make_dfactor(an.F, pc->S, pc->dF, &key, nullptr, &fsrc, &bsrc);
+            for (auto &q : fsrc) q = an.rsrc[q];  // relabelled slot -> exported (CSC) slot
+            dldl_setup(pc->dl, an.sym, an.F0, fsrc, bsrc, pc->S.order);
+        } else {
+            make_dfactor(an.F, pc->S, pc->dF, &key);
+        }
     }
     clk.lap("device factor layout + upload");
+    if (an.device_numeric) {
+        dldl_factor(c, pc->dl, pc->dKp.val.p, pc->dF);
+        CPK_HIP(hipStreamSynchronize(c.stream));
+        clk.lap("numeric factorization (device)");
+    }
     an.F = Factor();
     pc->F = std::move(an.F0);
     pc->w.alloc(pc->N);
@@ -180,8 +193,46 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an) {
     return pc.release();
 }
 
+uint64_t pattern_hash(const HCsr &A11, const HCsr &B, const HCsr &C22) {
+    uint64_t h = 1469598103934665603ull;  // FNV-1a over the dimensions, row pointers and columns
+    auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+    for (const HCsr *a : {&A11, &B, &C22}) {
+        mix((uint64_t)a->nrows), mix((uint64_t)a->ncols);
+        for (int64_t v : a->ptr) mix((uint64_t)v);
+        for (int32_t v : a->ind) mix((uint32_t)v);
+    }
+    return h;
+}
+
+// Single GPU: the host does the symbolic analysis, the device the numeric factorization
+// (CPK_HOST_FACTOR=1: host numeric, the reference path of the device one's parity tests).
 Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22) {
-    return precond_create(c, analyze(A11, B, C22));
+    const bool dev = getenv("CPK_HOST_FACTOR") == nullptr;
+    Analysis an = analyze(A11, B, C22, dev);
+    std::vector<int64_t> src;
+    if (dev) src = kp_value_sources(A11, B, C22);
+    Precond *pc = precond_create(c, std::move(an));
+    pc->pattern_hash = pattern_hash(A11, B, C22);
+    if (dev) pc->dl.kp_from.upload(src);
+    return pc;
+}
+
+double precond_refactor(Precond &p, const DMat &A11, const DMat &B, const DMat &C22) {
+    if (p.dist || !p.dl.ready)
+        throw Error(CPK_ERR_UNSUPPORTED, "refactorization needs a single-GPU preconditioner with the device factorization");
+    auto t0 = std::chrono::steady_clock::now();
+    Ctx &c = *p.ctx;
+    dldl_assemble_kp(c, p.dl, A11.val.p, B.val.p, C22.val.p, p.dKp.val.p);
+    dldl_factor(c, p.dl, p.dKp.val.p, p.dF);
+    // the host copy of Kp follows (divide / export read the device copies; the distributed
+    // shift rows, built from the host copy, do not exist on one GPU)
+    if (!p.Kp.val.empty())
+        CPK_HIP(hipMemcpyAsync(p.Kp.val.data(), p.dKp.val.p, p.Kp.val.size() * sizeof(double), hipMemcpyDeviceToHost,
+                               c.stream));
+    CPK_HIP(hipStreamSynchronize(c.stream));
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    p.ptime = s;
+    return s;
 }
 
 // y (=|+=) LDL * xin: forward sweep, [distributed: separator exchange + solve], backward sweep

@@ -137,6 +137,14 @@ int cpk_mat_spmv(cpk_mat A, const double *x, double *y);
  * rank's LOCAL slice in the order cpk_pc_local_dofs reports ([x-part; y-part]). */
 int cpk_pc_create(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptime, cpk_pc *out);
 int cpk_pc_destroy(cpk_pc M);
+/* Refactorization with new values and the same sparsity: opLDL2(G, B, C) rebuilt in an
+ * interior-point outer loop (the constructor, opLDL2.m:60-92, called per outer iteration
+ * through reg_cpkrylov.m:131).  Kp and the numeric LDL' (opLDL2.m:81-82) are recomputed on
+ * the device from the matrices' device copies; ordering, elimination tree and sweep schedule
+ * are reused.  The factors equal those of a fresh cpk_pc_create on the same values, bit for
+ * bit.  Single GPU; CPK_ERR_ARGS when the sparsity differs, CPK_ERR_FACTOR on a zero pivot.
+ * ptime: seconds of the refactorization. */
+int cpk_pc_refactor(cpk_pc M, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptime);
 /* M.nitref = ...; M.itref_tol = ...; etc. (opLDL2.m:45-50, 97-115), has_* fields select. */
 int cpk_pc_set(cpk_pc M, const cpk_opts *opts);
 int cpk_pc_get(cpk_pc M, double *nitref, double *itref_tol, double *force_itref, double *residual_update);

@@ -469,6 +469,14 @@ void orc_ldl2_get_props(const orc_ldl2 *op, double *a, double *b, double *c, dou
     *a = op->nitref, *b = op->itref_tol, *c = op->force_itref, *d = op->residual_update;
 }
 int64_t orc_ldl2_nnzL(const orc_ldl2 *op) { return op->Lp[op->N]; }
+/* the factors P'*Kp*P = L*D*L' (strict lower L in CSC, D in pivot order); any pointer may be NULL */
+void orc_ldl2_export(const orc_ldl2 *op, int64_t *Lp, int32_t *Li, double *Lx, double *D) {
+    const int64_t N = op->N, nnz = op->Lp[N];
+    if (Lp) memcpy(Lp, op->Lp, (size_t)(N + 1) * sizeof(int64_t));
+    if (Li) memcpy(Li, op->Li, (size_t)nnz * sizeof(int32_t));
+    if (Lx) memcpy(Lx, op->Lx, (size_t)nnz * sizeof(double));
+    if (D) memcpy(D, op->D, (size_t)N * sizeof(double));
+}
 void orc_ldl2_get_perm(const orc_ldl2 *op, int32_t *perm) {
     memcpy(perm, op->perm, (size_t)op->N * sizeof(int32_t));
 }

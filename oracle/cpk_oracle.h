@@ -85,6 +85,7 @@ void orc_ldl2_get_props(const orc_ldl2 *op, double *nitref, double *itref_tol, d
 int orc_ldl2_apply(orc_ldl2 *op, const double *x, double *y);
 /* factor queries */
 int64_t orc_ldl2_nnzL(const orc_ldl2 *op);
+void orc_ldl2_export(const orc_ldl2 *op, int64_t *Lp, int32_t *Li, double *Lx, double *D);
 void orc_ldl2_get_perm(const orc_ldl2 *op, int32_t *perm);
 
 /* [x, y, stats, flag] = method(b, A, C, M, opts) -- kernels/cp*.m */

@@ -67,6 +67,7 @@ def lib():
         L.orc_ldl2_nnzL.argtypes = [C.c_void_p]
         L.orc_ldl2_nnzL.restype = C.c_int64
         L.orc_ldl2_get_perm.argtypes = [C.c_void_p, P(C.c_int32)]
+        L.orc_ldl2_export.argtypes = [C.c_void_p, P(C.c_int64), P(C.c_int32), P(C.c_double), P(C.c_double)]
         L.orc_method.argtypes = [C.c_int, P(C.c_double), P(_Csr), P(_Csr), C.c_void_p, P(_Opts),
                                  P(C.c_double), P(C.c_double), P(_Stats)]
         L.orc_reg_cpkrylov.argtypes = [C.c_int, P(C.c_double), P(_Csr), P(_Csr), P(_Csr), P(_Csr), P(_Opts),
@@ -175,6 +176,18 @@ class LDL2:
 
     def nnzL(self):
         return lib().orc_ldl2_nnzL(self.h)
+
+    def factors(self):
+        """(L strict lower CSC, D, perm) of the oracle's own factorization."""
+        N = self.n + self.m
+        nnz = int(self.nnzL())
+        Lp = np.empty(N + 1, np.int64)
+        Li = np.empty(max(nnz, 1), np.int32)
+        Lx = np.empty(max(nnz, 1))
+        D = np.empty(N)
+        lib().orc_ldl2_export(self.h, _ptr(Lp, C.c_int64), _ptr(Li, C.c_int32), _ptr(Lx, C.c_double),
+                              _ptr(D, C.c_double))
+        return sp.csc_matrix((Lx[:nnz], Li[:nnz], Lp), shape=(N, N)), D, self.perm()
 
     def perm(self):
         p = np.empty(self.n + self.m, np.int32)

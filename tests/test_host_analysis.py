@@ -142,3 +142,26 @@ def test_split_tol_option_validated(monkeypatch):
     monkeypatch.delenv("CPK_SPLIT_TOL")
     p3 = cpk.dist_plan(S["G"], S["B"], -S["C"], S["Q"], S["C"], 2, 0)
     assert p6["nT"] <= p3["nT"]
+
+
+@pytest.mark.parametrize("name", ["cvxqp1_m", "cvxqp2_s"])
+def test_host_factor_vs_oracle_factor(name):
+    """The product's host factorization (rows' reach in ascending order, the order the device
+    numeric phase uses) against the oracle's (Davis's stack order), same pivot order: equal
+    structure, values within rounding; and P'*Kp*P = L*D*L' to rounding in scipy."""
+    import scipy.sparse as sp
+
+    from oracle import oracle as O
+    P = F.load(name)
+    H = cpk.analyze(P["G"], P["B"], -P["C"])
+    Mo = O.LDL2(P["G"], P["B"], -P["C"], perm=H["perm"])
+    Lo, Do, permo = Mo.factors()
+    L, D = H["L"], H["D"]
+    assert np.array_equal(permo, H["perm"])
+    assert np.array_equal(Lo.indptr, L.indptr) and np.array_equal(Lo.indices, L.indices)
+    assert np.max(np.abs(L.data - Lo.data)) <= 1e-10 * max(1.0, np.max(np.abs(L.data)))
+    assert np.max(np.abs(D - Do) / np.abs(Do)) <= 1e-10
+    K = sp.bmat([[P["G"], P["B"].T], [P["B"], -P["C"]]]).tocsr()[H["perm"]][:, H["perm"]]
+    Lu = L + sp.identity(K.shape[0], format="csc")
+    R = K - Lu @ sp.diags(D) @ Lu.T
+    assert abs(R).max() <= 1e-12 * abs(K).max() * max(1.0, abs(Lu).max() ** 2)
