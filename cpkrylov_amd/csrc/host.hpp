@@ -1,9 +1,11 @@
 // host.hpp -- host-side sparse structures, ordering and the static-pivot LDL' factorization
 // that replaces MATLAB's ldl() inside opLDL2 (ops/opLDL2.m:81-86).
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace cpk {
@@ -39,6 +41,26 @@ bool is_diagonal(const HCsr &a);
 enum OrderKind { ORD_NATURAL = 0, ORD_GFIRST_ND = 1, ORD_GFIRST_MD = 2, ORD_ND = 3, ORD_MD = 4 };
 // Fill-reducing symmetric ordering of Kp (n = size of the (1,1) block). perm[k] = old index.
 std::vector<int32_t> order_kp(const HCsr &Kp, int64_t n, int *kind_out);
+// host threads for the analysis (CPK_THREADS, else OMP_NUM_THREADS, else the hardware's)
+int host_threads();
+// f(lo, hi) over contiguous chunks of [0, n) on up to host_threads() threads; for loops whose
+// iterations write disjoint data (results do not depend on the thread count)
+template <class F>
+void parallel_for(int64_t n, F f, int64_t grain = 4096) {
+    const int64_t T = std::min<int64_t>(host_threads(), (n + grain - 1) / grain);
+    if (T <= 1) {
+        if (n > 0) f(int64_t(0), n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int64_t chunk = (n + T - 1) / T;
+    for (int64_t t = 1; t < T; t++) {
+        const int64_t lo = t * chunk, hi = std::min(n, lo + chunk);
+        if (lo < hi) th.emplace_back([=] { f(lo, hi); });
+    }
+    f(int64_t(0), std::min(n, chunk));
+    for (auto &x : th) x.join();
+}
 // building blocks (exposed for tests)
 std::vector<int32_t> min_degree(const HCsr &graph);
 std::vector<int32_t> nested_dissection(const HCsr &graph, int leaf_size);

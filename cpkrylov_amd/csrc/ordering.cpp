@@ -9,6 +9,10 @@
 //     by nested dissection (large) or minimum degree (small);
 //   - otherwise nested dissection / minimum degree on the whole graph of Kp.
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <memory>
+#include <thread>
 #include <cstring>
 #include <numeric>
 #include <queue>
@@ -22,21 +26,37 @@ namespace cpk {
 static constexpr int64_t kMdLimit = 60000;  // exact minimum degree up to this many nodes
 static constexpr int kNdLeaf = 4;
 
-// symmetric adjacency graph (no self loops) from a list of undirected edges
+// symmetric adjacency graph (no self loops, sorted unique neighbours) from undirected edges:
+// bucketed by endpoint, then each row sorted and deduplicated on its own
 static HCsr graph_from_edges(int64_t nv, std::vector<std::pair<int32_t, int32_t>> &edges) {
+    std::vector<int64_t> cnt(nv + 1, 0);
     for (auto &e : edges)
-        if (e.first > e.second) std::swap(e.first, e.second);
-    std::sort(edges.begin(), edges.end());
-    edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
+        if (e.first != e.second) cnt[e.first + 1]++, cnt[e.second + 1]++;
+    for (int64_t i = 0; i < nv; i++) cnt[i + 1] += cnt[i];
+    std::vector<int32_t> adj(cnt[nv]);
+    {
+        std::vector<int64_t> nx(cnt.begin(), cnt.end() - 1);
+        for (auto &e : edges)
+            if (e.first != e.second) adj[nx[e.first]++] = e.second, adj[nx[e.second]++] = e.first;
+    }
+    edges.clear();
+    edges.shrink_to_fit();
+    std::vector<int64_t> deg(nv, 0);
+    parallel_for(nv, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; i++) {
+            auto b0 = adj.begin() + cnt[i], b1 = adj.begin() + cnt[i + 1];
+            std::sort(b0, b1);
+            deg[i] = std::unique(b0, b1) - b0;
+        }
+    });
     HCsr g;
     g.nrows = g.ncols = nv;
     g.ptr.assign(nv + 1, 0);
-    for (auto &e : edges) g.ptr[e.first + 1]++, g.ptr[e.second + 1]++;
-    for (int64_t i = 0; i < nv; i++) g.ptr[i + 1] += g.ptr[i];
+    for (int64_t i = 0; i < nv; i++) g.ptr[i + 1] = g.ptr[i] + deg[i];
     g.ind.resize(g.ptr[nv]);
-    std::vector<int64_t> next(g.ptr.begin(), g.ptr.end() - 1);
-    for (auto &e : edges) g.ind[next[e.first]++] = e.second, g.ind[next[e.second]++] = e.first;
-    for (int64_t i = 0; i < nv; i++) std::sort(g.ind.begin() + g.ptr[i], g.ind.begin() + g.ptr[i + 1]);
+    parallel_for(nv, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; i++) std::copy(adj.begin() + cnt[i], adj.begin() + cnt[i] + deg[i], g.ind.begin() + g.ptr[i]);
+    });
     return g;
 }
 
@@ -79,32 +99,43 @@ std::vector<int32_t> min_degree(const HCsr &g) {
 }
 
 // ---- nested dissection by BFS level structures (George-Liu) ------------------------------
+// The two halves of a dissection are independent, so large halves are ordered on their own
+// threads.  Every subset writes its nodes to its own precomputed range of the output (half A,
+// then half B, then the separator), and every decision depends only on the subset itself, so
+// the ordering is the same for any number of threads.
 namespace {
 struct Nd {
     const HCsr &g;
-    std::vector<int32_t> label;   // subset id of each node
-    std::vector<int32_t> dist;    // BFS distance (valid when stamp matches)
+    std::unique_ptr<std::atomic<int32_t>[]> label;  // subset id of each node
+    std::vector<int32_t> dist;                       // BFS distance (valid when stamp matches)
     std::vector<int32_t> stamp;
     std::vector<int32_t> out;
-    int64_t out_pos = 0;
-    int32_t next_label = 1, cur_stamp = 0;
+    std::atomic<int32_t> next_label{1}, next_stamp{0};
+    std::atomic<int> spare_threads;
     int leaf;
-    explicit Nd(const HCsr &gg, int lf) : g(gg), label(gg.nrows, 0), dist(gg.nrows, 0), stamp(gg.nrows, -1),
-                                          out(gg.nrows), leaf(lf) {}
+    Nd(const HCsr &gg, int lf, int threads)
+        : g(gg), label(new std::atomic<int32_t>[gg.nrows]), dist(gg.nrows, 0), stamp(gg.nrows, -1), out(gg.nrows),
+          spare_threads(threads - 1), leaf(lf) {
+        for (int64_t i = 0; i < gg.nrows; i++) label[i].store(0, std::memory_order_relaxed);
+    }
+    int32_t lab_of(int32_t v) const { return label[v].load(std::memory_order_relaxed); }
+    void set_lab(int32_t v, int32_t l) { label[v].store(l, std::memory_order_relaxed); }
 
     // BFS within nodes of `lab` from `src`; fills `bfs` in visit order, returns eccentricity.
-    int32_t bfs(int32_t src, int32_t lab, std::vector<int32_t> &bfs_order) {
-        cur_stamp++;
+    // Nodes of other subsets (possibly relabelled concurrently by another thread) never carry
+    // `lab`, so reading their labels is harmless.
+    int32_t bfs(int32_t src, int32_t lab, std::vector<int32_t> &bfs_order, int32_t &st) {
+        st = next_stamp.fetch_add(1, std::memory_order_relaxed) + 1;
         bfs_order.clear();
         bfs_order.push_back(src);
-        stamp[src] = cur_stamp;
+        stamp[src] = st;
         dist[src] = 0;
         for (size_t h = 0; h < bfs_order.size(); h++) {
             int32_t v = bfs_order[h];
             for (int64_t p = g.ptr[v]; p < g.ptr[v + 1]; p++) {
                 int32_t w = g.ind[p];
-                if (label[w] != lab || stamp[w] == cur_stamp) continue;
-                stamp[w] = cur_stamp;
+                if (lab_of(w) != lab || stamp[w] == st) continue;
+                stamp[w] = st;
                 dist[w] = dist[v] + 1;
                 bfs_order.push_back(w);
             }
@@ -112,100 +143,141 @@ struct Nd {
         return dist[bfs_order.back()];
     }
 
-    void emit(std::vector<int32_t> &nodes) {
+    void emit(std::vector<int32_t> &nodes, int64_t pos) {
         std::sort(nodes.begin(), nodes.end());
-        for (int32_t v : nodes) out[out_pos++] = v;
+        for (int32_t v : nodes) out[pos++] = v;
     }
 
-    // order the nodes of subset `nodes` (all carry label `lab`)
-    void run(std::vector<int32_t> nodes, int32_t lab) {
-        std::vector<int32_t> order;
-        while (true) {
-            if ((int64_t)nodes.size() <= leaf) {
-                emit(nodes);
-                return;
-            }
-            // split into connected components first (one linear pass over the subset)
-            bfs(nodes[0], lab, order);
-            if (order.size() < nodes.size()) {
-                std::vector<std::pair<int32_t, std::vector<int32_t>>> comps;
-                const int32_t stamp0 = cur_stamp;  // every BFS below gets a newer stamp
-                for (int32_t v : nodes) {
-                    if (label[v] != lab || stamp[v] > stamp0) continue;  // relabelled or seen
-                    if (stamp[v] == stamp0) {  // the component found by the first BFS
-                        comps.emplace_back(next_label++, order);
-                    } else {
-                        std::vector<int32_t> c;
-                        bfs(v, lab, c);
-                        comps.emplace_back(next_label++, std::move(c));
-                    }
-                    for (int32_t w : comps.back().second) label[w] = comps.back().first;
-                }
-                for (auto &c : comps) run(std::move(c.second), c.first);
-                return;
-            }
-            // pseudo-peripheral node
-            int32_t start = order.back();
-            int32_t ecc = bfs(start, lab, order);
-            for (int it = 0; it < 4; it++) {
-                int32_t cand = order.back();
-                std::vector<int32_t> o2;
-                int32_t e2 = bfs(cand, lab, o2);
-                if (e2 <= ecc) break;
-                ecc = e2, start = cand, order.swap(o2);
-            }
-            bfs(start, lab, order);
-            if (ecc < 2) {  // too shallow to dissect: order by minimum degree locally
-                emit(nodes);
-                return;
-            }
-            // level sizes; split at the level reaching half of the nodes
-            std::vector<int64_t> lsz(ecc + 1, 0);
-            for (int32_t v : order) lsz[dist[v]]++;
-            int64_t acc = 0, half = (int64_t)nodes.size() / 2;
-            int32_t s = 1;
-            for (int32_t l = 0; l <= ecc; l++) {
-                acc += lsz[l];
-                if (acc >= half) {
-                    s = l;
-                    break;
-                }
-            }
-            s = std::max<int32_t>(1, std::min<int32_t>(s, ecc - 1));
-            // separator: level-s nodes adjacent to level s+1 (the rest join part A)
-            int32_t la = next_label++, lb = next_label++, ls = next_label++;
-            std::vector<int32_t> a, b, sep;
-            for (int32_t v : order) {
-                int32_t d = dist[v];
-                if (d < s) a.push_back(v);
-                else if (d > s) b.push_back(v);
-                else {
-                    bool touches = false;
-                    for (int64_t p = g.ptr[v]; p < g.ptr[v + 1] && !touches; p++) {
-                        int32_t w = g.ind[p];
-                        touches = label[w] == lab && stamp[w] == cur_stamp && dist[w] == s + 1;
-                    }
-                    (touches ? sep : a).push_back(v);
-                }
-            }
-            for (int32_t v : a) label[v] = la;
-            for (int32_t v : b) label[v] = lb;
-            for (int32_t v : sep) label[v] = ls;
-            run(std::move(a), la);
-            run(std::move(b), lb);
-            emit(sep);
+    // a and b in parallel when both are large and a thread is spare
+    template <class FA, class FB>
+    void both(size_t na, FA fa, FB fb) {
+        if (na > 20000 && spare_threads.fetch_sub(1) > 0) {
+            std::thread t(fa);
+            fb();
+            t.join();
+            spare_threads.fetch_add(1);
             return;
+        }
+        if (na > 20000) spare_threads.fetch_add(1);
+        fa();
+        fb();
+    }
+
+    // order the nodes of subset `nodes` (all carry label `lab`) into out[pos, pos + |nodes|)
+    void run(std::vector<int32_t> nodes, int32_t lab, int64_t pos) {
+        std::vector<int32_t> order;
+        int32_t st = 0;
+        if ((int64_t)nodes.size() <= leaf) {
+            emit(nodes, pos);
+            return;
+        }
+        // split into connected components first (one linear pass over the subset)
+        bfs(nodes[0], lab, order, st);
+        if (order.size() < nodes.size()) {
+            std::vector<std::pair<int32_t, std::vector<int32_t>>> comps;
+            const int32_t stamp0 = st;  // this subset's later BFS get newer stamps
+            for (int32_t v : nodes) {
+                if (lab_of(v) != lab || (stamp[v] != stamp0 && stamp[v] > stamp0)) continue;  // relabelled or seen
+                int32_t c_st;
+                if (stamp[v] == stamp0) {  // the component found by the first BFS
+                    comps.emplace_back(next_label.fetch_add(1), order);
+                } else {
+                    std::vector<int32_t> c;
+                    bfs(v, lab, c, c_st);
+                    comps.emplace_back(next_label.fetch_add(1), std::move(c));
+                }
+                for (int32_t w : comps.back().second) set_lab(w, comps.back().first);
+            }
+            run_comps(comps, 0, pos);
+            return;
+        }
+        // pseudo-peripheral node
+        int32_t start = order.back();
+        int32_t ecc = bfs(start, lab, order, st);
+        for (int it = 0; it < 4; it++) {
+            int32_t cand = order.back();
+            std::vector<int32_t> o2;
+            int32_t st2;
+            int32_t e2 = bfs(cand, lab, o2, st2);
+            if (e2 <= ecc) break;
+            ecc = e2, start = cand, order.swap(o2);
+        }
+        bfs(start, lab, order, st);
+        if (ecc < 2) {  // too shallow to dissect
+            emit(nodes, pos);
+            return;
+        }
+        // level sizes; split at the level reaching half of the nodes
+        std::vector<int64_t> lsz(ecc + 1, 0);
+        for (int32_t v : order) lsz[dist[v]]++;
+        int64_t acc = 0, half = (int64_t)nodes.size() / 2;
+        int32_t s = 1;
+        for (int32_t l = 0; l <= ecc; l++) {
+            acc += lsz[l];
+            if (acc >= half) {
+                s = l;
+                break;
+            }
+        }
+        s = std::max<int32_t>(1, std::min<int32_t>(s, ecc - 1));
+        // separator: level-s nodes adjacent to level s+1 (the rest join part A)
+        const int32_t la = next_label.fetch_add(1), lb = next_label.fetch_add(1), ls = next_label.fetch_add(1);
+        std::vector<int32_t> a, b, sep;
+        for (int32_t v : order) {
+            int32_t d = dist[v];
+            if (d < s) a.push_back(v);
+            else if (d > s) b.push_back(v);
+            else {
+                bool touches = false;
+                for (int64_t p = g.ptr[v]; p < g.ptr[v + 1] && !touches; p++) {
+                    int32_t w = g.ind[p];
+                    touches = lab_of(w) == lab && stamp[w] == st && dist[w] == s + 1;
+                }
+                (touches ? sep : a).push_back(v);
+            }
+        }
+        for (int32_t v : a) set_lab(v, la);
+        for (int32_t v : b) set_lab(v, lb);
+        for (int32_t v : sep) set_lab(v, ls);
+        nodes.clear();
+        nodes.shrink_to_fit();
+        const int64_t pa = pos, pb = pos + (int64_t)a.size(), ps = pb + (int64_t)b.size();
+        emit(sep, ps);
+        const size_t na = std::min(a.size(), b.size());
+        both(na, [&] { run(std::move(a), la, pa); }, [&] { run(std::move(b), lb, pb); });
+    }
+
+    // components [i, end) into consecutive output ranges starting at pos
+    void run_comps(std::vector<std::pair<int32_t, std::vector<int32_t>>> &comps, size_t i, int64_t pos) {
+        for (; i < comps.size(); i++) {
+            const size_t sz = comps[i].second.size();
+            if (i + 1 < comps.size() && sz > 20000) {
+                auto &c = comps[i];
+                both(sz, [&] { run(std::move(c.second), c.first, pos); },
+                     [&, i] { run_comps(comps, i + 1, pos + (int64_t)sz); });
+                return;
+            }
+            run(std::move(comps[i].second), comps[i].first, pos);
+            pos += (int64_t)sz;
         }
     }
 };
 }  // namespace
 
+int host_threads() {
+    const char *e = getenv("CPK_THREADS");
+    if (!e) e = getenv("OMP_NUM_THREADS");
+    int t = e ? atoi(e) : 0;
+    if (t <= 0) t = (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(t, 64));
+}
+
 std::vector<int32_t> nested_dissection(const HCsr &g, int leaf_size) {
-    Nd nd(g, leaf_size);
+    Nd nd(g, leaf_size, host_threads());
     std::vector<int32_t> all(g.nrows);
     std::iota(all.begin(), all.end(), 0);
-    if (g.nrows) nd.run(std::move(all), 0);
-    return nd.out;
+    if (g.nrows) nd.run(std::move(all), 0, 0);
+    return std::move(nd.out);
 }
 
 std::vector<int32_t> order_kp(const HCsr &Kp, int64_t n, int *kind_out) {
