@@ -308,12 +308,12 @@ Factor relabel(const Factor &f, const Schedule &s, std::vector<int32_t> *src) {
     Factor g;
     g.N = N;
     g.perm.resize(N);
-    g.D.resize(N);
+    if (!f.D.empty()) g.D.resize(N);
     g.parent.assign(N, -1);
     for (int64_t q = 0; q < N; q++) {
         int32_t old = s.order[q];
         g.perm[q] = f.perm[old];
-        g.D[q] = f.D[old];
+        if (!f.D.empty()) g.D[q] = f.D[old];
         if (f.parent[old] >= 0) g.parent[q] = pos[f.parent[old]];
     }
     g.Lp.assign(N + 1, 0);

@@ -94,6 +94,7 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
             std::vector<int32_t> fsrc, bsrc;
             make_dfactor(an.F, pc->S, pc->dF, &key, nullptr, &fsrc, &bsrc);
             for (auto &q : fsrc) q = an.rsrc[q];  // relabelled slot -> exported (CSC) slot
+            for (auto &q : bsrc) q = an.rsrc[q];
             dldl_setup(pc->dl, an.sym, an.F0, fsrc, bsrc, pc->S.order);
         } else {
             make_dfactor(an.F, pc->S, pc->dF, &key);
