@@ -161,12 +161,22 @@ void launch_spmv_resid_norm(Ctx &c, const DMat &A, const double *xin, int64_t ne
 // y = A*x restricted to columns >= col_min (B'*v from the first n rows of Kp)
 void launch_spmv_colmask(Ctx &c, const DMat &A, int64_t col_min, const double *x, double *y, const int *run);
 // forward sweep w = L \ (P' * xin), backward sweep out (=|+=) P * (L' \ (D \ w))
+// sched_in: xin is already in schedule order (no perm gather, no negation)
 void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                       const int *active);
+                       const int *active, bool sched_in = false);
 // diagnostic: the forward sweep without its level phase (staging + write-back only)
 void launch_sptrsv_fwd_diag(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w);
+// out == null: the solution stays in schedule order in w (and with add, ys += it in place);
+// add with ys: out = P * (ys + solution), ys the previous solution in schedule order
 void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
-                       const int *active);
+                       const int *active, double *ys = nullptr);
+// r = xin(perm) - A*y with A = P'*Kp*P in schedule order (rows and columns), y in schedule
+// order; each row sums its entries in Kp's column order, so r(k) equals row perm(k) of the
+// original-order residual bit for bit
+void launch_spmv_resid_sched(Ctx &c, const DMat &A, const int32_t *perm, const double *xin, int64_t neg_from,
+                             const double *y, double *r, const int *run);
+// out[i] = x[idx[i]]
+void launch_gather(Ctx &c, const double *x, const int32_t *idx, int64_t n, double *out);
 // small vector helpers
 void launch_set_concat(Ctx &c, double *dst, const double *a, int64_t na, int64_t nb);  // dst = [a; 0]
 
@@ -270,6 +280,12 @@ struct Precond {
     DFactor dF;
     DBuf<double> w, r;   // permuted work vector, refinement residual
     DLdl dl;             // device numeric factorization (single GPU); dl.ready: F.Lx / F.D live on the device
+    // single GPU, forced refinement: Kp permuted into schedule order (P'*Kp*P, each row's
+    // entries in Kp's order) so the refinement residual, the forward sweep's input and the
+    // accumulated solution all stay in schedule order (apply); kps_from: Kps entry -> Kp entry
+    DMat dKps;
+    DBuf<int32_t> kps_from;
+    DBuf<double> w2;     // work vector of the refinement solves (w keeps the first solution)
     uint64_t pattern_hash = 0;  // sparsity of (A11, B, C22): a refactorization must keep it
     DBuf<int> active;    // refinement predicate
     // public properties of opLDL2 (opLDL2.m:45-50)
@@ -291,6 +307,9 @@ struct Precond {
     // apply every rank finds rank r's values at sep.rbuf[r * sep.kt + sep.kt_data + j]
     void apply(const double *x, int64_t neg_from, double *y, const int *run, const double *piggy_src = nullptr);
     bool piggyback_ok() const { return dist && sep.kt > 0; }
+    // the schedule-order refinement path (single GPU; CPK_NO_SCHED_RESID=1 forces the plain one)
+    bool sched_path() const { return !dist && dKps.nnz > 0 && !no_sched; }
+    bool no_sched = false;
     void set_handle(bool on);  // enabling or disabling clears the state
     void ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run, const int *act,
                    const double *piggy_src = nullptr);

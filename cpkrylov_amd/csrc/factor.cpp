@@ -322,7 +322,7 @@ Factor relabel(const Factor &f, const Schedule &s, std::vector<int32_t> *src) {
         g.Lp[q + 1] = g.Lp[q] + (f.Lp[old + 1] - f.Lp[old]);
     }
     g.Li.resize(f.Li.size());
-    const bool vals = !f.Lx.empty();
+    const bool vals = (int64_t)f.D.size() == N;  // numeric factor (Lx may be empty: no entries)
     if (vals) g.Lx.resize(f.Lx.size());
     if (src) src->resize(f.Li.size());
     std::vector<std::pair<int32_t, int64_t>> col;

@@ -69,7 +69,9 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     if (extra)
         for (const auto &e : *extra) nextra += (int64_t)e.size();
     if (extra && bsrc) throw Error(CPK_ERR_UNSUPPORTED, "internal: entry sources with extra backward entries");
-    const bool vals = !f.Lx.empty();  // structure-only factor: values come from the device numeric phase
+    // structure-only factor (no D): values come from the device numeric phase.  Not f.Lx: a
+    // numeric factor without off-diagonal entries has an empty Lx but a valid D
+    const bool vals = (int64_t)f.D.size() == f.N;
     d.N = N;
     d.nnz = (int64_t)f.Li.size() + nextra;
     if (d.nnz > (int64_t)INT32_MAX) throw Error(CPK_ERR_UNSUPPORTED, "factor has more than 2^31 entries");
@@ -191,6 +193,22 @@ struct EpiResid {
     }
     __device__ void finish() {}
 };
+struct EpiResidSched {  // r(k) = xin(perm(k)) - (A y)(k), A and y in schedule order
+    const double *xin;
+    const int32_t *perm;
+    int64_t neg_from;
+    double *r;
+    const int *run;
+    __device__ bool skip() const { return run && *run == 0; }
+    __device__ const double *xvec(const double *x) const { return x; }
+    __device__ double pre(int64_t i) const {
+        const int32_t s = perm[i];
+        const double x = xin[s];
+        return s >= neg_from ? -x : x;
+    }
+    __device__ void row(int64_t i, double acc, double xi) { r[i] = xi - acc; }
+    __device__ void finish() {}
+};
 struct EpiResidNorm {
     const double *xin;
     int64_t neg_from;
@@ -242,7 +260,7 @@ __global__ void gather_kernel(const double *__restrict__ x, const int32_t *__res
         out[i] = x[idx[i]];
 }
 
-static void launch_gather(Ctx &c, const double *x, const int32_t *idx, int64_t n, double *out) {
+void launch_gather(Ctx &c, const double *x, const int32_t *idx, int64_t n, double *out) {
     if (n <= 0) return;
     const int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
     hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(256), 0, c.stream, x, idx, n, out);
@@ -296,6 +314,12 @@ void launch_spmv_resid(Ctx &c, const DMat &A, const double *xin, int64_t neg_fro
     launch_halo(c, A, y);
     if (!A.nblk) return;
     spmv_launch(c, A, y, 0, EpiResid{xin, neg_from, r, run, active});
+}
+
+void launch_spmv_resid_sched(Ctx &c, const DMat &A, const int32_t *perm, const double *xin, int64_t neg_from,
+                             const double *y, double *r, const int *run) {
+    if (!A.nblk) return;
+    spmv_launch(c, A, y, 0, EpiResidSched{xin, perm, neg_from, r, run});
 }
 
 // the refinement predicate from the allreduced (|r|^2, |x|^2) (distributed mode)
@@ -876,12 +900,26 @@ __device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_firs
     }
 }
 
+// Backward write-back of row k (schedule order) with value z:
+//   out != null: out[perm[k]] = z, or (ADD) base + z with base = ys[k] when ys is given (the
+//                previous solution kept in schedule order), else out[perm[k]];
+//   out == null: the solution stays in schedule order (w), and (ADD) ys[k] += z in place.
+template <bool ADD>
+__device__ __forceinline__ void bwd_store(double *out, double *ys, const int32_t *perm, int64_t k, double z) {
+    if (out) {
+        const int32_t dst = perm[k];
+        out[dst] = ADD ? (ys ? ys[k] : out[dst]) + z : z;
+    } else if (ADD) {
+        ys[k] = ys[k] + z;
+    }
+}
+
 template <int TPB, int MODE = 0>  // MODE 1 (diagnostic): staging + write-back only, no level phase
 __global__ __launch_bounds__(TPB) void sptrsv_fwd_kernel(
     int64_t blk0, int R, int CAP, int skip_first, const int32_t *__restrict__ blk_lvl, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from, double *w,
-    const int *run, const int *active) {
+    const int *run, const int *active, int sched_in) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
     const int64_t b = blk0 + blockIdx.x;
@@ -895,7 +933,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_fwd_kernel(
 #pragma unroll 4
         for (int i = tid; i < nr; i += TPB) {
             S.p[i] = (int16_t)(ptr[r0 + i] - e0);
-            const int32_t src = perm[r0 + i];
+            const int32_t src = sched_in ? r0 + i : perm[r0 + i];
             const double x = xin[src];
             S.w[i] = (src >= neg_from) ? -x : x;
         }
@@ -924,7 +962,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_fwd_kernel(
     for (int l = l0; l < l1; l++) {  // direct path: oversized block
         const int a = lvl_row[l], z = lvl_row[l + 1];
         for (int k = a + tid; k < z; k += TPB) {
-            const int32_t src = perm[k];
+            const int32_t src = sched_in ? k : perm[k];
             double acc = xin[src];
             if (src >= neg_from) acc = -acc;
             const uint32_t q1 = ptr[k + 1];
@@ -940,7 +978,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_bwd_kernel(
     int64_t blk0, int R, int CAP, const int32_t *__restrict__ blk_lvl, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, double *w, double *out, const int *run,
-    const int *active) {
+    const int *active, double *ys) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
     const int64_t b = blk0 + blockIdx.x;
@@ -972,8 +1010,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_bwd_kernel(
         for (int i = tid; i < nr; i += TPB) {
             const double z = S.w[i];
             w[r0 + i] = z;
-            const int32_t dst = perm[r0 + i];
-            out[dst] = ADD ? out[dst] + z : z;
+            bwd_store<ADD>(out, ys, perm, r0 + i, z);
         }
         return;
     }
@@ -984,9 +1021,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_bwd_kernel(
             const uint32_t q1 = ptr[k + 1];
             for (uint32_t e = ptr[k]; e < q1; e++) acc -= val[e] * w[col[e]];
             w[k] = acc;
-            const int32_t dst = perm[k];
-            if (ADD) out[dst] = out[dst] + acc;
-            else out[dst] = acc;
+            bwd_store<ADD>(out, ys, perm, k, acc);
         }
         __syncthreads();
     }
@@ -1015,7 +1050,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
     int64_t blk0, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
-    double *w, double *out, const int *run, const int *active) {
+    double *w, double *out, const int *run, const int *active, int sched_in, double *ys) {
     constexpr int R = RPU * TPB, CAP = EPU * TPB;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
@@ -1033,7 +1068,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
 #pragma unroll
     for (int j = 0; j < RPU; j++) {
         const int i = tid + j * TPB, rr = r0 + (i < nr ? i : nr - 1);
-        q[j] = ptr[rr], sp[j] = perm[rr];
+        q[j] = ptr[rr], sp[j] = (BWD ? out != nullptr : !sched_in) ? perm[rr] : rr;
         if (BWD) a[j] = w[rr], d[j] = D[rr];
     }
 #pragma unroll
@@ -1080,14 +1115,18 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
         if (i < nr) {
             const double z = S.w[i];
             w[r0 + i] = z;
-            if (BWD) out[sp[j]] = ADD ? out[sp[j]] + z : z;
+            if (BWD) {
+                if (out) out[sp[j]] = ADD ? (ys ? ys[r0 + i] : out[sp[j]]) + z : z;
+                else if (ADD) ys[r0 + i] = ys[r0 + i] + z;
+            }
         }
     }
 }
 
 // upper round r through sptrsv_upper_kernel when the configuration matches an instantiation
 static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add, const double *xin,
-                        int64_t neg_from, double *w, double *out, const int *run, const int *active) {
+                        int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in,
+                        double *ys) {
     constexpr int TPB = 512, RPU = 2, EPU = 8;
     if (getenv("CPK_NO_UPPER") || F.sweep_threads[1] != TPB || F.sweep_rows[1] > RPU * TPB ||
         F.sweep_cap[1] > EPU * TPB || r >= (int64_t)F.round_fits.size() || !F.round_fits[r])
@@ -1099,15 +1138,15 @@ static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add,
     if (!bwd)
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, false, false>), dim3((unsigned)nb), dim3(TPB), lds,
                            c.stream, b0, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active);
+                           neg_from, w, out, run, active, sched_in, ys);
     else if (add)
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, true>), dim3((unsigned)nb), dim3(TPB), lds,
                            c.stream, b0, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active);
+                           neg_from, w, out, run, active, sched_in, ys);
     else
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, false>), dim3((unsigned)nb), dim3(TPB), lds,
                            c.stream, b0, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active);
+                           neg_from, w, out, run, active, sched_in, ys);
     return true;
 }
 
@@ -1120,8 +1159,11 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     int64_t blk0, int64_t nblk, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,
-    int64_t neg_from, double *w, double *out, const int *run, const int *active) {
+    int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in, double *ys) {
     static_assert(SPLIT == 1 || TPB * SPLIT == 64, "split blocks must share one wave");
+    // perm is read for the forward gather (unless the input is in schedule order) and for the
+    // backward scatter (unless the solution stays in schedule order)
+    const bool need_perm = BWD ? out != nullptr : !sched_in;
     constexpr int R = RPT * TPB, CAP = EPT * TPB;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
@@ -1144,7 +1186,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
             const int i = tid + j * TPB;
             const int rr = m.r0 + (i < nr ? i : nr - 1);  // clamped: later gathers need no predicate
             q[j] = ptr[rr];
-            sp[j] = perm[rr];
+            sp[j] = need_perm ? perm[rr] : rr;
             if (BWD) wr[j] = w[rr], dr[j] = D[rr];
             if (i < nl) lvr[j] = lvl_row[m.l0 + i];
         }
@@ -1170,8 +1212,9 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
         double xg[RPT];
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
+            const int i = tid + j * TPB;
             if (!BWD) xg[j] = xin[sp[j]];
-            if (BWD && ADD) xg[j] = out[sp[j]];
+            if (BWD && ADD) xg[j] = ys ? ys[r0 + (i < nr ? i : nr - 1)] : out[sp[j]];
         }
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
@@ -1221,7 +1264,10 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
             if (i < nr) {
                 const double z = S.w[i];
                 w[r0 + i] = z;
-                if (BWD) out[dst[j]] = ADD ? xg[j] + z : z;
+                if (BWD) {
+                    if (out) out[dst[j]] = ADD ? xg[j] + z : z;
+                    else if (ADD) ys[r0 + i] = xg[j] + z;
+                }
             }
         }
         if (bn >= bend) break;
@@ -1235,7 +1281,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
 // per 64-lane wave
 template <int TPB, int RPT, int EPT, int SPLIT = 1>
 static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
-                       double *w, double *out, const int *run, const int *active) {
+                       double *w, double *out, const int *run, const int *active, int sched_in, double *ys) {
     if (F.sweep_threads[0] != TPB || F.sweep_rows[0] != RPT * TPB || F.sweep_cap[0] != EPT * TPB) return false;
     const int64_t nb = F.round_ptr[1] - F.round_ptr[0];
     const size_t lds = sweep_lds_bytes(RPT * TPB, EPT * TPB) * SPLIT;
@@ -1253,105 +1299,111 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
     if (!bwd)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active);
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys);
     else if (add)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active);
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys);
     else
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active);
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys);
     return true;
 }
 
 // round 0 through the pipelined kernel when its configuration is one of the instantiated ones
 static bool pipe_round0(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
-                        double *w, double *out, const int *run, const int *active) {
+                        double *w, double *out, const int *run, const int *active, int sched_in, double *ys) {
     if (!F.pipelined || F.round_ptr.size() < 2) return false;
-    return pipe_round<32, 6, 18, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
-           pipe_round<32, 4, 12, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
-           pipe_round<32, 8, 24, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
-           pipe_round<128, 2, 6>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
-           pipe_round<64, 3, 9>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
-           pipe_round<64, 4, 12>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
-           pipe_round<64, 6, 18>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
-           pipe_round<64, 8, 24>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
-           pipe_round<128, 1, 4>(c, F, bwd, add, xin, neg_from, w, out, run, active) ||
-           pipe_round<256, 1, 3>(c, F, bwd, add, xin, neg_from, w, out, run, active);
+    return pipe_round<32, 6, 18, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
+           pipe_round<32, 4, 12, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
+           pipe_round<32, 8, 24, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
+           pipe_round<128, 2, 6>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
+           pipe_round<64, 3, 9>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
+           pipe_round<64, 4, 12>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
+           pipe_round<64, 6, 18>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
+           pipe_round<64, 8, 24>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
+           pipe_round<128, 1, 4>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
+           pipe_round<256, 1, 3>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys);
 }
 
 template <int TPB, int MODE>
 static void fwd_round(Ctx &c, const DFactor &F, int64_t r, const double *xin, int64_t neg_from, double *w,
-                      const int *run, const int *active) {
+                      const int *run, const int *active, int sched_in) {
     const int i = r == 0 ? 0 : 1;
     const int64_t b0 = F.round_ptr[r], nb = F.round_ptr[r + 1] - b0;
     if (!nb) return;
     hipLaunchKernelGGL((sptrsv_fwd_kernel<TPB, MODE>), dim3((unsigned)nb), dim3(TPB),
                        sweep_lds_bytes(F.sweep_rows[i], F.sweep_cap[i]), c.stream, b0, F.sweep_rows[i],
                        F.sweep_cap[i], r == 0 ? 1 : 0, F.blk_lvl.p, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.perm.p,
-                       xin, neg_from, w, run, active);
+                       xin, neg_from, w, run, active, sched_in);
 }
 
 template <int TPB, bool ADD>
 static void bwd_round(Ctx &c, const DFactor &F, int64_t r, double *w, double *out, const int *run,
-                      const int *active) {
+                      const int *active, double *ys) {
     const int i = r == 0 ? 0 : 1;
     const int64_t b0 = F.round_ptr[r], nb = F.round_ptr[r + 1] - b0;
     if (!nb) return;
     hipLaunchKernelGGL((sptrsv_bwd_kernel<TPB, ADD>), dim3((unsigned)nb), dim3(TPB),
                        sweep_lds_bytes(F.sweep_rows[i], F.sweep_cap[i]), c.stream, b0, F.sweep_rows[i],
                        F.sweep_cap[i], F.blk_lvl.p, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, w,
-                       out, run, active);
+                       out, run, active, ys);
 }
 
 template <int MODE>
 static void fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                    const int *active) {
+                    const int *active, int sched_in) {
     const int64_t R = (int64_t)F.round_ptr.size() - 1;
     for (int64_t r = 0; r < R; r++) {
-        if (r == 0 && MODE == 0 && pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active)) continue;
-        if (r > 0 && MODE == 0 && upper_round(c, F, r, false, false, xin, neg_from, w, nullptr, run, active)) continue;
+        if (r == 0 && MODE == 0 &&
+            pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr))
+            continue;
+        if (r > 0 && MODE == 0 &&
+            upper_round(c, F, r, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr))
+            continue;
         switch (F.sweep_threads[r == 0 ? 0 : 1]) {
-        case 32: fwd_round<32, MODE>(c, F, r, xin, neg_from, w, run, active); break;
-        case 64: fwd_round<64, MODE>(c, F, r, xin, neg_from, w, run, active); break;
-        case 128: fwd_round<128, MODE>(c, F, r, xin, neg_from, w, run, active); break;
-        case 512: fwd_round<512, MODE>(c, F, r, xin, neg_from, w, run, active); break;
-        case 1024: fwd_round<1024, MODE>(c, F, r, xin, neg_from, w, run, active); break;
-        default: fwd_round<256, MODE>(c, F, r, xin, neg_from, w, run, active); break;
+        case 32: fwd_round<32, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in); break;
+        case 64: fwd_round<64, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in); break;
+        case 128: fwd_round<128, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in); break;
+        case 512: fwd_round<512, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in); break;
+        case 1024: fwd_round<1024, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in); break;
+        default: fwd_round<256, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in); break;
         }
     }
     CPK_HIP(hipGetLastError());
 }
 
 void launch_sptrsv_fwd_diag(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w) {
-    fwd_all<1>(c, F, xin, neg_from, w, nullptr, nullptr);
+    fwd_all<1>(c, F, xin, neg_from, w, nullptr, nullptr, 0);
 }
 
 void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                       const int *active) {
-    fwd_all<0>(c, F, xin, neg_from, w, run, active);
+                       const int *active, bool sched_in) {
+    // schedule-order input: no perm gather and no negation (neg_from applies to original indices)
+    fwd_all<0>(c, F, xin, sched_in ? INT64_MAX : neg_from, w, run, active, sched_in ? 1 : 0);
 }
 
 void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
-                       const int *active) {
+                       const int *active, double *ys) {
+    if (!out && add && !ys) throw Error(CPK_ERR_ARGS, "internal: accumulating backward sweep without a base");
     const int64_t R = (int64_t)F.round_ptr.size() - 1;
     for (int64_t r = R - 1; r >= 0; r--) {
-        if (r == 0 && pipe_round0(c, F, true, add, nullptr, 0, w, out, run, active)) continue;
-        if (r > 0 && upper_round(c, F, r, true, add, nullptr, 0, w, out, run, active)) continue;
+        if (r == 0 && pipe_round0(c, F, true, add, nullptr, 0, w, out, run, active, 0, ys)) continue;
+        if (r > 0 && upper_round(c, F, r, true, add, nullptr, 0, w, out, run, active, 0, ys)) continue;
         switch (F.sweep_threads[r == 0 ? 0 : 1] * 2 + (add ? 1 : 0)) {
-        case 64: bwd_round<32, false>(c, F, r, w, out, run, active); break;
-        case 65: bwd_round<32, true>(c, F, r, w, out, run, active); break;
-        case 128: bwd_round<64, false>(c, F, r, w, out, run, active); break;
-        case 129: bwd_round<64, true>(c, F, r, w, out, run, active); break;
-        case 256: bwd_round<128, false>(c, F, r, w, out, run, active); break;
-        case 257: bwd_round<128, true>(c, F, r, w, out, run, active); break;
-        case 1024: bwd_round<512, false>(c, F, r, w, out, run, active); break;
-        case 1025: bwd_round<512, true>(c, F, r, w, out, run, active); break;
-        case 2048: bwd_round<1024, false>(c, F, r, w, out, run, active); break;
-        case 2049: bwd_round<1024, true>(c, F, r, w, out, run, active); break;
-        case 513: bwd_round<256, true>(c, F, r, w, out, run, active); break;
-        default: bwd_round<256, false>(c, F, r, w, out, run, active); break;
+        case 64: bwd_round<32, false>(c, F, r, w, out, run, active, ys); break;
+        case 65: bwd_round<32, true>(c, F, r, w, out, run, active, ys); break;
+        case 128: bwd_round<64, false>(c, F, r, w, out, run, active, ys); break;
+        case 129: bwd_round<64, true>(c, F, r, w, out, run, active, ys); break;
+        case 256: bwd_round<128, false>(c, F, r, w, out, run, active, ys); break;
+        case 257: bwd_round<128, true>(c, F, r, w, out, run, active, ys); break;
+        case 1024: bwd_round<512, false>(c, F, r, w, out, run, active, ys); break;
+        case 1025: bwd_round<512, true>(c, F, r, w, out, run, active, ys); break;
+        case 2048: bwd_round<1024, false>(c, F, r, w, out, run, active, ys); break;
+        case 2049: bwd_round<1024, true>(c, F, r, w, out, run, active, ys); break;
+        case 513: bwd_round<256, true>(c, F, r, w, out, run, active, ys); break;
+        default: bwd_round<256, false>(c, F, r, w, out, run, active, ys); break;
         }
     }
     CPK_HIP(hipGetLastError());

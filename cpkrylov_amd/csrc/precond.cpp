@@ -106,9 +106,36 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
         CPK_HIP(hipStreamSynchronize(c.stream));
         clk.lap("numeric factorization (device)");
     }
+    pc->no_sched = getenv("CPK_NO_SCHED_RESID") != nullptr;
+    if (pc->Kp.nnz() <= (int64_t)INT32_MAX) {
+        // Kp in schedule order: row q = Kp row perm_s[q] with its entries in Kp's order, columns
+        // renumbered to schedule positions (perm_s = the relabelled factor's pivot order)
+        const std::vector<int32_t> &ps = an.F.perm;
+        const int64_t N = pc->N;
+        std::vector<int32_t> pos(N);
+        for (int64_t q = 0; q < N; q++) pos[ps[q]] = (int32_t)q;
+        HCsr ks;
+        ks.nrows = ks.ncols = N;
+        ks.ptr.assign(N + 1, 0);
+        for (int64_t q = 0; q < N; q++) ks.ptr[q + 1] = ks.ptr[q] + (pc->Kp.ptr[ps[q] + 1] - pc->Kp.ptr[ps[q]]);
+        ks.ind.resize(pc->Kp.nnz());
+        ks.val.resize(pc->Kp.nnz());
+        std::vector<int32_t> from(pc->Kp.nnz());
+        parallel_for(N, [&](int64_t lo, int64_t hi) {
+            for (int64_t q = lo; q < hi; q++) {
+                int64_t t = ks.ptr[q];
+                for (int64_t p = pc->Kp.ptr[ps[q]]; p < pc->Kp.ptr[ps[q] + 1]; p++, t++)
+                    ks.ind[t] = pos[pc->Kp.ind[p]], ks.val[t] = pc->Kp.val[p], from[t] = (int32_t)p;
+            }
+        });
+        make_dmat(ks, pc->dKps);
+        pc->kps_from.upload(from);
+    }
+    clk.lap("schedule-order Kp");
     an.F = Factor();
     pc->F = std::move(an.F0);
     pc->w.alloc(pc->N);
+    pc->w2.alloc(pc->N);
     pc->r.alloc(pc->N);
     pc->active.alloc(1);
     c.ensure_partials(std::max<size_t>(pc->dKp.nblk * 2, 4096));
@@ -224,6 +251,7 @@ double precond_refactor(Precond &p, const DMat &A11, const DMat &B, const DMat &
     auto t0 = std::chrono::steady_clock::now();
     Ctx &c = *p.ctx;
     dldl_assemble_kp(c, p.dl, A11.val.p, B.val.p, C22.val.p, p.dKp.val.p);
+    if (p.dKps.nnz) launch_gather(c, p.dKp.val.p, p.kps_from.p, p.dKps.nnz, p.dKps.val.p);
     dldl_factor(c, p.dl, p.dKp.val.p, p.dF);
     // the host copy of Kp follows (divide / export read the device copies; the distributed
     // shift rows, built from the host copy, do not exist on one GPU)
@@ -266,6 +294,10 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
         launch_sub_state(c, x, neg_from, ghn.p, N, t.p, run);
         ldl_solve(t.p, N, y, false, run, nullptr, piggy_src);
         launch_spmv_colmask(c, dKp, n, y, ghn.p, run);
+    } else if (nitref >= 1 && force_itref != 0 && sched_path()) {
+        // y = op.LDL * x kept in schedule order (w) for the refinement below: no scatter
+        launch_sptrsv_fwd(c, dF, x, neg_from, w.p, run, nullptr);
+        launch_sptrsv_bwd(c, dF, w.p, nullptr, false, run, nullptr);
     } else {
         // y = op.LDL * x   (opLDL2.m:165-167); the residual-update branch subtracts the zero
         // state of a value object and its SpMVs are dead: skipped
@@ -273,6 +305,16 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
     }
     if (nitref <= 0) return;
     const int64_t steps = (int64_t)nitref;
+    if (force_itref != 0 && sched_path()) {
+        // every step runs and the norms are dead; everything stays in schedule order until the
+        // last backward sweep scatters y = P * (ys + dy)
+        for (int64_t s = 0; s < steps; s++) {
+            launch_spmv_resid_sched(c, dKps, dF.perm.p, x, neg_from, w.p, r.p, run);  // r = x - op.A*y
+            launch_sptrsv_fwd(c, dF, r.p, N, w2.p, run, nullptr, true);
+            launch_sptrsv_bwd(c, dF, w2.p, s + 1 == steps ? y : nullptr, true, run, nullptr, w.p);  // y += op.LDL*r
+        }
+        return;
+    }
     if (force_itref != 0) {
         // every step runs; rNorm/xNorm and the final residual are dead
         for (int64_t s = 0; s < steps; s++) {
@@ -298,8 +340,21 @@ double Precond::apply_bytes() const {
     const double fwd = 12 * l + 4 * (Nn + 1) + 16 * Nn + 4 * Nn;
     const double bwd = 12 * l + 4 * (Nn + 1) + 16 * Nn + 4 * Nn + 8 * Nn + 8 * Nn;
     const double kp = 12 * (double)dKp.nnz + 4 * (Nn + 1) + 8 * Nn /*y*/ + 8 * Nn /*x*/ + 8 * Nn /*r*/;
-    double b = fwd + bwd;
     const int64_t steps = nitref > 0 ? (int64_t)nitref : 0;
+    if (steps && force_itref != 0 && sched_path() && !(residual_update != 0 && handle)) {
+        // schedule-order path: the first backward sweep keeps its solution (no perm, no
+        // scatter); the residual gathers x through perm; the refinement forward sweeps read it
+        // contiguously (no perm); each refinement backward sweep reads ys contiguously and only
+        // the last scatters
+        const double bwd_keep = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn;
+        const double kps = 12 * (double)dKps.nnz + 4 * (Nn + 1) + 8 * Nn /*y*/ + 12 * Nn /*x(perm)*/ + 8 * Nn /*r*/;
+        const double fwd_s = 12 * l + 4 * (Nn + 1) + 16 * Nn;
+        const double bwd_acc = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn + 8 * Nn /*ys*/;
+        double b = fwd + bwd_keep + steps * (kps + fwd_s + bwd_acc) + (4 + 8) * Nn /*last: perm + scatter*/ +
+                   (steps - 1) * 8.0 * Nn /*ys written back in place*/;
+        return b;
+    }
+    double b = fwd + bwd;
     b += steps * (kp + fwd + bwd + 8 * Nn);
     return b + ghn_bytes;
 }

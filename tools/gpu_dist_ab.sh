@@ -1,11 +1,8 @@
-# per-rank timing of a P-way split for library variants (libcpk_<v>.so)
-set -e
+# bisect the distributed apply tests over tree snapshots under tools/ab
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-RUNS=${RUNS:-8:0}
-for v in "$@"; do
-  if [ "$v" = default ]; then lib=cpkrylov_amd/libcpk.so; else lib=cpkrylov_amd/libcpk_$v.so; fi
-  echo "== $v" >> gpurun_out/dist_ab.log
-  CPK_LIB_PATH=$PWD/$lib timeout -k 10 300 python -u tools/dist_timing.py $RUNS 2>&1 | grep "^{" >> gpurun_out/dist_ab.log
+for t in tools/ab/t_*; do
+  (cd $t && timeout -k 10 120 python -u -m pytest tests/test_gpu_dist.py -q -k "test_dist_apply_bitexact and cvxqp1_m" --timeout 60 --timeout-method thread > $GRAFT_REPO_ROOT/gpurun_out/dist_$(basename $t).log 2>&1)
+  echo "$t rc=$?"
 done
