@@ -1839,8 +1839,13 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
     const double Nn = (double)N, l = (double)M.dF.nnz;
     out->spmv_ms = timeit([&]() { launch_spmv(c, AC, x.p, y.p, nullptr); });
     out->spmv_bytes = 12.0 * AC.nnz + 4.0 * (Nn + 1) + 8.0 * Nn + 8.0 * Nn;
-    out->resid_ms = timeit([&]() { launch_spmv_resid(c, M.dKp, x.p, M.n, y.p, z.p, nullptr, nullptr); });
-    out->resid_bytes = 12.0 * M.dKp.nnz + 4.0 * (Nn + 1) + 8.0 * Nn /*y*/ + 8.0 * Nn /*x*/ + 8.0 * Nn /*r*/;
+    if (M.sched_path()) {  // the refinement residual the apply runs: Kp in schedule order, x through perm
+        out->resid_ms = timeit([&]() { launch_spmv_resid_sched(c, M.dKps, M.dF.perm.p, x.p, M.n, y.p, z.p, nullptr); });
+        out->resid_bytes = 12.0 * M.dKps.nnz + 4.0 * (Nn + 1) + 8.0 * Nn /*y*/ + 12.0 * Nn /*x, perm*/ + 8.0 * Nn /*r*/;
+    } else {
+        out->resid_ms = timeit([&]() { launch_spmv_resid(c, M.dKp, x.p, M.n, y.p, z.p, nullptr, nullptr); });
+        out->resid_bytes = 12.0 * M.dKp.nnz + 4.0 * (Nn + 1) + 8.0 * Nn /*y*/ + 8.0 * Nn /*x*/ + 8.0 * Nn /*r*/;
+    }
     if (getenv("CPK_PROFILE_FWD_NOLEVELS"))
         out->fwd_ms = timeit([&]() { launch_sptrsv_fwd_diag(c, M.dF, x.p, M.n, M.w.p); });
     else
