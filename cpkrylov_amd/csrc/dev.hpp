@@ -107,6 +107,7 @@ void launch_halo(Ctx &c, const DMat &A, const double *x);
 // HBM-resident factor + sweep schedule (rows in schedule order).
 struct DFactor {
     int64_t N = 0, nnz = 0, nblk = 0, nlvl = 0;
+    int64_t ndet = 0;     // detached rows [0, ndet): no forward entries, in no block (Schedule::ndet)
     DBuf<uint32_t> fptr;  // forward rows of strict lower L, columns ascending
     DBuf<int32_t> fcol;
     DBuf<double> fval;
@@ -285,7 +286,6 @@ struct Precond {
     // accumulated solution all stay in schedule order (apply); kps_from: Kps entry -> Kp entry
     DMat dKps;
     DBuf<int32_t> kps_from;
-    DBuf<double> w2;     // work vector of the refinement solves (w keeps the first solution)
     uint64_t pattern_hash = 0;  // sparsity of (A11, B, C22): a refactorization must keep it
     DBuf<int> active;    // refinement predicate
     // public properties of opLDL2 (opLDL2.m:45-50)

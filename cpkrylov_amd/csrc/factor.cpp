@@ -2,6 +2,7 @@
 // [L,D,P] = ldl(op.A), ops/opLDL2.m:82) and the block/round schedule for the device
 // triangular sweeps that replace op.LDL = P*inv(L')*inv(D)*inv(L)*P' (ops/opLDL2.m:86).
 #include <algorithm>
+#include <cstdlib>
 #include <numeric>
 
 #include "cpk.h"
@@ -139,11 +140,12 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     // Node weights: a block is staged in LDS when it holds at most R rows, at most CAP forward
     // entries (rows of L) and at most CAP backward entries (columns of L).  With
     // wt(v) = max(CAP/R, fwd(v), bwd(v)), a cluster of total weight <= CAP meets all three.
-    std::vector<int64_t> ent(N), wt0(N), wt1(N);
+    std::vector<int64_t> ent(N), wt0(N), wt1(N), ent_fwd;
     {
         const int64_t u0 = std::max<int64_t>(1, CAP0 / std::max<int64_t>(R0, 1));
         const int64_t u1 = std::max<int64_t>(1, CAP1 / std::max<int64_t>(R1, 1));
-        std::vector<int64_t> fl(N, 0);
+        std::vector<int64_t> &fl = ent_fwd;
+        fl.assign(N, 0);
         for (int32_t i : f.Li) fl[i]++;
         for (int64_t v = 0; v < N; v++) {
             ent[v] = std::max(fl[v], f.Lp[v + 1] - f.Lp[v] + (extra_bwd ? (*extra_bwd)[v] : 0));
@@ -173,9 +175,20 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     // (1) Layer peeling: round r takes the maximal subtrees of at most R rows of the tree that
     //     remains after rounds 0..r-1.  On bushy (nested-dissection) trees the remainder
     //     shrinks geometrically and a few rounds suffice.
-    std::vector<int32_t> alive(N);
-    std::iota(alive.begin(), alive.end(), 0);
-    std::vector<char> is_alive(N, 1);
+    // Detached rows: rows of L without entries (the G pivots of a G-first ordering, leaves of the
+    // elimination tree).  Their forward value is their input and nothing reads them before the
+    // backward sweep's last step, so they stay out of the blocks: they come first in the new
+    // order and are solved by one streaming pass per sweep (DFactor::ndet), and the blocks hold
+    // only rows whose levels do work.  CPK_NO_DETACH keeps them in the blocks.
+    std::vector<char> detached(N, 0);
+    if (!getenv("CPK_NO_DETACH"))
+        for (int64_t v = 0; v < N; v++) detached[v] = ent_fwd[v] == 0;
+    std::vector<int32_t> alive;
+    alive.reserve(N);
+    for (int64_t v = 0; v < N; v++)
+        if (!detached[v]) alive.push_back((int32_t)v);
+    std::vector<char> is_alive(N, 0);
+    for (int32_t v : alive) is_alive[v] = 1;
     std::vector<int64_t> sz(N, 0);
     std::vector<int32_t> root_of(N, -1);
     int32_t round = 0;
@@ -238,10 +251,12 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
         if (f.parent[v] < 0) closed_round[v] = dep + 1;
     }
     // cluster membership (top-down): a non-root joins its parent's cluster
-    std::vector<int32_t> cl(N);
-    for (int64_t v = N - 1; v >= 0; v--) cl[v] = closed_round[v] >= 0 ? (int32_t)v : cl[f.parent[v]];
+    std::vector<int32_t> cl(N, -1);
+    for (int64_t v = N - 1; v >= 0; v--)
+        if (!detached[v]) cl[v] = closed_round[v] >= 0 ? (int32_t)v : cl[f.parent[v]];
     std::vector<int64_t> csize(N, 0);
-    for (int64_t v = 0; v < N; v++) csize[cl[v]] += (closed_round[cl[v]] == 0 ? wt0[v] : wt1[v]);
+    for (int64_t v = 0; v < N; v++)
+        if (cl[v] >= 0) csize[cl[v]] += (closed_round[cl[v]] == 0 ? wt0[v] : wt1[v]);
     int32_t nrounds = 0;
     for (int64_t v = 0; v < N; v++)
         if (closed_round[v] >= 0) nrounds = std::max(nrounds, closed_round[v] + 1);
@@ -265,24 +280,27 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
         }
         s.round_ptr.push_back(nb);
     }
-    std::vector<int32_t> block(N);
-    for (int64_t v = 0; v < N; v++) block[v] = cluster_block[cl[v]];
+    std::vector<int32_t> block(N, -1);  // -1: detached
+    for (int64_t v = 0; v < N; v++)
+        if (cl[v] >= 0) block[v] = cluster_block[cl[v]];
     // intra-block levels (CSC columns ascend, so level[j] is final when column j is visited)
     std::vector<int32_t> level(N, 0);
     for (int64_t j = 0; j < N; j++)
         for (int64_t p = f.Lp[j]; p < f.Lp[j + 1]; p++) {
             const int32_t i = f.Li[p];
-            if (block[i] == block[j]) level[i] = std::max(level[i], level[j] + 1);
+            if (block[j] >= 0 && block[i] == block[j]) level[i] = std::max(level[i], level[j] + 1);
         }
-    // new order: blocks ascending (= rounds ascending), then level, then old index
-    std::vector<int64_t> bcount(nb + 1, 0);
-    for (int64_t v = 0; v < N; v++) bcount[block[v] + 1]++;
-    for (int32_t b = 0; b < nb; b++) bcount[b + 1] += bcount[b];
-    s.blk_row = bcount;
+    // new order: detached rows (ascending), then blocks ascending (= rounds ascending), then
+    // level, then old index
+    std::vector<int64_t> bcount(nb + 2, 0);  // bcount[0]: detached
+    for (int64_t v = 0; v < N; v++) bcount[block[v] + 2]++;
+    for (int32_t b = 0; b <= nb; b++) bcount[b + 1] += bcount[b];
+    s.ndet = bcount[1];
+    s.blk_row.assign(bcount.begin() + 1, bcount.end());
     s.order.resize(N);
     {
         std::vector<int64_t> nx(bcount.begin(), bcount.end() - 1);
-        for (int64_t v = 0; v < N; v++) s.order[nx[block[v]]++] = (int32_t)v;
+        for (int64_t v = 0; v < N; v++) s.order[nx[block[v] + 1]++] = (int32_t)v;
     }
     s.blk_lvl.assign(1, 0);
     s.lvl_row.clear();

@@ -112,6 +112,7 @@ struct Schedule {
     std::vector<int64_t> lvl_row;      // level boundaries (row positions), one array for all blocks
     int64_t max_levels = 0;
     int64_t depth = 0;
+    int64_t ndet = 0;                  // detached rows (no L entries): positions [0, ndet), in no block
 };
 // Round 0 (the wide bottom of the tree) uses blocks of (R0 rows, CAP0 entries); the upper
 // rounds use (R1, CAP1), typically larger so that few launches cover the top of the tree.

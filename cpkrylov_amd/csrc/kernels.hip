@@ -155,6 +155,7 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     d.blk_lvl.upload(bl);
     d.lvl_row.upload(lr);
     d.round_ptr = s.round_ptr;
+    d.ndet = s.ndet;
     // per-block metadata records for the pipelined round-0 kernel
     std::vector<int32_t> meta((size_t)d.nblk * 8);
     for (int64_t b = 0; b < d.nblk; b++) {
@@ -1159,7 +1160,8 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     int64_t blk0, int64_t nblk, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,
-    int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in, double *ys) {
+    int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
+    int skip0) {
     static_assert(SPLIT == 1 || TPB * SPLIT == 64, "split blocks must share one wave");
     // perm is read for the forward gather (unless the input is in schedule order) and for the
     // backward scatter (unless the solution stays in schedule order)
@@ -1257,7 +1259,9 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
             nxt = meta[bn];
             issue(nxt);  // in flight during the level phase
         }
-        sweep_levels<TPB, BWD, false, CPK_PIPE_CH, false, true>(S, nl, true, tid);
+        // skip0: level 0 holds only rows without entries (no detached rows: the G pivots are in
+        // the blocks); with detached rows a block's level 0 subtracts their (outside) terms
+        sweep_levels<TPB, BWD, false, CPK_PIPE_CH, false, true>(S, nl, skip0 != 0, tid);
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             const int i = tid + j * TPB;
@@ -1299,15 +1303,15 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
     if (!bwd)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys);
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0);
     else if (add)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys);
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0);
     else
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys);
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0);
     return true;
 }
 
@@ -1335,7 +1339,7 @@ static void fwd_round(Ctx &c, const DFactor &F, int64_t r, const double *xin, in
     if (!nb) return;
     hipLaunchKernelGGL((sptrsv_fwd_kernel<TPB, MODE>), dim3((unsigned)nb), dim3(TPB),
                        sweep_lds_bytes(F.sweep_rows[i], F.sweep_cap[i]), c.stream, b0, F.sweep_rows[i],
-                       F.sweep_cap[i], r == 0 ? 1 : 0, F.blk_lvl.p, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.perm.p,
+                       F.sweep_cap[i], (r == 0 && F.ndet == 0) ? 1 : 0, F.blk_lvl.p, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.perm.p,
                        xin, neg_from, w, run, active, sched_in);
 }
 
@@ -1351,10 +1355,46 @@ static void bwd_round(Ctx &c, const DFactor &F, int64_t r, double *w, double *ou
                        out, run, active, ys);
 }
 
+// ---- detached rows (Schedule::ndet): rows of L without entries ------------------------------
+// forward: their value is their input, w = P'x (or x itself in schedule order)
+__global__ void det_fwd_kernel(int64_t ndet, const int32_t *__restrict__ perm, const double *__restrict__ xin,
+                               int64_t neg_from, int sched_in, double *__restrict__ w, const int *run, const int *active) {
+    if (skip(run, active)) return;
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < ndet; q += (int64_t)gridDim.x * blockDim.x) {
+        if (sched_in) {
+            w[q] = xin[q];
+        } else {
+            const int32_t s = perm[q];
+            const double x = xin[s];
+            w[q] = s >= neg_from ? -x : x;
+        }
+    }
+}
+// backward, after every block: y = w / D minus their terms (columns of L, stored order), one
+// row per thread, the same operations as a block row; then the write-back of bwd_store
+template <bool ADD>
+__global__ void det_bwd_kernel(int64_t ndet, const uint32_t *__restrict__ bptr, const int32_t *__restrict__ bcol,
+                               const double *__restrict__ bval, const double *__restrict__ D,
+                               const int32_t *__restrict__ perm, double *w, double *out, double *ys, const int *run,
+                               const int *active) {
+    if (skip(run, active)) return;
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < ndet; q += (int64_t)gridDim.x * blockDim.x) {
+        double acc = w[q] / D[q];
+        const uint32_t e1 = bptr[q + 1];
+        for (uint32_t e = bptr[q]; e < e1; e++) acc -= bval[e] * w[bcol[e]];
+        w[q] = acc;
+        bwd_store<ADD>(out, ys, perm, q, acc);
+    }
+}
+static inline unsigned det_grid(int64_t n) { return (unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 8192); }
+
 template <int MODE>
 static void fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
                     const int *active, int sched_in) {
     const int64_t R = (int64_t)F.round_ptr.size() - 1;
+    if (F.ndet > 0 && !(sched_in && xin == w))  // in place in schedule order: already there
+        hipLaunchKernelGGL(det_fwd_kernel, dim3(det_grid(F.ndet)), dim3(kBlock), 0, c.stream, F.ndet, F.perm.p, xin,
+                           neg_from, sched_in, w, run, active);
     for (int64_t r = 0; r < R; r++) {
         if (r == 0 && MODE == 0 &&
             pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr))
@@ -1405,6 +1445,14 @@ void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
         case 513: bwd_round<256, true>(c, F, r, w, out, run, active, ys); break;
         default: bwd_round<256, false>(c, F, r, w, out, run, active, ys); break;
         }
+    }
+    if (F.ndet > 0) {
+        if (add)
+            hipLaunchKernelGGL(det_bwd_kernel<true>, dim3(det_grid(F.ndet)), dim3(kBlock), 0, c.stream, F.ndet, F.bptr.p,
+                               F.bcol.p, F.bval.p, F.D.p, F.perm.p, w, out, ys, run, active);
+        else
+            hipLaunchKernelGGL(det_bwd_kernel<false>, dim3(det_grid(F.ndet)), dim3(kBlock), 0, c.stream, F.ndet,
+                               F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, w, out, ys, run, active);
     }
     CPK_HIP(hipGetLastError());
 }

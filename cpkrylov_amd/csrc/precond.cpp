@@ -135,7 +135,6 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
     an.F = Factor();
     pc->F = std::move(an.F0);
     pc->w.alloc(pc->N);
-    pc->w2.alloc(pc->N);
     pc->r.alloc(pc->N);
     pc->active.alloc(1);
     c.ensure_partials(std::max<size_t>(pc->dKp.nblk * 2, 4096));
@@ -309,9 +308,11 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
         // every step runs and the norms are dead; everything stays in schedule order until the
         // last backward sweep scatters y = P * (ys + dy)
         for (int64_t s = 0; s < steps; s++) {
-            launch_spmv_resid_sched(c, dKps, dF.perm.p, x, neg_from, w.p, r.p, run);  // r = x - op.A*y
-            launch_sptrsv_fwd(c, dF, r.p, N, w2.p, run, nullptr, true);
-            launch_sptrsv_bwd(c, dF, w2.p, s + 1 == steps ? y : nullptr, true, run, nullptr, w.p);  // y += op.LDL*r
+            // r = x - op.A*y; the refinement solve runs in place on r (each row reads its own
+            // input before it writes, detached rows keep theirs); y += op.LDL*r
+            launch_spmv_resid_sched(c, dKps, dF.perm.p, x, neg_from, w.p, r.p, run);
+            launch_sptrsv_fwd(c, dF, r.p, N, r.p, run, nullptr, true);
+            launch_sptrsv_bwd(c, dF, r.p, s + 1 == steps ? y : nullptr, true, run, nullptr, w.p);
         }
         return;
     }
@@ -348,7 +349,7 @@ double Precond::apply_bytes() const {
         // the last scatters
         const double bwd_keep = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn;
         const double kps = 12 * (double)dKps.nnz + 4 * (Nn + 1) + 8 * Nn /*y*/ + 12 * Nn /*x(perm)*/ + 8 * Nn /*r*/;
-        const double fwd_s = 12 * l + 4 * (Nn + 1) + 16 * Nn;
+        const double fwd_s = 12 * l + 4 * (Nn + 1) + 16 * Nn - 16 * (double)dF.ndet;  // in place: detached rows untouched
         const double bwd_acc = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn + 8 * Nn /*ys*/;
         double b = fwd + bwd_keep + steps * (kps + fwd_s + bwd_acc) + (4 + 8) * Nn /*last: perm + scatter*/ +
                    (steps - 1) * 8.0 * Nn /*ys written back in place*/;
