@@ -175,13 +175,15 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     // (1) Layer peeling: round r takes the maximal subtrees of at most R rows of the tree that
     //     remains after rounds 0..r-1.  On bushy (nested-dissection) trees the remainder
     //     shrinks geometrically and a few rounds suffice.
-    // Detached rows: rows of L without entries (the G pivots of a G-first ordering, leaves of the
-    // elimination tree).  Their forward value is their input and nothing reads them before the
-    // backward sweep's last step, so they stay out of the blocks: they come first in the new
-    // order and are solved by one streaming pass per sweep (DFactor::ndet), and the blocks hold
-    // only rows whose levels do work.  CPK_NO_DETACH keeps them in the blocks.
+    // Detached rows (opt-in, CPK_DETACH=1): rows of L without entries (the G pivots of a
+    // G-first ordering, leaves of the elimination tree).  Their forward value is their input and
+    // nothing reads them before the backward sweep's last step, so they can stay out of the
+    // blocks: they come first in the new order and are solved by one streaming pass per sweep
+    // (DFactor::ndet).  Measured at S10: the round-0 blocks stay as many
+    // (the entry cap binds, not the rows) and the streaming passes cost more than the G rows
+    // did inside the blocks, so the default keeps them in.
     std::vector<char> detached(N, 0);
-    if (!getenv("CPK_NO_DETACH"))
+    if (getenv("CPK_DETACH"))
         for (int64_t v = 0; v < N; v++) detached[v] = ent_fwd[v] == 0;
     std::vector<int32_t> alive;
     alive.reserve(N);

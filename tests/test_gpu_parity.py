@@ -197,3 +197,47 @@ def test_precond_apply_bitexact_sweep_configs(gpu_ctx, name, sweep, monkeypatch)
     Mo.set(nitref=1.0, force_itref=1.0)
     z = np.random.default_rng(11).standard_normal(M.n)
     assert np.array_equal(M * z, Mo @ z)
+
+
+@pytest.mark.parametrize("name", ["cvxqp1_m", "cvxqp2_s", "synthetic"])
+@pytest.mark.parametrize("props", [dict(nitref=0), dict(nitref=1, force_itref=True), dict(nitref=2, force_itref=True)])
+def test_precond_apply_bitexact_detached_rows(gpu_ctx, name, props, monkeypatch):
+    """Opt-in schedule with the entry-less rows outside the blocks (CPK_DETACH: a streaming pass
+    per sweep) and the refinement in schedule order: the same bits as the oracle."""
+    import cpkrylov_amd as cpk
+    from cpkrylov_amd.synthetic import saddle_system
+    monkeypatch.setenv("CPK_DETACH", "1")
+    if name == "synthetic":
+        S = saddle_system(N=50000)
+        G, B, C = S["G"], S["B"], S["C"]
+    else:
+        P = F.load(name)
+        G, B, C = P["G"], P["B"], P["C"]
+    M = cpk.opLDL2(G, B, -C)
+    for k, v in props.items():
+        setattr(M, k, v)
+    L, D, perm = M.export_factors()
+    Mo = O.LDL2(G, B, -C, factors=(L, D, perm))
+    Mo.set(**{k: float(v) for k, v in props.items()})
+    z = np.random.default_rng(12).standard_normal(M.n)
+    assert np.array_equal(M * z, Mo @ z)
+
+
+@pytest.mark.parametrize("name", ["cvxqp1_m", "cvxqp2_s"])
+def test_precond_apply_plain_refinement_path(gpu_ctx, name, monkeypatch):
+    """CPK_NO_SCHED_RESID: the refinement through the original-order residual and scatter,
+    the same bits as the schedule-order path and the oracle."""
+    import cpkrylov_amd as cpk
+    P = F.load(name)
+    z = np.random.default_rng(13).standard_normal(P["n"] + P["m"])
+    ys = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("CPK_NO_SCHED_RESID", env)
+        M = cpk.opLDL2(P["G"], P["B"], -P["C"])
+        M.nitref, M.force_itref = 2, True
+        ys.append(M * z)
+    L, D, perm = M.export_factors()
+    Mo = O.LDL2(P["G"], P["B"], -P["C"], factors=(L, D, perm))
+    Mo.set(nitref=2.0, force_itref=1.0)
+    assert np.array_equal(ys[0], ys[1]) and np.array_equal(ys[0], Mo @ z)
