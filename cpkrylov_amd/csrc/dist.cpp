@@ -125,6 +125,27 @@ TreeSplit split_tree(const Factor &f, int P, double tol, int64_t tmax) {
             else if (rank_of[v] < 0) rank_of[v] = last;
         }
     }
+    // Rows drive the Krylov side (vectors, SpMV rows), so long stretches of consecutive isolated
+    // dofs (S50: the slack blocks no constraint touches, nZ/2 rows each) are split into P equal
+    // contiguous parts, part r to rank r, instead of all following one neighbour.  A slack row
+    // couples (in A) with the bounded variable at the same relative position of its block, so
+    // equal parts in dof order land next to each rank's share of those variables.
+    {
+        std::vector<int32_t> node_of(N);
+        for (int64_t v = 0; v < N; v++) node_of[f.perm[v]] = (int32_t)v;
+        const int64_t min_run = 64 * (int64_t)ts.P;
+        for (int64_t g = 0; g < N;) {
+            if (!iso[node_of[g]]) {
+                g++;
+                continue;
+            }
+            int64_t e = g;
+            while (e < N && iso[node_of[e]]) e++;
+            if (e - g >= min_run)
+                for (int64_t q = g; q < e; q++) rank_of[node_of[q]] = (int32_t)(((q - g) * ts.P) / (e - g));
+            g = e;
+        }
+    }
     for (int64_t v = 0; v < N; v++) ts.node_rank[v] = inT[v] ? -1 : rank_of[v];
     return ts;
 }

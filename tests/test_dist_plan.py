@@ -178,3 +178,14 @@ def test_gloo_world2_apply_and_residual():
     assert np.array_equal(yg, Mo @ x)
     Kp = sp.bmat([[P_["G"], P_["B"].T], [P_["B"], -P_["C"]]]).tocsr()
     assert np.array_equal(rg, x - _global_rowsum(Kp, yg))
+
+
+def test_plan_balances_rows_with_isolated_stretches():
+    """S50's slack blocks (dofs no constraint touches: isolated rows of the factor) are long
+    contiguous stretches; the plan deals them out so every rank holds ~N/P rows (the Krylov
+    vectors and SpMV rows), instead of all of them following one neighbouring dof."""
+    from cpkrylov_amd.synthetic import nonsym_system
+    S = nonsym_system(N=200000, seed=11)
+    P = 8
+    rows = [int(cpk.dist_plan(S["G"], S["B"], -S["C"], S["Q"], S["C"], P, r)["sizes"][7]) for r in range(P)]
+    assert sum(rows) <= S["N"] and max(rows) <= 1.05 * S["N"] / P, rows
