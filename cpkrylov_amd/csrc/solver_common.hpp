@@ -93,6 +93,31 @@ __global__ __launch_bounds__(kBlock) void ewred_kernel(int64_t N, F f, RedBuf rb
     if (grid_sum<NV>(acc, rb, tot) && threadIdx.x == 0) f.fin(tot);
 }
 
+// Tiled forms for the Arnoldi window passes: each thread takes kTile elements per step,
+// kBlock apart (every load coalesced), and F::tile() runs the window loop once for all of them:
+// a window coefficient and basis pointer read from LDS serve kTile elements, and kTile
+// independent chains keep more loads in flight.  Each element's arithmetic is unchanged.
+constexpr int kTile = 4;
+template <class F>
+__global__ __launch_bounds__(kBlock) void ewt_kernel(int64_t N, F f) {
+    if (!f.setup()) return;
+    for (int64_t i0 = blockIdx.x * (int64_t)kBlock * kTile + threadIdx.x; i0 < N;
+         i0 += (int64_t)gridDim.x * kBlock * kTile)
+        f.tile(i0, N);
+}
+template <int NV, class F>
+__global__ __launch_bounds__(kBlock) void ewtred_kernel(int64_t N, F f, RedBuf rb) {
+    if (!f.setup()) return;
+    double acc[NV];
+#pragma unroll
+    for (int j = 0; j < NV; j++) acc[j] = 0.0;
+    for (int64_t i0 = blockIdx.x * (int64_t)kBlock * kTile + threadIdx.x; i0 < N;
+         i0 += (int64_t)gridDim.x * kBlock * kTile)
+        f.tile(i0, N, acc);
+    double tot[NV];
+    if (grid_sum<NV>(acc, rb, tot) && threadIdx.x == 0) f.fin(tot);
+}
+
 // Single-thread scalar step.
 template <class F>
 __global__ void scalar_kernel(F f) {
@@ -120,6 +145,21 @@ inline void launch_ewred(Ctx &c, int64_t N, const F &f) {
     c.ensure_partials((size_t)ew_grid(N) * NV);
     const bool dist = c.dist();
     hipLaunchKernelGGL((ewred_kernel<NV, F>), dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f,
+                       RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr});
+    if (dist) {
+        c.comm->allreduce_sum(c.red.p, NV, c.stream);
+        hipLaunchKernelGGL(ewred_fin_kernel<F>, dim3(1), dim3(64), 0, c.stream, f, (const double *)c.red.p);
+    }
+}
+template <class F>
+inline void launch_ewt(Ctx &c, int64_t N, const F &f) {
+    hipLaunchKernelGGL(ewt_kernel<F>, dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f);
+}
+template <int NV, class F>
+inline void launch_ewtred(Ctx &c, int64_t N, const F &f) {
+    c.ensure_partials((size_t)ew_grid(N) * NV);
+    const bool dist = c.dist();
+    hipLaunchKernelGGL((ewtred_kernel<NV, F>), dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f,
                        RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr});
     if (dist) {
         c.comm->allreduce_sum(c.red.p, NV, c.stream);

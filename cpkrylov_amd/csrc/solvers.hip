@@ -985,6 +985,31 @@ struct ArnoldiOrth {
         vnew[i] = v;
         acc[i < n ? 0 : 1] += ut[i] * v;
     }
+    // kTile elements i0 + e * kBlock (ewtred_kernel): the same operations per element; the
+    // thread's partial sums take its elements in this tiled order (deterministic)
+    __device__ void tile(int64_t i0, int64_t Nn, double *acc) {
+        if (tab.nv < 0 || i0 + (kTile - 1) * kBlock >= Nn) {
+            for (int e = 0; e < kTile; e++)
+                if (i0 + e * kBlock < Nn) (*this)(i0 + e * kBlock, acc);
+            return;
+        }
+        double v[kTile];
+#pragma unroll
+        for (int e = 0; e < kTile; e++) v[e] = vnew[i0 + e * kBlock];
+#pragma unroll 4
+        for (int j = 0; j < tab.nv; j++) {
+            const double hj = tab.h[j];
+            const double *pj = tab.p[j] + i0;
+#pragma unroll
+            for (int e = 0; e < kTile; e++) v[e] = v[e] - hj * pj[e * kBlock];
+        }
+#pragma unroll
+        for (int e = 0; e < kTile; e++) {
+            const int64_t i = i0 + e * kBlock;
+            vnew[i] = v[e];
+            acc[i < n ? 0 : 1] += ut[i] * v[e];
+        }
+    }
     __device__ void fin(const double *tot) {
         const int64_t kk = win.kk;
         const double hn2 = tot[0] + tot[1];
@@ -1096,6 +1121,34 @@ struct DqgmresDirection {
         pv = pv / hkk;
         pk[i] = pv;
         xy[i] = i < n ? xy[i] + gk * pv : xy[i] - gk * pv;
+    }
+    __device__ void tile(int64_t i0, int64_t Nn) {
+        if (tab.nv < 0 || i0 + (kTile - 1) * kBlock >= Nn) {
+            for (int e = 0; e < kTile; e++)
+                if (i0 + e * kBlock < Nn) (*this)(i0 + e * kBlock);
+            return;
+        }
+        double pv[kTile];
+#pragma unroll
+        for (int e = 0; e < kTile; e++) {
+            const int64_t i = i0 + e * kBlock;
+            if (h != 0) vn[i] = vn[i] / h;
+            pv[e] = vk[i];
+        }
+#pragma unroll 4
+        for (int j = 0; j < tab.nv; j++) {
+            const double hj = tab.h[j];
+            const double *pj = tab.p[j] + i0;
+#pragma unroll
+            for (int e = 0; e < kTile; e++) pv[e] = pv[e] - hj * pj[e * kBlock];
+        }
+#pragma unroll
+        for (int e = 0; e < kTile; e++) {
+            const int64_t i = i0 + e * kBlock;
+            const double q = pv[e] / hkk;
+            pk[i] = q;
+            xy[i] = i < n ? xy[i] + gk * q : xy[i] - gk * q;
+        }
     }
 };
 
@@ -1652,7 +1705,7 @@ void SolveCore::gmres(const double *b, double *xy, cpk_stats *stats) {
             launch_krylov_spmv(c, AC, st, UT, n, PolArnoldiSpmv{V, N, 0});
             M.apply(UT, n, Wv, &st->running);
             launch_arnoldi_dots(c, st, V, Wv, UT, n, N, 0, R);
-            launch_ewred<2>(c, N, ArnoldiOrth{st, V, UT, n, N, 0, Window{}, nullptr});
+            launch_ewtred<2>(c, N, ArnoldiOrth{st, V, UT, n, N, 0, Window{}, nullptr});
             launch_ew(c, N, GmresNormalize{st, V, N});
         };
         loop(body, [&]() {  // printed iteration = (outer - 1) * restart + k  (cpgmres.m:252)
@@ -1707,8 +1760,8 @@ void SolveCore::dqgmres(const double *b, double *xy, cpk_stats *stats) {
         launch_krylov_spmv(c, AC, st, UT, n, PolArnoldiSpmv{V, N, M1});
         M.apply(UT, n, Wv, &st->running);
         launch_arnoldi_dots(c, st, V, Wv, UT, n, N, M1, Mm);
-        launch_ewred<2>(c, N, ArnoldiOrth{st, V, UT, n, N, M1, Window{}, nullptr});
-        launch_ew(c, N, DqgmresDirection{st, V, PV, xy, n, N});
+        launch_ewtred<2>(c, N, ArnoldiOrth{st, V, UT, n, N, M1, Window{}, nullptr});
+        launch_ewt(c, N, DqgmresDirection{st, V, PV, xy, n, N});
     };
     if (print) print_hist_lines("%5lld  %14.7e\n");
     loop(body, [&]() { print_hist_lines("%5lld  %14.7e\n"); });
