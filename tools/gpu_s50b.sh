@@ -1,8 +1,7 @@
-# S50 bench (no CPU baseline) + rocprof kernel trace of a 10M S50-shaped run
+# S50 at 50M: the bench line (120 iterations per step) and one run to convergence
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python bench.py --config s50 --steps 3 --no-cpu-baseline > gpurun_out/bench_s50.json 2> gpurun_out/bench_s50.err
-rm -rf gpurun_out/prof50
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof50 -o s50 -- python3 bench.py --config s50 --size 10000000 --steps 2 --no-cpu-baseline --no-pmc --profile-reps 1 > gpurun_out/prof50.json 2>/dev/null
+timeout -k 10 400 python bench.py --config s50 --steps 3 --warmup 1 --no-cpu-baseline --no-pmc > gpurun_out/s50_bench.json 2> gpurun_out/s50_bench.err
+timeout -k 10 600 python bench.py --config s50 --itmax 3000 --steps 1 --warmup 0 --no-cpu-baseline --no-pmc > gpurun_out/s50_conv.json 2> gpurun_out/s50_conv.err
