@@ -203,7 +203,7 @@ def main():
                 "avg_ms": round(sweep_ms, 5), "launches": 2 * int(prof.fwd_launches)}
     # the metric's "SpMV GB/s": the saddle-point SpMV inside every M*z (refinement residual)
     spmv_achieved = gbs(prof.resid_bytes, prof.resid_ms)
-    spmv_roofline = {"kernel": "spmv_stream<EpiResidSched> (r = x(perm) - P'Kp P y, schedule order)",
+    spmv_roofline = {"kernel": "spmv_stream<EpiResidSched> (r = x - P'Kp P y, all in schedule order)",
                      "achieved": round(spmv_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(spmv_achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "bytes_per_launch": prof.resid_bytes, "avg_ms": round(prof.resid_ms, 5)}

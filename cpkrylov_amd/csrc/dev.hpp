@@ -163,8 +163,9 @@ void launch_spmv_resid_norm(Ctx &c, const DMat &A, const double *xin, int64_t ne
 void launch_spmv_colmask(Ctx &c, const DMat &A, int64_t col_min, const double *x, double *y, const int *run);
 // forward sweep w = L \ (P' * xin), backward sweep out (=|+=) P * (L' \ (D \ w))
 // sched_in: xin is already in schedule order (no perm gather, no negation)
+// xs (optional): also store the signed input in schedule order (the refinement residual's x)
 void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                       const int *active, bool sched_in = false);
+                       const int *active, bool sched_in = false, double *xs = nullptr);
 // diagnostic: the forward sweep without its level phase (staging + write-back only)
 void launch_sptrsv_fwd_diag(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w);
 // out == null: the solution stays in schedule order in w (and with add, ys += it in place);
@@ -172,6 +173,7 @@ void launch_sptrsv_fwd_diag(Ctx &c, const DFactor &F, const double *xin, int64_t
 void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
                        const int *active, double *ys = nullptr);
 // r = xin(perm) - A*y with A = P'*Kp*P in schedule order (rows and columns), y in schedule
+// order (perm null: xin is the signed input already in schedule order, see launch_sptrsv_fwd);
 // order; each row sums its entries in Kp's column order, so r(k) equals row perm(k) of the
 // original-order residual bit for bit
 void launch_spmv_resid_sched(Ctx &c, const DMat &A, const int32_t *perm, const double *xin, int64_t neg_from,
@@ -286,6 +288,7 @@ struct Precond {
     // accumulated solution all stay in schedule order (apply); kps_from: Kps entry -> Kp entry
     DMat dKps;
     DBuf<int32_t> kps_from;
+    DBuf<double> xs;     // the apply's signed input in schedule order (captured by the first forward sweep)
     uint64_t pattern_hash = 0;  // sparsity of (A11, B, C22): a refactorization must keep it
     DBuf<int> active;    // refinement predicate
     // public properties of opLDL2 (opLDL2.m:45-50)

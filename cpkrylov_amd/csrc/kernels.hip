@@ -196,13 +196,14 @@ struct EpiResid {
 };
 struct EpiResidSched {  // r(k) = xin(perm(k)) - (A y)(k), A and y in schedule order
     const double *xin;
-    const int32_t *perm;
+    const int32_t *perm;  // null: xin is already the signed input in schedule order
     int64_t neg_from;
     double *r;
     const int *run;
     __device__ bool skip() const { return run && *run == 0; }
     __device__ const double *xvec(const double *x) const { return x; }
     __device__ double pre(int64_t i) const {
+        if (!perm) return xin[i];
         const int32_t s = perm[i];
         const double x = xin[s];
         return s >= neg_from ? -x : x;
@@ -920,7 +921,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_fwd_kernel(
     int64_t blk0, int R, int CAP, int skip_first, const int32_t *__restrict__ blk_lvl, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from, double *w,
-    const int *run, const int *active, int sched_in) {
+    const int *run, const int *active, int sched_in, double *xs) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
     const int64_t b = blk0 + blockIdx.x;
@@ -937,6 +938,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_fwd_kernel(
             const int32_t src = sched_in ? r0 + i : perm[r0 + i];
             const double x = xin[src];
             S.w[i] = (src >= neg_from) ? -x : x;
+            if (xs) xs[r0 + i] = S.w[i];
         }
         if (tid == 0) S.p[nr] = (int16_t)ne;
         for (int l = tid; l <= l1 - l0; l += TPB) S.lv[l] = (int16_t)(lvl_row[l0 + l] - r0);
@@ -966,6 +968,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_fwd_kernel(
             const int32_t src = sched_in ? k : perm[k];
             double acc = xin[src];
             if (src >= neg_from) acc = -acc;
+            if (xs) xs[k] = acc;
             const uint32_t q1 = ptr[k + 1];
             for (uint32_t e = ptr[k]; e < q1; e++) acc -= val[e] * w[col[e]];
             w[k] = acc;
@@ -1051,7 +1054,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
     int64_t blk0, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
-    double *w, double *out, const int *run, const int *active, int sched_in, double *ys) {
+    double *w, double *out, const int *run, const int *active, int sched_in, double *ys, double *xs) {
     constexpr int R = RPU * TPB, CAP = EPU * TPB;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
@@ -1091,6 +1094,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
         if (i < nr) {
             S.p[i] = (int16_t)(q[j] - e0);
             S.w[i] = BWD ? a[j] / d[j] : ((sp[j] >= neg_from) ? -a[j] : a[j]);
+            if (!BWD && xs) xs[r0 + i] = S.w[i];
         }
     }
     if (tid == 0) S.p[nr] = (int16_t)ne, S.w[R] = 1.0;
@@ -1127,7 +1131,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
 // upper round r through sptrsv_upper_kernel when the configuration matches an instantiation
 static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add, const double *xin,
                         int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in,
-                        double *ys) {
+                        double *ys, double *xs) {
     constexpr int TPB = 512, RPU = 2, EPU = 8;
     if (getenv("CPK_NO_UPPER") || F.sweep_threads[1] != TPB || F.sweep_rows[1] > RPU * TPB ||
         F.sweep_cap[1] > EPU * TPB || r >= (int64_t)F.round_fits.size() || !F.round_fits[r])
@@ -1139,15 +1143,15 @@ static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add,
     if (!bwd)
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, false, false>), dim3((unsigned)nb), dim3(TPB), lds,
                            c.stream, b0, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active, sched_in, ys);
+                           neg_from, w, out, run, active, sched_in, ys, xs);
     else if (add)
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, true>), dim3((unsigned)nb), dim3(TPB), lds,
                            c.stream, b0, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active, sched_in, ys);
+                           neg_from, w, out, run, active, sched_in, ys, xs);
     else
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, false>), dim3((unsigned)nb), dim3(TPB), lds,
                            c.stream, b0, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active, sched_in, ys);
+                           neg_from, w, out, run, active, sched_in, ys, xs);
     return true;
 }
 
@@ -1161,7 +1165,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,
     int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
-    int skip0) {
+    int skip0, double *xs) {
     static_assert(SPLIT == 1 || TPB * SPLIT == 64, "split blocks must share one wave");
     // perm is read for the forward gather (unless the input is in schedule order) and for the
     // backward scatter (unless the solution stays in schedule order)
@@ -1225,6 +1229,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
                 S.p[i] = (int16_t)(q[j] - e0);
                 if (BWD) S.w[i] = wr[j] / dr[j];
                 else S.w[i] = (sp[j] >= neg_from) ? -xg[j] : xg[j];
+                if (!BWD && xs) xs[r0 + i] = S.w[i];  // the input in schedule order, for the residual
             }
             if (i < nl) S.lv[i] = (int16_t)(lvr[j] - r0);
         }
@@ -1285,7 +1290,8 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
 // per 64-lane wave
 template <int TPB, int RPT, int EPT, int SPLIT = 1>
 static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
-                       double *w, double *out, const int *run, const int *active, int sched_in, double *ys) {
+                       double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
+                       double *xs) {
     if (F.sweep_threads[0] != TPB || F.sweep_rows[0] != RPT * TPB || F.sweep_cap[0] != EPT * TPB) return false;
     const int64_t nb = F.round_ptr[1] - F.round_ptr[0];
     const size_t lds = sweep_lds_bytes(RPT * TPB, EPT * TPB) * SPLIT;
@@ -1303,44 +1309,45 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
     if (!bwd)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0);
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs);
     else if (add)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0);
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs);
     else
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0);
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs);
     return true;
 }
 
 // round 0 through the pipelined kernel when its configuration is one of the instantiated ones
 static bool pipe_round0(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
-                        double *w, double *out, const int *run, const int *active, int sched_in, double *ys) {
+                        double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
+                        double *xs) {
     if (!F.pipelined || F.round_ptr.size() < 2) return false;
-    return pipe_round<32, 6, 18, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
-           pipe_round<32, 4, 12, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
-           pipe_round<32, 8, 24, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
-           pipe_round<128, 2, 6>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
-           pipe_round<64, 3, 9>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
-           pipe_round<64, 4, 12>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
-           pipe_round<64, 6, 18>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
-           pipe_round<64, 8, 24>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
-           pipe_round<128, 1, 4>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys) ||
-           pipe_round<256, 1, 3>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys);
+    return pipe_round<32, 6, 18, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
+           pipe_round<32, 4, 12, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
+           pipe_round<32, 8, 24, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
+           pipe_round<128, 2, 6>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
+           pipe_round<64, 3, 9>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
+           pipe_round<64, 4, 12>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
+           pipe_round<64, 6, 18>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
+           pipe_round<64, 8, 24>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
+           pipe_round<128, 1, 4>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
+           pipe_round<256, 1, 3>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs);
 }
 
 template <int TPB, int MODE>
 static void fwd_round(Ctx &c, const DFactor &F, int64_t r, const double *xin, int64_t neg_from, double *w,
-                      const int *run, const int *active, int sched_in) {
+                      const int *run, const int *active, int sched_in, double *xs) {
     const int i = r == 0 ? 0 : 1;
     const int64_t b0 = F.round_ptr[r], nb = F.round_ptr[r + 1] - b0;
     if (!nb) return;
     hipLaunchKernelGGL((sptrsv_fwd_kernel<TPB, MODE>), dim3((unsigned)nb), dim3(TPB),
                        sweep_lds_bytes(F.sweep_rows[i], F.sweep_cap[i]), c.stream, b0, F.sweep_rows[i],
                        F.sweep_cap[i], (r == 0 && F.ndet == 0) ? 1 : 0, F.blk_lvl.p, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.perm.p,
-                       xin, neg_from, w, run, active, sched_in);
+                       xin, neg_from, w, run, active, sched_in, xs);
 }
 
 template <int TPB, bool ADD>
@@ -1390,25 +1397,25 @@ static inline unsigned det_grid(int64_t n) { return (unsigned)std::min<int64_t>(
 
 template <int MODE>
 static void fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                    const int *active, int sched_in) {
+                    const int *active, int sched_in, double *xs = nullptr) {
     const int64_t R = (int64_t)F.round_ptr.size() - 1;
     if (F.ndet > 0 && !(sched_in && xin == w))  // in place in schedule order: already there
         hipLaunchKernelGGL(det_fwd_kernel, dim3(det_grid(F.ndet)), dim3(kBlock), 0, c.stream, F.ndet, F.perm.p, xin,
                            neg_from, sched_in, w, run, active);
     for (int64_t r = 0; r < R; r++) {
         if (r == 0 && MODE == 0 &&
-            pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr))
+            pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr, xs))
             continue;
         if (r > 0 && MODE == 0 &&
-            upper_round(c, F, r, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr))
+            upper_round(c, F, r, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr, xs))
             continue;
         switch (F.sweep_threads[r == 0 ? 0 : 1]) {
-        case 32: fwd_round<32, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in); break;
-        case 64: fwd_round<64, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in); break;
-        case 128: fwd_round<128, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in); break;
-        case 512: fwd_round<512, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in); break;
-        case 1024: fwd_round<1024, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in); break;
-        default: fwd_round<256, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in); break;
+        case 32: fwd_round<32, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
+        case 64: fwd_round<64, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
+        case 128: fwd_round<128, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
+        case 512: fwd_round<512, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
+        case 1024: fwd_round<1024, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
+        default: fwd_round<256, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
         }
     }
     CPK_HIP(hipGetLastError());
@@ -1419,9 +1426,10 @@ void launch_sptrsv_fwd_diag(Ctx &c, const DFactor &F, const double *xin, int64_t
 }
 
 void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                       const int *active, bool sched_in) {
+                       const int *active, bool sched_in, double *xs) {
     // schedule-order input: no perm gather and no negation (neg_from applies to original indices)
-    fwd_all<0>(c, F, xin, sched_in ? INT64_MAX : neg_from, w, run, active, sched_in ? 1 : 0);
+    if (xs && F.ndet > 0) throw Error(CPK_ERR_UNSUPPORTED, "internal: input capture with detached rows");
+    fwd_all<0>(c, F, xin, sched_in ? INT64_MAX : neg_from, w, run, active, sched_in ? 1 : 0, xs);
 }
 
 void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
@@ -1429,8 +1437,8 @@ void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
     if (!out && add && !ys) throw Error(CPK_ERR_ARGS, "internal: accumulating backward sweep without a base");
     const int64_t R = (int64_t)F.round_ptr.size() - 1;
     for (int64_t r = R - 1; r >= 0; r--) {
-        if (r == 0 && pipe_round0(c, F, true, add, nullptr, 0, w, out, run, active, 0, ys)) continue;
-        if (r > 0 && upper_round(c, F, r, true, add, nullptr, 0, w, out, run, active, 0, ys)) continue;
+        if (r == 0 && pipe_round0(c, F, true, add, nullptr, 0, w, out, run, active, 0, ys, nullptr)) continue;
+        if (r > 0 && upper_round(c, F, r, true, add, nullptr, 0, w, out, run, active, 0, ys, nullptr)) continue;
         switch (F.sweep_threads[r == 0 ? 0 : 1] * 2 + (add ? 1 : 0)) {
         case 64: bwd_round<32, false>(c, F, r, w, out, run, active, ys); break;
         case 65: bwd_round<32, true>(c, F, r, w, out, run, active, ys); break;

@@ -131,6 +131,7 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
         make_dmat(ks, pc->dKps);
         pc->kps_from.upload(from);
     }
+    if (pc->dKps.nnz && pc->dF.ndet == 0) pc->xs.alloc(pc->N);
     clk.lap("schedule-order Kp");
     an.F = Factor();
     pc->F = std::move(an.F0);
@@ -294,8 +295,9 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
         ldl_solve(t.p, N, y, false, run, nullptr, piggy_src);
         launch_spmv_colmask(c, dKp, n, y, ghn.p, run);
     } else if (nitref >= 1 && force_itref != 0 && sched_path()) {
-        // y = op.LDL * x kept in schedule order (w) for the refinement below: no scatter
-        launch_sptrsv_fwd(c, dF, x, neg_from, w.p, run, nullptr);
+        // y = op.LDL * x kept in schedule order (w) for the refinement below: no scatter; the
+        // forward sweep also leaves the signed input in schedule order (xs) for the residual
+        launch_sptrsv_fwd(c, dF, x, neg_from, w.p, run, nullptr, false, xs.n ? xs.p : nullptr);
         launch_sptrsv_bwd(c, dF, w.p, nullptr, false, run, nullptr);
     } else {
         // y = op.LDL * x   (opLDL2.m:165-167); the residual-update branch subtracts the zero
@@ -310,7 +312,8 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
         for (int64_t s = 0; s < steps; s++) {
             // r = x - op.A*y; the refinement solve runs in place on r (each row reads its own
             // input before it writes, detached rows keep theirs); y += op.LDL*r
-            launch_spmv_resid_sched(c, dKps, dF.perm.p, x, neg_from, w.p, r.p, run);
+            if (xs.n) launch_spmv_resid_sched(c, dKps, nullptr, xs.p, 0, w.p, r.p, run);
+            else launch_spmv_resid_sched(c, dKps, dF.perm.p, x, neg_from, w.p, r.p, run);
             launch_sptrsv_fwd(c, dF, r.p, N, r.p, run, nullptr, true);
             launch_sptrsv_bwd(c, dF, r.p, s + 1 == steps ? y : nullptr, true, run, nullptr, w.p);
         }
@@ -348,10 +351,11 @@ double Precond::apply_bytes() const {
         // contiguously (no perm); each refinement backward sweep reads ys contiguously and only
         // the last scatters
         const double bwd_keep = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn;
-        const double kps = 12 * (double)dKps.nnz + 4 * (Nn + 1) + 8 * Nn /*y*/ + 12 * Nn /*x(perm)*/ + 8 * Nn /*r*/;
+        const double kps = 12 * (double)dKps.nnz + 4 * (Nn + 1) + 8 * Nn /*y*/ +
+                           (xs.n ? 8 * Nn /*xs*/ : 12 * Nn /*x(perm)*/) + 8 * Nn /*r*/;
         const double fwd_s = 12 * l + 4 * (Nn + 1) + 16 * Nn - 16 * (double)dF.ndet;  // in place: detached rows untouched
         const double bwd_acc = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn + 8 * Nn /*ys*/;
-        double b = fwd + bwd_keep + steps * (kps + fwd_s + bwd_acc) + (4 + 8) * Nn /*last: perm + scatter*/ +
+        double b = fwd + (xs.n ? 8 * Nn : 0.0) /*xs written*/ + bwd_keep + steps * (kps + fwd_s + bwd_acc) + (4 + 8) * Nn /*last: perm + scatter*/ +
                    (steps - 1) * 8.0 * Nn /*ys written back in place*/;
         return b;
     }

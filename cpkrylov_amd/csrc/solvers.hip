@@ -1892,7 +1892,10 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
     const double Nn = (double)N, l = (double)M.dF.nnz;
     out->spmv_ms = timeit([&]() { launch_spmv(c, AC, x.p, y.p, nullptr); });
     out->spmv_bytes = 12.0 * AC.nnz + 4.0 * (Nn + 1) + 8.0 * Nn + 8.0 * Nn;
-    if (M.sched_path()) {  // the refinement residual the apply runs: Kp in schedule order, x through perm
+    if (M.sched_path() && M.xs.n) {  // the refinement residual the apply runs: Kp, x and y in schedule order
+        out->resid_ms = timeit([&]() { launch_spmv_resid_sched(c, M.dKps, nullptr, x.p, 0, y.p, z.p, nullptr); });
+        out->resid_bytes = 12.0 * M.dKps.nnz + 4.0 * (Nn + 1) + 8.0 * Nn /*y*/ + 8.0 * Nn /*x*/ + 8.0 * Nn /*r*/;
+    } else if (M.sched_path()) {  // x through perm
         out->resid_ms = timeit([&]() { launch_spmv_resid_sched(c, M.dKps, M.dF.perm.p, x.p, M.n, y.p, z.p, nullptr); });
         out->resid_bytes = 12.0 * M.dKps.nnz + 4.0 * (Nn + 1) + 8.0 * Nn /*y*/ + 12.0 * Nn /*x, perm*/ + 8.0 * Nn /*r*/;
     } else {

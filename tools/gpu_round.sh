@@ -1,8 +1,9 @@
-# parity tests, S10 bench (with its PMC passes), rocprofv3 kernel stats of the same bench command
+# parity tests (headline-size file separately), S10 bench (with its PMC passes and CPU baseline),
+# rocprofv3 kernel stats of the same bench command
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --deselect tests/test_gpu_scale.py --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 timeout -k 10 900 python bench.py > gpurun_out/bench_s10.json 2> gpurun_out/bench_s10.err
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py --steps 5 --no-cpu-baseline --no-pmc > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err
