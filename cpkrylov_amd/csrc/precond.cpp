@@ -288,6 +288,7 @@ void Precond::set_handle(bool on) {
 
 void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run, const double *piggy_src) {
     Ctx &c = *ctx;
+    bool have_xs = false;  // the first forward sweep left the signed x in schedule order (xs)
     if (residual_update != 0 && handle) {
         // y = op.LDL * [x(1:n) - op.Aty; x(n+1:N) - op.Cy]; then op.Aty = op.A(1:n, n+1:N) * y2,
         // op.Cy = op.A(n+1:N, n+1:N) * y2 = the columns n+1:N of Kp times y2  (opLDL2.m:164-172)
@@ -298,6 +299,7 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
         // y = op.LDL * x kept in schedule order (w) for the refinement below: no scatter; the
         // forward sweep also leaves the signed input in schedule order (xs) for the residual
         launch_sptrsv_fwd(c, dF, x, neg_from, w.p, run, nullptr, false, xs.n ? xs.p : nullptr);
+        have_xs = xs.n > 0;
         launch_sptrsv_bwd(c, dF, w.p, nullptr, false, run, nullptr);
     } else {
         // y = op.LDL * x   (opLDL2.m:165-167); the residual-update branch subtracts the zero
@@ -312,7 +314,7 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
         for (int64_t s = 0; s < steps; s++) {
             // r = x - op.A*y; the refinement solve runs in place on r (each row reads its own
             // input before it writes, detached rows keep theirs); y += op.LDL*r
-            if (xs.n) launch_spmv_resid_sched(c, dKps, nullptr, xs.p, 0, w.p, r.p, run);
+            if (have_xs) launch_spmv_resid_sched(c, dKps, nullptr, xs.p, 0, w.p, r.p, run);
             else launch_spmv_resid_sched(c, dKps, dF.perm.p, x, neg_from, w.p, r.p, run);
             launch_sptrsv_fwd(c, dF, r.p, N, r.p, run, nullptr, true);
             launch_sptrsv_bwd(c, dF, r.p, s + 1 == steps ? y : nullptr, true, run, nullptr, w.p);
