@@ -1160,7 +1160,10 @@ static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add,
 // one instruction stream for SPLIT blocks instead of one per block; lanes of different logical
 // blocks never synchronise (within a single wave __syncthreads is a no-op fence).
 template <int TPB, int RPT, int EPT, bool BWD, bool ADD, int SPLIT = 1>
-__global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPLIT == 1 ? 4 : 1))) void sptrsv_pipe_kernel(
+#ifndef CPK_PIPE_WAVES
+#define CPK_PIPE_WAVES 4  // waves per SIMD the round-0 kernel's registers allow (4: 128 VGPRs)
+#endif
+__global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPLIT == 1 ? CPK_PIPE_WAVES : 1))) void sptrsv_pipe_kernel(
     int64_t blk0, int64_t nblk, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,
