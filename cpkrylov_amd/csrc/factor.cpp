@@ -2,6 +2,7 @@
 // [L,D,P] = ldl(op.A), ops/opLDL2.m:82) and the block/round schedule for the device
 // triangular sweeps that replace op.LDL = P*inv(L')*inv(D)*inv(L)*P' (ops/opLDL2.m:86).
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <numeric>
 
@@ -306,9 +307,12 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     }
     s.blk_lvl.assign(1, 0);
     s.lvl_row.clear();
+    parallel_for(nb, [&](int64_t lo, int64_t hi) {  // blocks sort independently
+        for (int64_t b = lo; b < hi; b++)
+            std::stable_sort(s.order.begin() + s.blk_row[b], s.order.begin() + s.blk_row[b + 1],
+                             [&](int32_t a, int32_t c) { return level[a] < level[c]; });
+    }, 256);
     for (int32_t b = 0; b < nb; b++) {
-        auto first = s.order.begin() + s.blk_row[b], last = s.order.begin() + s.blk_row[b + 1];
-        std::stable_sort(first, last, [&](int32_t a, int32_t c) { return level[a] < level[c]; });
         int32_t prev = -1;
         for (int64_t q = s.blk_row[b]; q < s.blk_row[b + 1]; q++) {
             const int32_t l = level[s.order[q]];
@@ -345,19 +349,23 @@ Factor relabel(const Factor &f, const Schedule &s, std::vector<int32_t> *src) {
     const bool vals = (int64_t)f.D.size() == N;  // numeric factor (Lx may be empty: no entries)
     if (vals) g.Lx.resize(f.Lx.size());
     if (src) src->resize(f.Li.size());
-    std::vector<std::pair<int32_t, int64_t>> col;
-    for (int64_t q = 0; q < N; q++) {
-        int32_t old = s.order[q];
-        col.clear();
-        for (int64_t p = f.Lp[old]; p < f.Lp[old + 1]; p++) col.emplace_back(pos[f.Li[p]], p);
-        std::sort(col.begin(), col.end(), [](auto &a, auto &b) { return a.first < b.first; });
-        for (size_t t = 0; t < col.size(); t++) {
-            if (col[t].first <= q) throw Error(CPK_ERR_FACTOR, "internal: relabel is not topological");
-            g.Li[g.Lp[q] + t] = col[t].first;
-            if (vals) g.Lx[g.Lp[q] + t] = f.Lx[col[t].second];
-            if (src) (*src)[g.Lp[q] + t] = (int32_t)col[t].second;
+    std::atomic<bool> bad{false};
+    parallel_for(N, [&](int64_t lo, int64_t hi) {  // columns relabel independently
+        std::vector<std::pair<int32_t, int64_t>> col;
+        for (int64_t q = lo; q < hi; q++) {
+            int32_t old = s.order[q];
+            col.clear();
+            for (int64_t p = f.Lp[old]; p < f.Lp[old + 1]; p++) col.emplace_back(pos[f.Li[p]], p);
+            std::sort(col.begin(), col.end(), [](auto &a, auto &b) { return a.first < b.first; });
+            for (size_t t = 0; t < col.size(); t++) {
+                if (col[t].first <= q) bad = true;
+                g.Li[g.Lp[q] + t] = col[t].first;
+                if (vals) g.Lx[g.Lp[q] + t] = f.Lx[col[t].second];
+                if (src) (*src)[g.Lp[q] + t] = (int32_t)col[t].second;
+            }
         }
-    }
+    });
+    if (bad) throw Error(CPK_ERR_FACTOR, "internal: relabel is not topological");
     return g;
 }
 

@@ -90,28 +90,32 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
                 fcol[q] = (int32_t)j;
                 fidx[q] = (int32_t)p;
             }
-        if (key) {
-            std::vector<std::pair<int64_t, std::pair<int32_t, int32_t>>> row;
-            for (int64_t i = 0; i < N; i++) {
-                row.clear();
-                for (uint32_t q = fptr[i]; q < fptr[i + 1]; q++) row.push_back({K(fcol[q]), {fcol[q], fidx[q]}});
-                std::sort(row.begin(), row.end(), [](auto &x, auto &y) { return x.first < y.first; });
-                for (size_t t = 0; t < row.size(); t++) fcol[fptr[i] + t] = row[t].second.first, fidx[fptr[i] + t] = row[t].second.second;
-            }
-        }
+        if (key)
+            parallel_for(N, [&](int64_t lo, int64_t hi) {  // rows sort independently
+                std::vector<std::pair<int64_t, std::pair<int32_t, int32_t>>> row;
+                for (int64_t i = lo; i < hi; i++) {
+                    row.clear();
+                    for (uint32_t q = fptr[i]; q < fptr[i + 1]; q++) row.push_back({K(fcol[q]), {fcol[q], fidx[q]}});
+                    std::sort(row.begin(), row.end(), [](auto &x, auto &y) { return x.first < y.first; });
+                    for (size_t t = 0; t < row.size(); t++)
+                        fcol[fptr[i] + t] = row[t].second.first, fidx[fptr[i] + t] = row[t].second.second;
+                }
+            });
     }
     std::vector<double> fval(nf, 0.0);
     if (vals)
-        for (int64_t q = 0; q < nf; q++) fval[q] = f.Lx[fidx[q]];
+        parallel_for(nf, [&](int64_t lo, int64_t hi) {
+            for (int64_t q = lo; q < hi; q++) fval[q] = f.Lx[fidx[q]];
+        });
     // backward rows: L's columns (plus extra entries), keys descending; bidx[q] = CSC slot
     std::vector<uint32_t> bptr(N + 1, 0);
     for (int64_t j = 0; j < N; j++)
         bptr[j + 1] = bptr[j] + (uint32_t)(f.Lp[j + 1] - f.Lp[j]) + (uint32_t)(extra ? (*extra)[j].size() : 0);
     std::vector<int32_t> bcol(d.nnz), bidx(bsrc ? d.nnz : 0);
     std::vector<double> bval(d.nnz, 0.0);
-    {
+    parallel_for(N, [&](int64_t lo, int64_t hi) {  // rows (columns of L) sort independently
         std::vector<std::pair<int64_t, std::pair<int32_t, int64_t>>> row;  // (key, (col, CSC slot | ~extra))
-        for (int64_t j = 0; j < N; j++) {
+        for (int64_t j = lo; j < hi; j++) {
             row.clear();
             for (int64_t p = f.Lp[j]; p < f.Lp[j + 1]; p++) row.push_back({K(f.Li[p]), {f.Li[p], p}});
             if (extra)
@@ -125,7 +129,7 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
                 if (bsrc) bidx[bptr[j] + t] = (int32_t)src;
             }
         }
-    }
+    });
     if (fsrc) *fsrc = std::move(fidx);
     if (bsrc) *bsrc = std::move(bidx);
     // rounds whose blocks all fit the upper-round staging image (sptrsv_upper_kernel)
