@@ -82,6 +82,7 @@ _SIGS = {
     "cpk_simgroup_destroy": ([vp], C.c_int),
     "cpk_ctx_create_sim": ([C.c_int, vp, C.c_int, C.c_int, P(vp)], C.c_int),
     "cpk_pc_local_dofs": ([vp, P(C.c_int64), P(C.c_int64), P(C.c_int32)], C.c_int),
+    "cpk_pc_sep_info": ([vp, P(C.c_int64)], C.c_int),
     "cpk_method_solve": ([vp, C.c_int, P(C.c_double), vp, vp, vp, P(Opts), P(C.c_double), P(C.c_double),
                           P(Stats)], C.c_int),
     "cpk_method_solve_device": ([vp, C.c_int, vp, vp, vp, vp, P(Opts), vp, P(Stats)], C.c_int),

@@ -248,6 +248,12 @@ class opLDL2:
             e[i] = 0
         return X
 
+    def sep_info(self):
+        """Diagnostic: the distributed separator solve's staging (cpk_pc_sep_info)."""
+        v = (C.c_int64 * 7)()
+        check(lib.cpk_pc_sep_info(self.h, v))
+        return dict(zip(("dist", "nT", "nlev", "nrec", "lds", "lds_g", "kt"), list(v)))
+
     def local_dofs(self):
         """Global indices of this rank's local vector entries ([x-part; y-part]) and n_loc."""
         nl, ml = C.c_int64(), C.c_int64()

@@ -539,6 +539,16 @@ int cpk_profile_kernels(cpk_ctx ctx, cpk_mat A, cpk_mat C, cpk_pc M, int reps, c
     API_END
 }
 
+int cpk_pc_sep_info(cpk_pc M, int64_t *info) {
+    API_BEGIN
+    need(M && info, "NULL argument");
+    const Precond &p = *M->p;
+    const DSep &T = p.sep;
+    const int64_t v[7] = {p.dist ? 1 : 0, T.nT, T.nlev, T.nrec, (int64_t)T.lds, (int64_t)T.lds_g, T.kt};
+    std::memcpy(info, v, sizeof v);
+    API_END
+}
+
 int cpk_pc_local_dofs(cpk_pc M, int64_t *n_loc, int64_t *m_loc, int32_t *dofs) {
     API_BEGIN
     need(M, "NULL argument");

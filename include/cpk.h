@@ -165,6 +165,10 @@ int cpk_pc_divide(cpk_pc M, const double *b, double *x);
 int cpk_pc_get_info(cpk_pc M, cpk_pc_info *info);
 /* Local slice of a (distributed) preconditioner: n_loc x-part and m_loc y-part dofs; dofs[i] =
  * global index of local entry i (n_loc + m_loc entries).  One GPU: the identity. */
+/* Diagnostic (not in the reference): the separator solve of a distributed preconditioner,
+ * info[7] = {distributed, separator rows, levels, step records, LDS bytes with the records
+ * staged (0: they do not fit), LDS bytes with the records left in HBM, payload per rank}. */
+int cpk_pc_sep_info(cpk_pc M, int64_t *info);
 int cpk_pc_local_dofs(cpk_pc M, int64_t *n_loc, int64_t *m_loc, int32_t *dofs);
 /* Export the factors P'*Kp*P = L*D*L': strict-lower L in CSC (Lcolptr[N+1], Lrowind[nnz_l],
  * Lval[nnz_l]), D[N], perm[N] (perm[k] = original index of pivot k).  Any pointer may be NULL. */

@@ -261,3 +261,33 @@ def test_dist_apply_separator_fallbacks_bitexact(P, path, monkeypatch):
     yo = Mo @ z
     for y, _ in res:
         assert np.array_equal(y, yo), np.max(np.abs(y - yo))
+
+
+def test_dist_apply_separator_records_overflow_lds(monkeypatch):
+    """A separator whose step records really exceed the 160 KB of LDS (a small split tolerance
+    grows T): the stepped solve reads its records from HBM (lds == 0, lds_g > 0), and the
+    apply still equals the oracle's bit for bit.  (The CPK_TSOLVE_GLOBAL test above forces
+    that path on a separator that would fit.)"""
+    import cpkrylov_amd as cpk
+    S = saddle_system(N=400000, seed=21)
+    z = np.random.default_rng(8).standard_normal(S["n"] + S["m"])
+    P = 4
+    for tol in ("0.002", "0.0005", "0.0002", "0.0001"):
+        monkeypatch.setenv("CPK_SPLIT_TOL", tol)
+
+        def work(ctx, r):
+            M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+            M.nitref, M.force_itref = 1, True
+            return M * z, M.sep_info(), M.export_factors() if r == 0 else None
+
+        res = _run_ranks(P, work)
+        info = res[0][1]
+        if info["lds"] == 0:
+            break
+    assert info["lds"] == 0 and info["lds_g"] > 0 and info["nrec"] > 0, info
+    L, D, perm = res[0][2]
+    Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=(L, D, perm))
+    Mo.set(nitref=1.0, force_itref=1.0)
+    yo = Mo @ z
+    for y, _, _ in res:
+        assert np.array_equal(y, yo), np.max(np.abs(y - yo))
