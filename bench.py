@@ -121,7 +121,7 @@ def main():
             with _quiet_stdout():
                 ctx = cpk.Context(device=local, rank=rank, nranks=world, unique_id=uid[0])
             A, B, Cm, G = (cpk.Matrix(S[k], ctx) for k in ("Q", "B", "C", "G"))
-            M = cpk.opLDL2(G, B, -S["C"], ctx=ctx)
+            M = cpk.opLDL2(G, B, -S["C"], ctx=ctx, krylov_A=A)  # A: placement hint (cpk_pc_create_hint)
         except Exception as e:  # noqa: BLE001  (reported, then every rank exits)
             err = f"{type(e).__name__}: {e}"
         ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)

@@ -59,6 +59,7 @@ _SIGS = {
     "cpk_mat_destroy": ([vp], C.c_int),
     "cpk_mat_spmv": ([vp, P(C.c_double), P(C.c_double)], C.c_int),
     "cpk_pc_create": ([vp, vp, vp, vp, P(C.c_double), P(vp)], C.c_int),
+    "cpk_pc_create_hint": ([vp, vp, vp, vp, vp, P(C.c_double), P(vp)], C.c_int),
     "cpk_pc_destroy": ([vp], C.c_int),
     "cpk_pc_refactor": ([vp, vp, vp, vp, P(C.c_double)], C.c_int),
     "cpk_pc_set": ([vp, P(Opts)], C.c_int),

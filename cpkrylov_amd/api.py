@@ -164,7 +164,9 @@ class opLDL2:
       residual_update stored as given (default false); a functional no-op, as in the reference
     """
 
-    def __init__(self, A, B, Cm, ctx=None, _handle=None):
+    def __init__(self, A, B, Cm, ctx=None, _handle=None, krylov_A=None):
+        """krylov_A (optional): the Krylov operator's A, a placement hint for a distributed
+        context (cpk_pc_create_hint); ignored on one GPU."""
         self.ctx = ctx or default_context()
         if _handle is not None:
             self.h = _handle
@@ -172,7 +174,12 @@ class opLDL2:
             mats = [_as_matrix(M, self.ctx) for M in (A, B, Cm)]
             h = C.c_void_p()
             pt = C.c_double()
-            check(lib.cpk_pc_create(self.ctx.h, mats[0].h, mats[1].h, mats[2].h, C.byref(pt), C.byref(h)))
+            if krylov_A is not None:
+                ka = _as_matrix(krylov_A, self.ctx)
+                check(lib.cpk_pc_create_hint(self.ctx.h, mats[0].h, mats[1].h, mats[2].h, ka.h, C.byref(pt),
+                                             C.byref(h)))
+            else:
+                check(lib.cpk_pc_create(self.ctx.h, mats[0].h, mats[1].h, mats[2].h, C.byref(pt), C.byref(h)))
             self.h = h
             self.ptime = pt.value
         info = _lib.PcInfo()

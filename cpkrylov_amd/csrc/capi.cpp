@@ -313,6 +313,19 @@ int cpk_pc_create(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptim
     API_END
 }
 
+int cpk_pc_create_hint(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, cpk_mat Akry, double *ptime,
+                       cpk_pc *out) {
+    API_BEGIN
+    need(ctx && A11 && B && C22 && out, "opLDL2: Invalid number of arguments.");
+    auto pc = std::make_unique<cpk_pc_s>();
+    pc->ctx = ctx;
+    if (ctx->c.dist()) pc->p.reset(precond_create_dist(ctx->c, analyze(A11->h, B->h, C22->h), Akry ? &Akry->h : nullptr));
+    else pc->p.reset(precond_create(ctx->c, A11->h, B->h, C22->h));
+    if (ptime) *ptime = pc->p->ptime;
+    *out = pc.release();
+    API_END
+}
+
 int cpk_pc_refactor(cpk_pc M, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptime) {
     API_BEGIN
     need(M && A11 && B && C22, "opLDL2: Invalid number of arguments.");
@@ -578,7 +591,7 @@ int cpk_reg_solve(cpk_ctx ctx, int method, const double *b, cpk_mat A, cpk_mat B
     check_dist_method(c, method);
     auto pc = std::make_unique<cpk_pc_s>();
     pc->ctx = ctx;
-    if (c.dist()) pc->p.reset(precond_create_dist(c, analyze(G->h, B->h, negC)));
+    if (c.dist()) pc->p.reset(precond_create_dist(c, analyze(G->h, B->h, negC), &A->h));
     else pc->p.reset(precond_create(c, G->h, B->h, negC));
     Precond &p = *pc->p;
     apply_props(p, opts);  // reg_cpkrylov.m:135-148
@@ -662,7 +675,7 @@ int cpk_analysis_plan(cpk_analysis a, cpk_mat A, cpk_mat C, int nranks, int rank
          "A and C must match the analysis' n and m");
     auto p = std::make_unique<cpk_plan_s>();
     p->n = an.n, p->m = an.m;
-    p->ts = split_tree(an.F0, nranks, split_tol_option());
+    p->ts = split_tree(an.F0, nranks, split_tol_option(), -1, &A->h);
     p->dm = make_dofmap(an.F0, p->ts, an.n);
     p->rp = make_rank_plan(an.F0, p->ts, p->dm, rank);
     p->kp = dist_csr(an.Kp, p->dm, rank, false);

@@ -326,6 +326,7 @@ double precond_refactor(Precond &p, const DMat &A11, const DMat &B, const DMat &
 uint64_t pattern_hash(const HCsr &A11, const HCsr &B, const HCsr &C22);
 Precond *precond_create(Ctx &c, Analysis &&an);
 // distributed preconditioner of rank c.rank out of c.nranks
-Precond *precond_create_dist(Ctx &c, Analysis &&an);
+// Akry (optional): the Krylov operator's A, a placement hint for isolated rows (split_tree)
+Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry = nullptr);
 
 }  // namespace cpk

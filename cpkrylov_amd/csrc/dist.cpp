@@ -24,7 +24,7 @@ double split_tol_option() {
     return v;
 }
 
-TreeSplit split_tree(const Factor &f, int P, double tol, int64_t tmax) {
+TreeSplit split_tree(const Factor &f, int P, double tol, int64_t tmax, const HCsr *Akry) {
     const int64_t N = f.N;
     TreeSplit ts;
     ts.P = std::max(P, 1);
@@ -144,6 +144,27 @@ TreeSplit split_tree(const Factor &f, int P, double tol, int64_t tmax) {
             if (e - g >= min_run)
                 for (int64_t q = g; q < e; q++) rank_of[node_of[q]] = (int32_t)(((q - g) * ts.P) / (e - g));
             g = e;
+        }
+    }
+    // with the Krylov operator known, an isolated row takes the rank of the first dof its A row
+    // couples it with that the tree placed (the slack rows of S50 couple with one bounded
+    // variable each): the halo of A then holds only the coupling across rank boundaries
+    if (Akry) {
+        std::vector<int32_t> node_of(N);
+        for (int64_t v = 0; v < N; v++) node_of[f.perm[v]] = (int32_t)v;
+        for (int64_t v = 0; v < N; v++) {
+            if (!iso[v] || inT[v]) continue;
+            const int64_t g = f.perm[v];
+            if (g >= Akry->nrows) continue;
+            for (int64_t p = Akry->ptr[g]; p < Akry->ptr[g + 1]; p++) {
+                const int32_t c = Akry->ind[p];
+                if (c == g || c >= N) continue;
+                const int32_t u = node_of[c];
+                if (!iso[u] && !inT[u]) {
+                    rank_of[v] = rank_of[u];
+                    break;
+                }
+            }
         }
     }
     for (int64_t v = 0; v < N; v++) ts.node_rank[v] = inT[v] ? -1 : rank_of[v];

@@ -26,7 +26,10 @@ struct TreeSplit {
 // tol: accepted load imbalance (max/avg - 1); T grows until it is met or T reaches tmax rows.
 // Every rank must pass the same tol (each builds the same global plan independently).
 constexpr double kSplitTol = 0.03;
-TreeSplit split_tree(const Factor &f, int P, double tol = kSplitTol, int64_t tmax = -1);
+// Akry (optional): the Krylov operator's (1,1) block A (n x n).  Isolated rows (no factor
+// entries) then follow the rank of a dof A couples them with, which keeps the Krylov SpMV's
+// halo small (S50's slack rows couple only through A).
+TreeSplit split_tree(const Factor &f, int P, double tol = kSplitTol, int64_t tmax = -1, const HCsr *Akry = nullptr);
 // the diagnostic override CPK_SPLIT_TOL, validated: a finite number in
 // (0, 1), else CPK_ERR_ARGS; kSplitTol when unset.  Read by the callers of split_tree.
 double split_tol_option();

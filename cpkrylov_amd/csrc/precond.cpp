@@ -144,14 +144,14 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
     return pc.release();
 }
 
-Precond *precond_create_dist(Ctx &c, Analysis &&an) {
+Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     auto t0 = std::chrono::steady_clock::now();
     auto pc = std::make_unique<Precond>();
     pc->ctx = &c;
     pc->dist = true;
     pc->gn = an.n, pc->gm = an.m, pc->gN = an.N;
     pc->ordering = an.ordering;
-    const TreeSplit ts = split_tree(an.F0, c.nranks, split_tol_option());
+    const TreeSplit ts = split_tree(an.F0, c.nranks, split_tol_option(), -1, Akry);
     auto dm = std::make_shared<DofMap>(make_dofmap(an.F0, ts, an.n));
     RankPlan rp = make_rank_plan(an.F0, ts, *dm, c.rank);
     pc->n = dm->n_loc[c.rank], pc->m = dm->m_loc[c.rank], pc->N = pc->n + pc->m;

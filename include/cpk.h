@@ -136,6 +136,12 @@ int cpk_mat_spmv(cpk_mat A, const double *x, double *y);
  * then take and return GLOBAL vectors on every rank; device-vector entry points take the
  * rank's LOCAL slice in the order cpk_pc_local_dofs reports ([x-part; y-part]). */
 int cpk_pc_create(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptime, cpk_pc *out);
+/* cpk_pc_create with the Krylov operator's A (n x n) as a placement hint for a distributed
+ * context: rows the factor leaves isolated are owned with the dofs A couples them with, so the
+ * Krylov SpMV's halo stays small.  reg_cpkrylov (cpk_reg_solve) passes its A itself.  On one
+ * GPU identical to cpk_pc_create; Akry may be NULL. */
+int cpk_pc_create_hint(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, cpk_mat Akry, double *ptime,
+                       cpk_pc *out);
 int cpk_pc_destroy(cpk_pc M);
 /* Refactorization with new values and the same sparsity: opLDL2(G, B, C) rebuilt in an
  * interior-point outer loop (the constructor, opLDL2.m:60-92, called per outer iteration

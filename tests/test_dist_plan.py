@@ -187,5 +187,10 @@ def test_plan_balances_rows_with_isolated_stretches():
     from cpkrylov_amd.synthetic import nonsym_system
     S = nonsym_system(N=200000, seed=11)
     P = 8
-    rows = [int(cpk.dist_plan(S["G"], S["B"], -S["C"], S["Q"], S["C"], P, r)["sizes"][7]) for r in range(P)]
+    plans = [cpk.dist_plan(S["G"], S["B"], -S["C"], S["Q"], S["C"], P, r) for r in range(P)]
+    rows = [int(p["sizes"][7]) for p in plans]
     assert sum(rows) <= S["N"] and max(rows) <= 1.05 * S["N"] / P, rows
+    # with the Krylov operator as placement hint (the plan gets A), each slack row sits with
+    # the bounded variable A couples it with: the Krylov SpMV's halo stays a small fraction
+    ac_kmax = max(int(p["sizes"][12]) for p in plans)
+    assert ac_kmax <= 0.2 * S["N"] / P, (ac_kmax, rows)
