@@ -291,3 +291,36 @@ def test_dist_apply_separator_records_overflow_lds(monkeypatch):
     yo = Mo @ z
     for y, _, _ in res:
         assert np.array_equal(y, yo), np.max(np.abs(y - yo))
+
+
+@pytest.mark.parametrize("P", [3, 4])
+def test_dist_placement_hint_nonsym(P):
+    """cpk_pc_create_hint: the Krylov operator's A places the isolated rows (the slack block of
+    the nonsymmetric 3x3 system); M*z is still bit-exact and a cpdqgmres solve on the device
+    vectors of that placement matches the oracle."""
+    import cpkrylov_amd as cpk
+    from cpkrylov_amd.synthetic import nonsym_system
+    S = nonsym_system(N=30000, seed=4)
+    z = np.random.default_rng(9).standard_normal(S["N"])
+    opts = dict(F.EXPROG_OPTS, mem=20, itmax=60)
+
+    def work(ctx, r):
+        M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx, krylov_A=S["Q"])
+        M.nitref, M.force_itref = 1, True
+        y = M * z
+        x, yy, st = cpk.cpdqgmres(S["rhs"][:S["n"]], S["Q"], S["C"], M, opts)[:3]
+        return y, M.export_factors() if r == 0 else None, x, yy, st
+
+    res = _run_ranks(P, work)
+    L, D, perm = res[0][1]
+    Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=(L, D, perm))
+    Mo.set(nitref=1.0, force_itref=1.0)
+    yo = Mo @ z
+    for y, *_ in res:
+        assert np.array_equal(y, yo)
+    xo, yyo, so = O.method("dqgmres", S["rhs"][:S["n"]], S["Q"], S["C"], Mo, opts)
+    _, _, x, yy, st = res[0]
+    assert st["niters"] == so["niters"]
+    h, ho = st["residHistory"], so["residHistory"]
+    assert len(h) == len(ho) and np.max(np.abs(h - ho)) <= 1e-8 * ho[0]
+    assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
