@@ -1132,17 +1132,24 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
     }
 }
 
-// upper round r through sptrsv_upper_kernel when the configuration matches an instantiation
-static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add, const double *xin,
-                        int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in,
-                        double *ys, double *xs) {
-    constexpr int TPB = 512, RPU = 2, EPU = 8;
-    if (getenv("CPK_NO_UPPER") || F.sweep_threads[1] != TPB || F.sweep_rows[1] > RPU * TPB ||
-        F.sweep_cap[1] > EPU * TPB || r >= (int64_t)F.round_fits.size() || !F.round_fits[r])
+template <int TPB, int RPU, int EPU>
+static bool upper_round_t(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add, const double *xin,
+                          int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in,
+                          double *ys, double *xs) {
+    if (F.sweep_threads[1] != TPB || F.sweep_rows[1] > RPU * TPB || F.sweep_cap[1] > EPU * TPB ||
+        r >= (int64_t)F.round_fits.size() || !F.round_fits[r])
         return false;
     const int64_t b0 = F.round_ptr[r], nb = F.round_ptr[r + 1] - b0;
     if (!nb) return true;
     const size_t lds = sweep_lds_bytes(RPU * TPB, EPU * TPB);  // the kernel's image (>= the configured block)
+    static const bool lds_ok = lds <= 64 * 1024 ||
+        (hipFuncSetAttribute((const void *)sptrsv_upper_kernel<TPB, RPU, EPU, false, false>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
+         hipFuncSetAttribute((const void *)sptrsv_upper_kernel<TPB, RPU, EPU, true, true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
+         hipFuncSetAttribute((const void *)sptrsv_upper_kernel<TPB, RPU, EPU, true, false>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess);
+    if (!lds_ok) return false;
     const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
     if (!bwd)
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, false, false>), dim3((unsigned)nb), dim3(TPB), lds,
@@ -1157,6 +1164,16 @@ static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add,
                            c.stream, b0, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, xin,
                            neg_from, w, out, run, active, sched_in, ys, xs);
     return true;
+}
+
+// upper round r through sptrsv_upper_kernel when the configuration matches the instantiation
+// (512 threads: blocks of <= 1024 rows / 4096 entries).  Measured at S10 and not kept: 1024
+// threads with blocks of 1536 / 6144 and 2048 / 8192 (still 4 rounds; sweeps 2-7 % slower).
+static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add, const double *xin,
+                        int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in,
+                        double *ys, double *xs) {
+    if (getenv("CPK_NO_UPPER")) return false;
+    return upper_round_t<512, 2, 8>(c, F, r, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs);
 }
 
 // SPLIT > 1: the workgroup is one wave holding SPLIT independent logical blocks of TPB lanes
