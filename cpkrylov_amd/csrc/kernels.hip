@@ -249,7 +249,7 @@ static inline int grid_of(const DMat &A) { return (int)A.nblk; }
 
 template <class Epi>
 static void spmv_launch(Ctx &c, const DMat &A, const double *x, int64_t col_min, const Epi &e, bool reduces = false) {
-    const unsigned grid = spmv_grid(A.nblk, reduces);
+    const unsigned grid = A.halo() ? spmv_grid<Epi, true>(A.nblk, reduces) : spmv_grid<Epi, false>(A.nblk, reduces);
     if (A.halo())
         hipLaunchKernelGGL((spmv_stream<Epi, true>), dim3(grid), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
                            A.val.p, A.blk.p, A.nblk, x, col_min, e, (const double *)A.rbuf.p, A.nloc);

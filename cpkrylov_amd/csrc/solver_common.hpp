@@ -72,7 +72,10 @@ __device__ __forceinline__ void sym_givens(double a, double b, double &c, double
     }
 }
 
-constexpr int kEwGrid = 1024;  // fixed grid of the streaming vector kernels (deterministic partials)
+#ifndef CPK_EW_GRID
+#define CPK_EW_GRID 1024
+#endif
+constexpr int kEwGrid = CPK_EW_GRID;  // fixed grid of the streaming vector kernels (deterministic partials)
 
 // Elementwise kernel over [0, N): F::setup() loads scalars (false => no-op), F::operator()(i).
 template <class F>

@@ -221,7 +221,8 @@ void launch_krylov_spmv(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n
     const bool dist = c.dist();
     if (AC.halo() && AC.kmax > 0 && !halo_ready) launch_krylov_halo(c, AC, st, pol);
     EpiKrylov<P> e{st, nullptr, y, n, RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr}, pol};
-    const unsigned grid = spmv_grid(AC.nblk, true);
+    const unsigned grid =
+        AC.halo() ? spmv_grid<EpiKrylov<P>, true>(AC.nblk, true) : spmv_grid<EpiKrylov<P>, false>(AC.nblk, true);
     if (AC.halo())
         hipLaunchKernelGGL((spmv_stream<EpiKrylov<P>, true>), dim3(grid), dim3(kBlock), 0, c.stream, AC.ptr.p,
                            AC.col.p, AC.val.p, AC.blk.p, AC.nblk, (const double *)nullptr, (int64_t)0, e,
