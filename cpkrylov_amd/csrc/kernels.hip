@@ -248,8 +248,8 @@ struct EpiResidNorm {
 static inline int grid_of(const DMat &A) { return (int)A.nblk; }
 
 template <class Epi>
-static void spmv_launch(Ctx &c, const DMat &A, const double *x, int64_t col_min, const Epi &e, bool reduces = false) {
-    const unsigned grid = A.halo() ? spmv_grid<Epi, true>(A.nblk, reduces) : spmv_grid<Epi, false>(A.nblk, reduces);
+static void spmv_launch(Ctx &c, const DMat &A, const double *x, int64_t col_min, const Epi &e) {
+    const unsigned grid = A.halo() ? spmv_grid<Epi, true>(A.nblk) : spmv_grid<Epi, false>(A.nblk);
     if (A.halo())
         hipLaunchKernelGGL((spmv_stream<Epi, true>), dim3(grid), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
                            A.val.p, A.blk.p, A.nblk, x, col_min, e, (const double *)A.rbuf.p, A.nloc);
@@ -343,7 +343,7 @@ void launch_spmv_resid_norm(Ctx &c, const DMat &A, const double *xin, int64_t ne
         c.ensure_partials((size_t)A.nblk * 2);
         EpiResidNorm e{xin, neg_from, r, tol, active_out, RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr},
                        run, active};
-        spmv_launch(c, A, y, 0, e, true);
+        spmv_launch(c, A, y, 0, e);
     }
     if (dist) {
         c.comm->allreduce_sum(c.red.p, 2, c.stream);

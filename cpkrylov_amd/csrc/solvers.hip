@@ -178,7 +178,8 @@ __global__ __launch_bounds__(kBlock) void lanczos_step_halo_kernel(int64_t N, F 
                                                                    double *sbuf) {
     if (!f.setup()) return;
     double acc[2] = {0.0, 0.0};
-    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) f(i, acc);
+    for (int64_t i0 = blockIdx.x * (int64_t)kBlock * kTile + threadIdx.x; i0 < N; i0 += (int64_t)gridDim.x * kBlock * kTile)
+        f.tile(i0, N, acc);  // the tiled order of ewtred_kernel (the 1-GPU step): the same partials
     double tot[2];
     bool last = false;
     grid_sum<2>(acc, rb, tot, &last);  // rb.defer: the payload's spare slots
@@ -222,7 +223,7 @@ void launch_krylov_spmv(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n
     if (AC.halo() && AC.kmax > 0 && !halo_ready) launch_krylov_halo(c, AC, st, pol);
     EpiKrylov<P> e{st, nullptr, y, n, RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr}, pol};
     const unsigned grid =
-        AC.halo() ? spmv_grid<EpiKrylov<P>, true>(AC.nblk, true) : spmv_grid<EpiKrylov<P>, false>(AC.nblk, true);
+        AC.halo() ? spmv_grid<EpiKrylov<P>, true>(AC.nblk) : spmv_grid<EpiKrylov<P>, false>(AC.nblk);
     if (AC.halo())
         hipLaunchKernelGGL((spmv_stream<EpiKrylov<P>, true>), dim3(grid), dim3(kBlock), 0, c.stream, AC.ptr.p,
                            AC.col.p, AC.val.p, AC.blk.p, AC.nblk, (const double *)nullptr, (int64_t)0, e,
@@ -293,6 +294,37 @@ struct LanczosStep {
             if (KIND == 1) xy[i] = xy[i] - zeta * W[i];  // y = y - zeta*wq
         }
         vkp1[i] = v;
+    }
+    // kTile elements kBlock apart (ewtred_kernel): every load of the tile in flight at once; the
+    // per-element arithmetic and the thread's accumulation order over its elements are unchanged
+    __device__ void tile(int64_t i0, int64_t Nn, double *acc) {
+        if (i0 + (kTile - 1) * kBlock >= Nn) {
+            for (int e = 0; e < kTile; e++)
+                if (i0 + e * kBlock < Nn) (*this)(i0 + e * kBlock, acc);
+            return;
+        }
+        double p[kTile], a[kTile], b[kTile], u[kTile];
+#pragma unroll
+        for (int e = 0; e < kTile; e++) {
+            const int64_t i = i0 + e * kBlock;
+            p[e] = vprec[i], a[e] = vk[i], b[e] = vkm1[i], u[e] = ut[i];
+        }
+#pragma unroll
+        for (int e = 0; e < kTile; e++) {
+            const int64_t i = i0 + e * kBlock;
+            double v;
+            if (i < n) {
+                v = p[e] - alpha * a[e] - beta * b[e];
+                acc[0] += u[e] * v;
+                if (KIND == 1) xy[i] = xy[i] + zeta * W[i];
+            } else {
+                const double t = a[e] - p[e];
+                v = t - alpha * a[e] - beta * b[e];
+                acc[1] += u[e] * v;
+                if (KIND == 1) xy[i] = xy[i] - zeta * W[i];
+            }
+            vkp1[i] = v;
+        }
     }
     __device__ void fin(const double *tot);
 };
@@ -504,6 +536,27 @@ struct MinresUpdate {
         const double w = (vk[i] - oldeps * w1[i] - delta * w2[i]) / gamma;
         wn[i] = w;
         xy[i] = (i < n) ? xy[i] + tau * w : xy[i] - tau * w;
+    }
+    __device__ void tile(int64_t i0, int64_t Nn) {  // ewt_kernel: the tile's loads all in flight
+        if (i0 + (kTile - 1) * kBlock >= Nn) {
+            for (int e = 0; e < kTile; e++)
+                if (i0 + e * kBlock < Nn) (*this)(i0 + e * kBlock);
+            return;
+        }
+        double q[kTile], a[kTile], b1[kTile], b2[kTile], x[kTile];
+#pragma unroll
+        for (int e = 0; e < kTile; e++) {
+            const int64_t i = i0 + e * kBlock;
+            q[e] = vkp1[i], a[e] = vk[i], b1[e] = w1[i], b2[e] = w2[i], x[e] = xy[i];
+        }
+#pragma unroll
+        for (int e = 0; e < kTile; e++) {
+            const int64_t i = i0 + e * kBlock;
+            if (beta > 0) vkp1[i] = q[e] / beta;
+            const double w = (a[e] - oldeps * b1[e] - delta * b2[e]) / gamma;
+            wn[i] = w;
+            xy[i] = (i < n) ? x[e] + tau * w : x[e] - tau * w;
+        }
     }
 };
 
@@ -1520,9 +1573,9 @@ void SolveCore::minres_like(int kind, const double *b, double *xy, cpk_stats *st
                 ls.sep = M.sep.rbuf.p, ls.sep_ranks = c.nranks, ls.sep_kt = M.sep.kt, ls.sep_data = M.sep.kt_data;
                 launch_lanczos_step_halo(c, AC, st, N, ls);
             } else {
-                launch_ewred<2>(c, N, ls);
+                launch_ewtred<2>(c, N, ls);
             }
-            launch_ew(c, N, MinresUpdate{st, VQ, W, xy, n, N});
+            launch_ewt(c, N, MinresUpdate{st, VQ, W, xy, n, N});
         };
         if (print) print_hist_lines("%5lld  %9.2e\n");
         loop(body, [&]() { print_hist_lines("%5lld  %9.2e\n"); });

@@ -15,9 +15,7 @@
 namespace cpk {
 
 // HALO: distributed rows (DistCsr); column c >= nloc reads the allgathered halo xg[c - nloc].
-// A workgroup handles row blocks blockIdx.x, blockIdx.x + gridDim.x, ...: launched with one
-// block per workgroup for plain products, and with a bounded grid when the epilogue reduces
-// (fewer arrivals on the reduction ticket).
+// A workgroup handles row blocks blockIdx.x, blockIdx.x + gridDim.x, ... (grid: spmv_grid).
 // 6 waves per SIMD (<= 80 VGPRs): the reducing epilogues otherwise take 82 and run 5
 #ifndef CPK_SPMV_WAVES
 #define CPK_SPMV_WAVES 6
@@ -99,14 +97,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CPK_SPMV
     epi.finish();
 }
 
-// Grid of a launch: one row block per workgroup for plain products.  A reducing epilogue gets
-// exactly the workgroups that are resident at once (occupancy x CUs: 6 x 256 = 1536 on MI355X),
-// each walking every 1536th row block, so no second, partial wave of workgroups trails the
-// launch (measured at S10: Krylov SpMV 123 us with a 2048 grid at 5 waves per SIMD, 93 us).
-// Deterministic for a given device: the grid fixes which partials each inner product sums.
+// Grid of a launch: exactly the workgroups that are resident at once (occupancy x CUs: 6 x 256
+// = 1536 on MI355X), each walking every 1536th row block, so no second, partial wave of
+// workgroups trails the launch.  Measured at S10: the Krylov SpMV (reducing) 123 us with a
+// 2048 grid at 5 waves per SIMD, 93-97 us; the residual SpMV (one workgroup per row block
+// before) 125 -> 120 us.  Deterministic for a given device: the grid fixes which partials each
+// inner product sums.
 template <class Epi, bool HALO>
-inline unsigned spmv_grid(int64_t nblk, bool reduces) {
-    if (!reduces) return (unsigned)nblk;
+inline unsigned spmv_grid(int64_t nblk) {
     static const int64_t resident = [] {
         int occ = 0, dev = 0, cus = 256;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)spmv_stream<Epi, HALO>, kBlock, 0) !=
