@@ -110,6 +110,8 @@ struct DFactor {
     int64_t ndet = 0;     // detached rows [0, ndet): no forward entries, in no block (Schedule::ndet)
     DBuf<uint32_t> fptr;  // forward rows of strict lower L, columns ascending
     DBuf<int32_t> fcol;
+    DBuf<int16_t> fcol16;  // round 0 when every forward entry is local: column - block's first row (else empty)
+    int64_t nnz16 = 0;     // forward entries stored in fcol16 (10 bytes each instead of 12)
     DBuf<double> fval;
     DBuf<uint32_t> bptr;  // backward rows (= columns of L), row indices descending
     DBuf<int32_t> bcol;
@@ -124,7 +126,7 @@ struct DFactor {
     std::vector<char> round_fits;    // host: every block of round r fits (sweep_rows[1], sweep_cap[1])
     int sweep_rows[2] = {192, 1024}, sweep_cap[2] = {576, 4096}, sweep_threads[2] = {64, 512};  // round 0 / rest
     size_t bytes() const {
-        return fptr.bytes() + fcol.bytes() + fval.bytes() + bptr.bytes() + bcol.bytes() + bval.bytes() + D.bytes() +
+        return fptr.bytes() + fcol.bytes() + fcol16.bytes() + fval.bytes() + bptr.bytes() + bcol.bytes() + bval.bytes() + D.bytes() +
                perm.bytes() + blk_lvl.bytes() + lvl_row.bytes() + meta.bytes();
     }
 };

@@ -171,6 +171,30 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     }
     d.meta.upload(meta);
     d.pipelined = getenv("CPK_NO_PIPE") == nullptr;
+    // round 0's forward entries as 16-bit block-local columns: a round-0 block holds whole
+    // subtrees, so a row's forward columns (its descendants) are in its own block unless rows
+    // were detached; checked here, and the image is only built when it holds for every block
+    d.fcol16.release();
+    d.nnz16 = 0;
+    if (s.ndet == 0 && s.round_ptr.size() >= 2 && !getenv("CPK_NO_COL16")) {
+        bool ok = true;
+        int64_t e_end = 0;
+        for (int64_t b = s.round_ptr[0]; b < s.round_ptr[1] && ok; b++) {
+            const int32_t *m = &meta[(size_t)b * 8];
+            if (m[1] - m[0] > INT16_MAX) ok = false;
+            for (int32_t e = m[4]; e < m[5] && ok; e++) ok = fcol[e] >= m[0] && fcol[e] < m[1];
+            e_end = std::max<int64_t>(e_end, m[5]);
+        }
+        if (ok) {
+            std::vector<int16_t> c16((size_t)e_end + kFactorPadEntries, 0);
+            for (int64_t b = s.round_ptr[0]; b < s.round_ptr[1]; b++) {
+                const int32_t *m = &meta[(size_t)b * 8];
+                for (int32_t e = m[4]; e < m[5]; e++) c16[e] = (int16_t)(fcol[e] - m[0]);
+                d.nnz16 += m[5] - m[4];
+            }
+            d.fcol16.upload(c16);
+        }
+    }
 }
 
 // ---- SpMV launchers --------------------------------------------------------------------------
@@ -1180,7 +1204,7 @@ static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add,
 // (TPB * SPLIT = 64), each with its own LDS image.  A level that occupies a few rows then costs
 // one instruction stream for SPLIT blocks instead of one per block; lanes of different logical
 // blocks never synchronise (within a single wave __syncthreads is a no-op fence).
-template <int TPB, int RPT, int EPT, bool BWD, bool ADD, int SPLIT = 1>
+template <int TPB, int RPT, int EPT, bool BWD, bool ADD, int SPLIT = 1, bool LOC = false>
 #ifndef CPK_PIPE_WAVES
 #define CPK_PIPE_WAVES 4  // waves per SIMD the round-0 kernel's registers allow (4: 128 VGPRs)
 #endif
@@ -1189,8 +1213,9 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,
     int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
-    int skip0, double *xs) {
+    int skip0, double *xs, const int16_t *__restrict__ col16) {
     static_assert(SPLIT == 1 || TPB * SPLIT == 64, "split blocks must share one wave");
+    static_assert(!LOC || !BWD, "block-local columns: forward round 0 only");
     // perm is read for the forward gather (unless the input is in schedule order) and for the
     // backward scatter (unless the solution stays in schedule order)
     const bool need_perm = BWD ? out != nullptr : !sched_in;
@@ -1223,8 +1248,11 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
             const int e = tid + j * TPB;
-            if (e < ne)  // streamed once per sweep: non-temporal, keeps L2 for the gathered vector
-                cc[j] = __builtin_nontemporal_load(col + e0 + e), vv[j] = __builtin_nontemporal_load(val + e0 + e);
+            if (e < ne) {  // streamed once per sweep: non-temporal, keeps L2 for the gathered vector
+                if (LOC) cc[j] = __builtin_nontemporal_load(col16 + e0 + e);
+                else cc[j] = __builtin_nontemporal_load(col + e0 + e);
+                vv[j] = __builtin_nontemporal_load(val + e0 + e);
+            }
         }
     };
     int64_t b = blk0 + (int64_t)blockIdx.x * SPLIT + sub;
@@ -1275,10 +1303,15 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
         for (int j = 0; j < EPT; j++) {
             const int e = tid + j * TPB;
             if (e < ne) {
-                const int32_t c = cc[j];
-                const bool local = c >= r0 && c < r1;
-                S.c[e] = local ? (int16_t)(c - r0) : (int16_t)R;
-                S.v[e] = local ? vv[j] : vv[j] * (BWD ? g[j] : w[c]);
+                if (LOC) {  // already block-local (fcol16)
+                    S.c[e] = (int16_t)cc[j];
+                    S.v[e] = vv[j];
+                } else {
+                    const int32_t c = cc[j];
+                    const bool local = c >= r0 && c < r1;
+                    S.c[e] = local ? (int16_t)(c - r0) : (int16_t)R;
+                    S.v[e] = local ? vv[j] : vv[j] * (BWD ? g[j] : w[c]);
+                }
             }
         }
         __syncthreads();
@@ -1320,9 +1353,11 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
     const int64_t nb = F.round_ptr[1] - F.round_ptr[0];
     const size_t lds = sweep_lds_bytes(RPT * TPB, EPT * TPB) * SPLIT;
     int occ = 0;
+    const bool loc = !bwd && F.fcol16.n > 0;
     const void *fn = bwd ? (add ? (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>
                                 : (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>)
-                         : (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>;
+                         : loc ? (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true>
+                               : (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, TPB * SPLIT, lds) != hipSuccess || occ < 1) occ = 1;
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
@@ -1330,18 +1365,26 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>((nb + SPLIT - 1) / SPLIT, (int64_t)occ * cus));
     const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
     const dim3 blk(TPB * SPLIT);
-    if (!bwd)
+    if (loc)
+        hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true>), dim3((unsigned)grid), blk,
+                           lds, c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, 1, xs,
+                           (const int16_t *)F.fcol16.p);
+    else if (!bwd)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs);
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
+                           (const int16_t *)nullptr);
     else if (add)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs);
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
+                           (const int16_t *)nullptr);
     else
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs);
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
+                           (const int16_t *)nullptr);
     return true;
 }
 

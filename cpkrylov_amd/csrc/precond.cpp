@@ -343,7 +343,7 @@ double Precond::apply_bytes() const {
     // SpTRSV sweep over the strict factor (l entries): 12*l + 4*(N+1) + 16*N (vector in/out)
     // + 4*N (perm) ; backward adds D (8*N) and the scatter (8*N, +8*N when accumulating).
     const double l = (double)dF.nnz, Nn = (double)N;
-    const double fwd = 12 * l + 4 * (Nn + 1) + 16 * Nn + 4 * Nn;
+    const double fwd = 12 * l - 2 * (double)dF.nnz16 + 4 * (Nn + 1) + 16 * Nn + 4 * Nn;  // fcol16: 10 B per entry
     const double bwd = 12 * l + 4 * (Nn + 1) + 16 * Nn + 4 * Nn + 8 * Nn + 8 * Nn;
     const double kp = 12 * (double)dKp.nnz + 4 * (Nn + 1) + 8 * Nn /*y*/ + 8 * Nn /*x*/ + 8 * Nn /*r*/;
     const int64_t steps = nitref > 0 ? (int64_t)nitref : 0;
@@ -355,7 +355,7 @@ double Precond::apply_bytes() const {
         const double bwd_keep = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn;
         const double kps = 12 * (double)dKps.nnz + 4 * (Nn + 1) + 8 * Nn /*y*/ +
                            (xs.n ? 8 * Nn /*xs*/ : 12 * Nn /*x(perm)*/) + 8 * Nn /*r*/;
-        const double fwd_s = 12 * l + 4 * (Nn + 1) + 16 * Nn - 16 * (double)dF.ndet;  // in place: detached rows untouched
+        const double fwd_s = 12 * l - 2 * (double)dF.nnz16 + 4 * (Nn + 1) + 16 * Nn - 16 * (double)dF.ndet;  // in place: detached rows untouched
         const double bwd_acc = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn + 8 * Nn /*ys*/;
         double b = fwd + (xs.n ? 8 * Nn : 0.0) /*xs written*/ + bwd_keep + steps * (kps + fwd_s + bwd_acc) + (4 + 8) * Nn /*last: perm + scatter*/ +
                    (steps - 1) * 8.0 * Nn /*ys written back in place*/;

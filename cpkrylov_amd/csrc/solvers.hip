@@ -1960,7 +1960,7 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
         out->fwd_ms = timeit([&]() { launch_sptrsv_fwd_diag(c, M.dF, x.p, M.n, M.w.p); });
     else
         out->fwd_ms = timeit([&]() { launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr); });
-    out->fwd_bytes = 12.0 * l + 4.0 * (Nn + 1) + 4.0 * Nn /*perm*/ + 8.0 * Nn /*x*/ + 8.0 * Nn /*w*/;
+    out->fwd_bytes = 12.0 * l - 2.0 * (double)M.dF.nnz16 + 4.0 * (Nn + 1) + 4.0 * Nn /*perm*/ + 8.0 * Nn /*x*/ + 8.0 * Nn /*w*/;
     out->bwd_ms = timeit([&]() { launch_sptrsv_bwd(c, M.dF, M.w.p, z.p, false, nullptr, nullptr); });
     out->bwd_bytes = 12.0 * l + 4.0 * (Nn + 1) + 4.0 * Nn + 8.0 * Nn /*D*/ + 8.0 * Nn /*w in*/ + 8.0 * Nn /*w out*/ +
                      8.0 * Nn /*y*/;
