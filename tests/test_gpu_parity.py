@@ -241,3 +241,24 @@ def test_precond_apply_plain_refinement_path(gpu_ctx, name, monkeypatch):
     Mo = O.LDL2(P["G"], P["B"], -P["C"], factors=(L, D, perm))
     Mo.set(nitref=2.0, force_itref=1.0)
     assert np.array_equal(ys[0], ys[1]) and np.array_equal(ys[0], Mo @ z)
+
+
+@pytest.mark.parametrize("name", ["cvxqp1_m", "cvxqp2_s", "syn_symm20k"])
+def test_precond_apply_int32_round0_columns(gpu_ctx, name, monkeypatch):
+    """CPK_NO_COL16: round 0's forward sweep stages int32 global columns with the locality test
+    instead of the stored block-local int16 columns; the same bits as the default path and the
+    oracle."""
+    import cpkrylov_amd as cpk
+    P = F.load(name)
+    z = np.random.default_rng(17).standard_normal(P["n"] + P["m"])
+    ys = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("CPK_NO_COL16", env)
+        M = cpk.opLDL2(P["G"], P["B"], -P["C"])
+        M.nitref, M.force_itref = 1, True
+        ys.append(M * z)
+    L, D, perm = M.export_factors()
+    Mo = O.LDL2(P["G"], P["B"], -P["C"], factors=(L, D, perm))
+    Mo.set(nitref=1.0, force_itref=1.0)
+    assert np.array_equal(ys[0], ys[1]) and np.array_equal(ys[0], Mo @ z)
