@@ -154,15 +154,21 @@ inline void launch_ewred(Ctx &c, int64_t N, const F &f) {
         hipLaunchKernelGGL(ewred_fin_kernel<F>, dim3(1), dim3(64), 0, c.stream, f, (const double *)c.red.p);
     }
 }
+#ifndef CPK_EWT_GRID
+#define CPK_EWT_GRID kEwGrid
+#endif
+inline int ewt_grid(int64_t N) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>((N + kBlock - 1) / kBlock, CPK_EWT_GRID));
+}
 template <class F>
 inline void launch_ewt(Ctx &c, int64_t N, const F &f) {
-    hipLaunchKernelGGL(ewt_kernel<F>, dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f);
+    hipLaunchKernelGGL(ewt_kernel<F>, dim3(ewt_grid(N)), dim3(kBlock), 0, c.stream, N, f);
 }
 template <int NV, class F>
 inline void launch_ewtred(Ctx &c, int64_t N, const F &f) {
-    c.ensure_partials((size_t)ew_grid(N) * NV);
+    c.ensure_partials((size_t)ewt_grid(N) * NV);
     const bool dist = c.dist();
-    hipLaunchKernelGGL((ewtred_kernel<NV, F>), dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f,
+    hipLaunchKernelGGL((ewtred_kernel<NV, F>), dim3(ewt_grid(N)), dim3(kBlock), 0, c.stream, N, f,
                        RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr});
     if (dist) {
         c.comm->allreduce_sum(c.red.p, NV, c.stream);

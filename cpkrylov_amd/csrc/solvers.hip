@@ -871,7 +871,14 @@ __device__ inline double &Hd(DState *st, int64_t j, int64_t kk) {  // H(j, kk), 
 
 // V(:,k+1) = w(1:n) ; Q(:,k+1) = Q(:,k) - w(n+1:N) ; H(j,k) = dot(V_j,u) + dot(Q_j,t) for the window
 // (cpgmres.m:212-215, cpdqgmres.m:208-213).  All window dots in one streaming pass.
-constexpr int kDotGroup = 16;
+#ifndef CPK_DOT_GROUP
+#define CPK_DOT_GROUP 8
+#endif
+#ifndef CPK_DOT_TILE
+#define CPK_DOT_TILE 3
+#endif
+constexpr int kDotGroup = CPK_DOT_GROUP;
+constexpr int kDotTile = CPK_DOT_TILE;  // elements per thread per step, kBlock apart
 __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double *V, const double *w,
                                                               const double *ut, int64_t n, int64_t N, int64_t ring,
                                                               int64_t maxv, RedBuf rb) {
@@ -892,17 +899,45 @@ __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double
 #pragma unroll
         for (int j = 0; j < kDotGroup; j++) vj[j] = (g0 + j < win.nv) ? V + win.slot(win.jlo + g0 + j) * N : nullptr;
         bool crossed = false;
-        for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) {
-            if (!crossed && i >= n) {
+        if (kDotTile == 1) {
+            for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) {
+                if (!crossed && i >= n) {
 #pragma unroll
-                for (int j = 0; j < kDotGroup; j++) accn[j] = acc[j], acc[j] = 0.0;
-                crossed = true;
+                    for (int j = 0; j < kDotGroup; j++) accn[j] = acc[j], acc[j] = 0.0;
+                    crossed = true;
+                }
+                const double u = ut[i];
+                if (g0 == 0) vnew[i] = i < n ? w[i] : vk[i] - w[i];
+#pragma unroll
+                for (int j = 0; j < kDotGroup; j++)
+                    if (vj[j]) acc[j] += vj[j][i] * u;
             }
-            const double u = ut[i];
-            if (g0 == 0) vnew[i] = i < n ? w[i] : vk[i] - w[i];
+        } else {
+            for (int64_t i0 = blockIdx.x * (int64_t)kBlock * kDotTile + threadIdx.x; i0 < N;
+                 i0 += (int64_t)gridDim.x * kBlock * kDotTile) {
+                double u[kDotTile], x[kDotTile][kDotGroup];
 #pragma unroll
-            for (int j = 0; j < kDotGroup; j++)
-                if (vj[j]) acc[j] += vj[j][i] * u;
+                for (int e = 0; e < kDotTile; e++) {
+                    const int64_t i = min(i0 + e * kBlock, N - 1);  // clamped: loads need no predicate
+                    u[e] = ut[i];
+#pragma unroll
+                    for (int j = 0; j < kDotGroup; j++) x[e][j] = vj[j] ? vj[j][i] : 0.0;
+                }
+#pragma unroll
+                for (int e = 0; e < kDotTile; e++) {
+                    const int64_t i = i0 + e * kBlock;
+                    if (i >= N) break;
+                    if (!crossed && i >= n) {
+#pragma unroll
+                        for (int j = 0; j < kDotGroup; j++) accn[j] = acc[j], acc[j] = 0.0;
+                        crossed = true;
+                    }
+                    if (g0 == 0) vnew[i] = i < n ? w[i] : vk[i] - w[i];
+#pragma unroll
+                    for (int j = 0; j < kDotGroup; j++)
+                        if (vj[j]) acc[j] += x[e][j] * u[e];
+                }
+            }
         }
         if (!crossed) {
 #pragma unroll
@@ -982,7 +1017,19 @@ static void launch_arnoldi_dots(Ctx &c, DState *st, double *V, const double *w, 
                                 int64_t ring, int64_t maxv) {
     const bool dist = c.dist();
     if (dist && (size_t)(2 * maxv) > c.red.n) throw Error(CPK_ERR_UNSUPPORTED, "Arnoldi window too wide for the distributed reduction buffer");
-    hipLaunchKernelGGL(arnoldi_dots_kernel, dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, st, V, w, ut, n, N, ring, maxv,
+    // at most the resident workgroups (occupancy x CUs): a trailing partial wave of workgroups
+    // would double the pass's tail (cf. spmv_grid)
+    static const int resident = [] {
+        int occ = 0, dev = 0, cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)arnoldi_dots_kernel, kBlock, 0) != hipSuccess ||
+            occ < 1)
+            occ = 1;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return occ * cus;
+    }();
+    const int grid = std::min(ew_grid(N), resident);
+    hipLaunchKernelGGL(arnoldi_dots_kernel, dim3(grid), dim3(kBlock), 0, c.stream, st, V, w, ut, n, N, ring, maxv,
                        RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr});
     if (dist) {
         c.comm->allreduce_sum(c.red.p, (size_t)(2 * maxv), c.stream);
@@ -1376,8 +1423,9 @@ struct SolveCore {
         }
         CPK_HIP(hipMemcpyAsync(dst.p, &h, sizeof h, hipMemcpyHostToDevice, c.stream));
         size_t need = std::max<size_t>((size_t)AC.nblk * 2, (size_t)M.dKp.nblk * 2);
-        need = std::max<size_t>(need, (size_t)kEwGrid * 2);
-        need = std::max<size_t>(need, (size_t)kEwGrid * 2 * std::max<int64_t>(maxv, 1));
+        const size_t ewg = (size_t)std::max<int64_t>(kEwGrid, ewt_grid(N));
+        need = std::max<size_t>(need, ewg * 2);
+        need = std::max<size_t>(need, ewg * 2 * std::max<int64_t>(maxv, 1));
         c.ensure_partials(need);
     }
 
