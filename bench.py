@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE passes")
     ap.add_argument("--dist", action="store_true", help="run the distributed path even on one GPU (1-rank RCCL)")
     ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--rhs-perturb", type=float, default=0.0,
+                    help="scale the rhs by (1 + eps*u), u uniform in [-1, 1] (sensitivity runs; never the bench line)")
+    ap.add_argument("--perturb-seed", type=int, default=1)
     a = ap.parse_args()
     s50 = a.config == "s50"
     if a.size is None:
@@ -141,7 +144,11 @@ def main():
     M.residual_update, M.force_itref = EXPROG_OPTS["residual_update"], EXPROG_OPTS["force_itref"]
     dofs, n_loc = M.local_dofs()
     N_loc = len(dofs)
-    b = torch.from_numpy(np.ascontiguousarray(S["rhs"][dofs])).to(dev)
+    rhs = S["rhs"]
+    if args.rhs_perturb:
+        u = np.random.default_rng(args.perturb_seed).uniform(-1.0, 1.0, rhs.shape[0])
+        rhs = rhs * (1.0 + args.rhs_perturb * u)
+    b = torch.from_numpy(np.ascontiguousarray(rhs[dofs])).to(dev)
     b1 = torch.empty(max(n_loc, 1), dtype=torch.float64, device=dev)
     xy0 = torch.empty(max(N_loc, 1), dtype=torch.float64, device=dev)
     xy = torch.empty(max(N_loc, 1), dtype=torch.float64, device=dev)
@@ -244,7 +251,9 @@ def main():
                        "sweep_launches": M.info["nrounds"], "elim_tree_depth": M.info["depth"],
                        "parallelism": f"rowblock{world}" if distributed else "single",
                        "seed": S["seed"],
-                       "rows_local_rank0": N_loc},
+                       "rows_local_rank0": N_loc,
+                       **({"rhs_perturb": args.rhs_perturb, "perturb_seed": args.perturb_seed}
+                          if args.rhs_perturb else {})},
             "iters_per_step": round(float(iters) / args.steps, 2), "solved": solved,
             "roofline": roofline,
             "spmv_roofline": spmv_roofline,
