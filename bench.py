@@ -218,6 +218,10 @@ def main():
                    "GBps": round(gbs(getattr(prof, k + "_bytes"), getattr(prof, k + "_ms")), 1)}
                for k in ("spmv", "resid", "fwd", "bwd", "apply")}
     kernels["fwd"]["launches"] = kernels["bwd"]["launches"] = int(prof.fwd_launches)
+    if prof.fwd_resid_ms > 0:  # the refinement's residual + forward sweep, fused (launch_sptrsv_fwd_resid)
+        kernels["fwd_resid"] = {"avg_ms": round(prof.fwd_resid_ms, 5), "bytes": prof.fwd_resid_bytes,
+                                "GBps": round(gbs(prof.fwd_resid_bytes, prof.fwd_resid_ms), 1),
+                                "replaces_ms": round(prof.resid_ms + prof.fwd_ms, 5)}
 
     cpu = None
     parity = None

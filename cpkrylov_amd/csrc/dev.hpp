@@ -122,6 +122,7 @@ struct DFactor {
     DBuf<int32_t> lvl_row;  // [nlvl + 1]
     DBuf<int32_t> meta;     // [nblk][8]: r0, r1, l0, l1, fwd e0, e1, bwd e0, e1
     bool pipelined = true;  // round 0 through the persistent pipelined kernel
+    int64_t round0_rows = -1;  // round 0 is the rows [0, round0_rows) (-1: not a leading row range)
     std::vector<int64_t> round_ptr;  // host copy: blocks per round
     std::vector<char> round_fits;    // host: every block of round r fits (sweep_rows[1], sweep_cap[1])
     int sweep_rows[2] = {192, 1024}, sweep_cap[2] = {576, 4096}, sweep_threads[2] = {64, 512};  // round 0 / rest
@@ -180,6 +181,14 @@ void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
 // original-order residual bit for bit
 void launch_spmv_resid_sched(Ctx &c, const DMat &A, const int32_t *perm, const double *xin, int64_t neg_from,
                              const double *y, double *r, const int *run);
+// fused refinement input: r = xs - Kps*y, then the forward sweep in place on r (schedule order);
+// round 0 forms r inside the sweep, the rows above it (tail_blk: Kps row blocks of rows >=
+// round0_rows) through the residual SpMV.  Bit-identical to launch_spmv_resid_sched +
+// launch_sptrsv_fwd(sched_in).  False (nothing launched): no matching configuration.
+bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const int32_t *tail_blk, int64_t tail_nblk,
+                             const double *xs, const double *y, double *r, const int *run);
+// Kps row blocks of the rows [row0, nrows) (A.blk with a boundary at row0)
+void make_tail_blk(const DMat &A, int64_t row0, DBuf<int32_t> &blk, int64_t &nblk);
 // out[i] = x[idx[i]]
 void launch_gather(Ctx &c, const double *x, const int32_t *idx, int64_t n, double *out);
 // small vector helpers
@@ -290,6 +299,9 @@ struct Precond {
     // accumulated solution all stay in schedule order (apply); kps_from: Kps entry -> Kp entry
     DMat dKps;
     DBuf<int32_t> kps_from;
+    // fused refinement residual (launch_sptrsv_fwd_resid): Kps row blocks of the rows above round 0
+    DBuf<int32_t> kps_tail_blk;
+    int64_t kps_tail_nblk = -1;  // -1: the fused path is off
     DBuf<double> xs;     // the apply's signed input in schedule order (captured by the first forward sweep)
     uint64_t pattern_hash = 0;  // sparsity of (A11, B, C22): a refactorization must keep it
     DBuf<int> active;    // refinement predicate

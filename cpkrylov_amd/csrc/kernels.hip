@@ -170,6 +170,13 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
         m[4] = (int32_t)fptr[r0], m[5] = (int32_t)fptr[r1], m[6] = (int32_t)bptr[r0], m[7] = (int32_t)bptr[r1];
     }
     d.meta.upload(meta);
+    d.round0_rows = -1;
+    if (s.ndet == 0 && s.round_ptr.size() >= 2) {  // round 0 a leading, contiguous row range?
+        int64_t r = 0;
+        for (int64_t b = s.round_ptr[0]; b < s.round_ptr[1] && r >= 0; b++)
+            r = meta[(size_t)b * 8] == r ? meta[(size_t)b * 8 + 1] : -1;
+        d.round0_rows = r;
+    }
     d.pipelined = getenv("CPK_NO_PIPE") == nullptr;
     // round 0's forward entries as 16-bit block-local columns: a round-0 block holds whole
     // subtrees, so a row's forward columns (its descendants) are in its own block unless rows
@@ -1071,6 +1078,20 @@ struct BlkMeta {
     int32_t r0, r1, l0, l1, fe0, fe1, be0, be1;
 };
 
+// Fused refinement residual (RES): the forward sweep's input r = xs - Kps*y for the block's rows,
+// formed inside the sweep instead of by a residual SpMV launch (opLDL2.m:175-182, one refinement
+// step).  Kps, y and xs are in schedule order, so a block's Kps rows are one contiguous entry
+// range: the entries are streamed coalesced (prefetched with the block), the products staged in
+// the block's entry region of LDS, and each row summed in Kps's column order from 0.0, then
+// subtracted from xs: the operations of spmv_stream<EpiResidSched>, bit for bit.
+struct ResArgs {
+    const uint32_t *ptr = nullptr;  // Kps rows
+    const int32_t *col = nullptr;
+    const double *val = nullptr;
+    const double *y = nullptr;   // the current solution in schedule order
+    const double *xs = nullptr;  // the signed input in schedule order
+};
+
 // ---- upper rounds ------------------------------------------------------------------------------
 // One workgroup per block, as sptrsv_fwd_kernel / sptrsv_bwd_kernel, with the staging laid out
 // for memory-level parallelism: the block's 32-byte record is one scalar load, every thread
@@ -1204,7 +1225,7 @@ static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add,
 // (TPB * SPLIT = 64), each with its own LDS image.  A level that occupies a few rows then costs
 // one instruction stream for SPLIT blocks instead of one per block; lanes of different logical
 // blocks never synchronise (within a single wave __syncthreads is a no-op fence).
-template <int TPB, int RPT, int EPT, bool BWD, bool ADD, int SPLIT = 1, bool LOC = false>
+template <int TPB, int RPT, int EPT, bool BWD, bool ADD, int SPLIT = 1, bool LOC = false, bool RES = false>
 #ifndef CPK_PIPE_WAVES
 #define CPK_PIPE_WAVES 4  // waves per SIMD the round-0 kernel's registers allow (4: 128 VGPRs)
 #endif
@@ -1213,9 +1234,10 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,
     int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
-    int skip0, double *xs, const int16_t *__restrict__ col16) {
+    int skip0, double *xs, const int16_t *__restrict__ col16, ResArgs ra) {
     static_assert(SPLIT == 1 || TPB * SPLIT == 64, "split blocks must share one wave");
     static_assert(!LOC || !BWD, "block-local columns: forward round 0 only");
+    static_assert(!RES || (LOC && SPLIT == 1), "fused residual: forward round 0 with block-local columns");
     // perm is read for the forward gather (unless the input is in schedule order) and for the
     // backward scatter (unless the solution stays in schedule order)
     const bool need_perm = BWD ? out != nullptr : !sched_in;
@@ -1232,10 +1254,22 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     double wr[RPT], dr[RPT];
     int32_t cc[EPT];
     double vv[EPT];
+    // RES: the block's Kps entry range, its rows' Kps pointers and xs, and the first chunk of
+    // Kps entries (CAP of them)
+    uint32_t kb0 = 0, kb1 = 0;
+    int32_t kc[RES ? EPT : 1];  // columns only: the values load beside the y gathers
     auto issue = [&](const BlkMeta &m) {
         const int nr = m.r1 - m.r0, nl = m.l1 - m.l0;
         const uint32_t e0 = BWD ? (uint32_t)m.be0 : (uint32_t)m.fe0;
         const int ne = BWD ? m.be1 - m.be0 : m.fe1 - m.fe0;
+        if (RES) {
+            kb0 = ra.ptr[m.r0], kb1 = ra.ptr[m.r1];
+#pragma unroll
+            for (int j = 0; j < (RES ? EPT : 0); j++) {
+                const uint32_t e = kb0 + (uint32_t)(tid + j * TPB);
+                if (e < kb1) kc[j] = __builtin_nontemporal_load(ra.col + e);
+            }
+        }
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             const int i = tid + j * TPB;
@@ -1271,19 +1305,87 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             const int i = tid + j * TPB;
-            if (!BWD) xg[j] = xin[sp[j]];
+            if (!BWD && !RES) xg[j] = xin[sp[j]];
             if (BWD && ADD) xg[j] = ys ? ys[r0 + (i < nr ? i : nr - 1)] : out[sp[j]];
+        }
+        if (RES) {  // r = xs - Kps*y for the block's rows, through the (free) value region of LDS
+            // the L columns go to LDS first (their region is not used here): fewer live registers
+#pragma unroll
+            for (int j = 0; j < EPT; j++) {
+                const int e = tid + j * TPB;
+                if (e < ne) S.c[e] = (int16_t)cc[j];
+            }
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {  // likewise the row pointers and level bounds
+                const int i = tid + j * TPB;
+                if (i < nr) S.p[i] = (int16_t)(q[j] - e0);
+                if (i < nl) S.lv[i] = (int16_t)(lvr[j] - r0);
+            }
+            // the rows' Kps pointers and xs load beside the first chunk's gathers (not prefetched
+            // with the block: the level phase holds the next block's registers)
+            uint32_t kqa[RPT], kqb[RPT];
+            double xsr[RPT], acc[RPT];
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+                const int i = tid + j * TPB, rr = r0 + (i < nr ? i : nr - 1);
+                kqa[j] = ra.ptr[rr], kqb[j] = ra.ptr[rr + 1], xsr[j] = ra.xs[rr];
+                acc[j] = 0.0;
+            }
+            for (uint32_t c0 = kb0;; c0 += (uint32_t)CAP) {
+                if (c0 != kb0) {  // a block with more than CAP Kps entries: the next chunk
+#pragma unroll
+                    for (int j = 0; j < (RES ? EPT : 0); j++) {
+                        const uint32_t e = c0 + (uint32_t)(tid + j * TPB);
+                        if (e < kb1) kc[j] = __builtin_nontemporal_load(ra.col + e);
+                    }
+                }
+                // two halves, the second issued after the first is in LDS: half the registers
+                constexpr int H = (EPT + 1) / 2;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    double kv[H], yg[H];
+#pragma unroll
+                    for (int u = 0; u < H; u++) {
+                        const int j = h * H + u;
+                        const uint32_t e = c0 + (uint32_t)(tid + j * TPB);
+                        if (j < EPT) {
+                            kv[u] = __builtin_nontemporal_load(ra.val + (e < kb1 ? e : 0));  // clamped: a valid entry
+                            yg[u] = ra.y[e < kb1 ? kc[j] : 0];
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < H; u++) {
+                        const int j = h * H + u;
+                        const uint32_t e = c0 + (uint32_t)(tid + j * TPB);
+                        if (j < EPT && e < kb1) S.v[e - c0] = kv[u] * yg[u];
+                    }
+                    if (h == 0) asm volatile("" ::: "memory");
+                }
+                __syncthreads();
+                const uint32_t c1 = c0 + (uint32_t)CAP;
+#pragma unroll
+                for (int j = 0; j < RPT; j++) {
+                    if (tid + j * TPB < nr) {
+                        const uint32_t lo = kqa[j] > c0 ? kqa[j] : c0, hi = kqb[j] < c1 ? kqb[j] : c1;
+                        for (uint32_t e = lo; e < hi; e++) acc[j] += S.v[e - c0];
+                    }
+                }
+                __syncthreads();
+                if (kb1 <= c1) break;
+            }
+#pragma unroll
+            for (int j = 0; j < RPT; j++) xg[j] = xsr[j] - acc[j];
         }
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             const int i = tid + j * TPB;
             if (i < nr) {
-                S.p[i] = (int16_t)(q[j] - e0);
+                if (!RES) S.p[i] = (int16_t)(q[j] - e0);
                 if (BWD) S.w[i] = wr[j] / dr[j];
                 else S.w[i] = (sp[j] >= neg_from) ? -xg[j] : xg[j];
                 if (!BWD && xs) xs[r0 + i] = S.w[i];  // the input in schedule order, for the residual
             }
-            if (i < nl) S.lv[i] = (int16_t)(lvr[j] - r0);
+            if (!RES && i < nl) S.lv[i] = (int16_t)(lvr[j] - r0);
         }
         int32_t dst[RPT];
 #pragma unroll
@@ -1304,7 +1406,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
             const int e = tid + j * TPB;
             if (e < ne) {
                 if (LOC) {  // already block-local (fcol16)
-                    S.c[e] = (int16_t)cc[j];
+                    if (!RES) S.c[e] = (int16_t)cc[j];
                     S.v[e] = vv[j];
                 } else {
                     const int32_t c = cc[j];
@@ -1348,13 +1450,16 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
 template <int TPB, int RPT, int EPT, int SPLIT = 1>
 static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
                        double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
-                       double *xs) {
+                       double *xs, const ResArgs *ra = nullptr) {
     if (F.sweep_threads[0] != TPB || F.sweep_rows[0] != RPT * TPB || F.sweep_cap[0] != EPT * TPB) return false;
+    if (ra && (bwd || F.fcol16.n == 0 || SPLIT != 1)) return false;  // fused residual: one instantiation
     const int64_t nb = F.round_ptr[1] - F.round_ptr[0];
     const size_t lds = sweep_lds_bytes(RPT * TPB, EPT * TPB) * SPLIT;
     int occ = 0;
     const bool loc = !bwd && F.fcol16.n > 0;
-    const void *fn = bwd ? (add ? (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>
+    constexpr bool kRes = SPLIT == 1;  // the fused residual kernel exists for unsplit blocks only
+    const void *fn = ra ? (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true, kRes>
+                  : bwd ? (add ? (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>
                                 : (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>)
                          : loc ? (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true>
                                : (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>;
@@ -1365,26 +1470,31 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>((nb + SPLIT - 1) / SPLIT, (int64_t)occ * cus));
     const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
     const dim3 blk(TPB * SPLIT);
-    if (loc)
+    if (ra)
+        hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true, kRes>), dim3((unsigned)grid),
+                           blk, lds, c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p,
+                           F.D.p, F.perm.p, xin, neg_from, w, out, run, active, 1, ys, 1, xs,
+                           (const int16_t *)F.fcol16.p, *ra);
+    else if (loc)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true>), dim3((unsigned)grid), blk,
                            lds, c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, 1, xs,
-                           (const int16_t *)F.fcol16.p);
+                           (const int16_t *)F.fcol16.p, ResArgs{});
     else if (!bwd)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
-                           (const int16_t *)nullptr);
+                           (const int16_t *)nullptr, ResArgs{});
     else if (add)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
-                           (const int16_t *)nullptr);
+                           (const int16_t *)nullptr, ResArgs{});
     else
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
-                           (const int16_t *)nullptr);
+                           (const int16_t *)nullptr, ResArgs{});
     return true;
 }
 
@@ -1464,12 +1574,12 @@ static inline unsigned det_grid(int64_t n) { return (unsigned)std::min<int64_t>(
 
 template <int MODE>
 static void fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                    const int *active, int sched_in, double *xs = nullptr) {
+                    const int *active, int sched_in, double *xs = nullptr, int64_t rfirst = 0) {
     const int64_t R = (int64_t)F.round_ptr.size() - 1;
-    if (F.ndet > 0 && !(sched_in && xin == w))  // in place in schedule order: already there
+    if (F.ndet > 0 && !(sched_in && xin == w) && rfirst == 0)  // in place in schedule order: already there
         hipLaunchKernelGGL(det_fwd_kernel, dim3(det_grid(F.ndet)), dim3(kBlock), 0, c.stream, F.ndet, F.perm.p, xin,
                            neg_from, sched_in, w, run, active);
-    for (int64_t r = 0; r < R; r++) {
+    for (int64_t r = rfirst; r < R; r++) {
         if (r == 0 && MODE == 0 &&
             pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr, xs))
             continue;
@@ -1497,6 +1607,41 @@ void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_
     // schedule-order input: no perm gather and no negation (neg_from applies to original indices)
     if (xs && F.ndet > 0) throw Error(CPK_ERR_UNSUPPORTED, "internal: input capture with detached rows");
     fwd_all<0>(c, F, xin, sched_in ? INT64_MAX : neg_from, w, run, active, sched_in ? 1 : 0, xs);
+}
+
+void make_tail_blk(const DMat &A, int64_t row0, DBuf<int32_t> &blk, int64_t &nblk) {
+    std::vector<int32_t> h((size_t)A.nblk + 1);
+    CPK_HIP(hipMemcpy(h.data(), A.blk.p, h.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    std::vector<int32_t> t{(int32_t)row0};  // splitting a block at row0 only shrinks it
+    for (int32_t b : h)
+        if (b > row0) t.push_back(b);
+    nblk = (int64_t)t.size() - 1;
+    blk.upload(t);
+}
+
+bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const int32_t *tail_blk, int64_t tail_nblk,
+                             const double *xs, const double *y, double *r, const int *run) {
+    const bool off = getenv("CPK_NO_FUSED_RESID") != nullptr;  // A/B switch: separate residual SpMV
+    if (off || tail_nblk < 0 || !F.pipelined || F.ndet != 0 || F.round0_rows < 0 || F.fcol16.n == 0 ||
+        F.round_ptr.size() < 2 || Kps.halo())
+        return false;
+    const ResArgs ra{Kps.ptr.p, Kps.col.p, Kps.val.p, y, xs};
+    // round 0: r of its rows formed in the sweep (nothing is launched unless a configuration matches)
+    if (!(pipe_round<64, 3, 9>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra) ||
+          pipe_round<64, 4, 12>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra) ||
+          pipe_round<128, 2, 6>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra) ||
+          pipe_round<64, 6, 18>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra)))
+        return false;
+    // the rows above round 0: their r by the residual SpMV over those rows, then the upper rounds
+    if (tail_nblk > 0) {
+        const EpiResidSched e{xs, nullptr, 0, r, run};
+        const unsigned grid = spmv_grid<EpiResidSched, false>(tail_nblk);
+        hipLaunchKernelGGL((spmv_stream<EpiResidSched, false>), dim3(grid), dim3(kBlock), 0, c.stream, Kps.ptr.p,
+                           Kps.col.p, Kps.val.p, tail_blk, tail_nblk, y, (int64_t)0, e, (const double *)nullptr,
+                           (int64_t)0);
+    }
+    fwd_all<0>(c, F, r, INT64_MAX, r, run, nullptr, 1, nullptr, 1);
+    return true;
 }
 
 void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,

@@ -132,6 +132,8 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
         pc->kps_from.upload(from);
     }
     if (pc->dKps.nnz && pc->dF.ndet == 0) pc->xs.alloc(pc->N);
+    if (pc->dKps.nnz && pc->dF.round0_rows >= 0 && pc->dF.fcol16.n > 0)
+        make_tail_blk(pc->dKps, pc->dF.round0_rows, pc->kps_tail_blk, pc->kps_tail_nblk);
     clk.lap("schedule-order Kp");
     an.F = Factor();
     pc->F = std::move(an.F0);
@@ -314,9 +316,11 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
         for (int64_t s = 0; s < steps; s++) {
             // r = x - op.A*y; the refinement solve runs in place on r (each row reads its own
             // input before it writes, detached rows keep theirs); y += op.LDL*r
-            if (have_xs) launch_spmv_resid_sched(c, dKps, nullptr, xs.p, 0, w.p, r.p, run);
-            else launch_spmv_resid_sched(c, dKps, dF.perm.p, x, neg_from, w.p, r.p, run);
-            launch_sptrsv_fwd(c, dF, r.p, N, r.p, run, nullptr, true);
+            if (!(have_xs && launch_sptrsv_fwd_resid(c, dF, dKps, kps_tail_blk.p, kps_tail_nblk, xs.p, w.p, r.p, run))) {
+                if (have_xs) launch_spmv_resid_sched(c, dKps, nullptr, xs.p, 0, w.p, r.p, run);
+                else launch_spmv_resid_sched(c, dKps, dF.perm.p, x, neg_from, w.p, r.p, run);
+                launch_sptrsv_fwd(c, dF, r.p, N, r.p, run, nullptr, true);
+            }
             launch_sptrsv_bwd(c, dF, r.p, s + 1 == steps ? y : nullptr, true, run, nullptr, w.p);
         }
         return;

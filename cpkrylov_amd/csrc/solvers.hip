@@ -2015,6 +2015,17 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
     out->apply_ms = timeit([&]() { M.apply(x.p, M.n, z.p, nullptr); });
     out->apply_bytes = M.apply_bytes();
     out->fwd_launches = out->bwd_launches = (int64_t)M.dF.round_ptr.size() - 1;
+    out->fwd_resid_ms = out->fwd_resid_bytes = 0;
+    if (M.sched_path() && M.xs.n &&
+        launch_sptrsv_fwd_resid(c, M.dF, M.dKps, M.kps_tail_blk.p, M.kps_tail_nblk, x.p, y.p, z.p, nullptr)) {
+        out->fwd_resid_ms = timeit([&]() {
+            launch_sptrsv_fwd_resid(c, M.dF, M.dKps, M.kps_tail_blk.p, M.kps_tail_nblk, x.p, y.p, z.p, nullptr);
+        });
+        // Kps, y, xs (the residual's reads) + the factor and w (the sweep's); r never goes to HBM
+        // for round 0 (the tail rows' r write and read are < 1 % and not counted)
+        out->fwd_resid_bytes = 12.0 * M.dKps.nnz + 4.0 * (Nn + 1) + 8.0 * Nn /*y*/ + 8.0 * Nn /*xs*/ + 12.0 * l -
+                               2.0 * (double)M.dF.nnz16 + 4.0 * (Nn + 1) + 8.0 * Nn /*w*/;
+    }
 }
 
 // Algorithmic HBM bytes of one method call: per iteration the Krylov SpMV,

@@ -246,6 +246,8 @@ typedef struct {
     double bwd_ms, bwd_bytes;        /* backward sweep y = P (L' \ (D \ w)) (all rounds) */
     double apply_ms, apply_bytes;    /* one M*z with the current properties */
     int64_t fwd_launches, bwd_launches;
+    double fwd_resid_ms, fwd_resid_bytes;  /* refinement input fused into the forward sweep: r = x - Kp*y,
+                                              then w = L \ P'r (0 when the apply does not fuse it) */
 } cpk_profile;
 int cpk_profile_kernels(cpk_ctx ctx, cpk_mat A, cpk_mat C, cpk_pc M, int reps, cpk_profile *out);
 

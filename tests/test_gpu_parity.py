@@ -262,3 +262,39 @@ def test_precond_apply_int32_round0_columns(gpu_ctx, name, monkeypatch):
     Mo = O.LDL2(P["G"], P["B"], -P["C"], factors=(L, D, perm))
     Mo.set(nitref=1.0, force_itref=1.0)
     assert np.array_equal(ys[0], ys[1]) and np.array_equal(ys[0], Mo @ z)
+
+
+@pytest.mark.parametrize("sweep", [None, "256,768,64", "256,768,128,2048,8192,512", "384,1152,64,2048,8192,512,400"])
+@pytest.mark.parametrize("name", ["cvxqp1_m", "cvxqp2_s", "synthetic"])
+def test_precond_apply_fused_residual(gpu_ctx, name, sweep, monkeypatch):
+    """The refinement residual formed inside the round-0 forward sweep (launch_sptrsv_fwd_resid,
+    opLDL2.m:175-182) against the separate residual SpMV (CPK_NO_FUSED_RESID) and the oracle:
+    the same bits, for one and two refinement steps.  The cvxqp rows carry more Kps entries per
+    block than one LDS chunk holds, so the kernel's chunk loop runs too."""
+    import cpkrylov_amd as cpk
+    from cpkrylov_amd.synthetic import saddle_system
+    if sweep:
+        monkeypatch.setenv("CPK_SWEEP", sweep)
+    if name == "synthetic":
+        S = saddle_system(N=50000)
+        G, B, C = S["G"], S["B"], S["C"]
+    else:
+        P = F.load(name)
+        G, B, C = P["G"], P["B"], P["C"]
+    z = np.random.default_rng(19).standard_normal(G.shape[0] + B.shape[0])
+    for steps in (1, 2):
+        ys = []
+        for env in (None, "1"):
+            if env:
+                monkeypatch.setenv("CPK_NO_FUSED_RESID", env)
+            else:
+                monkeypatch.delenv("CPK_NO_FUSED_RESID", raising=False)
+            M = cpk.opLDL2(G, B, -C)
+            M.nitref, M.force_itref = steps, True
+            ys.append(M * z)
+        L, D, perm = M.export_factors()
+        Mo = O.LDL2(G, B, -C, factors=(L, D, perm))
+        Mo.set(nitref=float(steps), force_itref=1.0)
+        yo = Mo @ z
+        assert np.array_equal(ys[1], yo), np.max(np.abs(ys[1] - yo))
+        assert np.array_equal(ys[0], yo), np.max(np.abs(ys[0] - yo))

@@ -19,5 +19,6 @@ for cfg in sys.argv[1:]:
     _lib.check(_lib.lib.cpk_profile_kernels(ctx.h, A.h, Cm.h, M.h, int(os.environ.get("REPS", "20")), C.byref(p)))
     print(f"{cfg:16s} rounds {M.info['nrounds']} blocks {M.info['nblocks']:6d} fwd {p.fwd_ms*1e3:7.1f} us "
           f"({p.fwd_bytes/p.fwd_ms/1e6:6.0f} GB/s) bwd {p.bwd_ms*1e3:7.1f} us ({p.bwd_bytes/p.bwd_ms/1e6:6.0f} GB/s) "
-          f"apply {p.apply_ms*1e3:7.1f} us resid {p.resid_ms*1e3:6.1f} us spmv {p.spmv_ms*1e3:6.1f} us", flush=True)
+          f"apply {p.apply_ms*1e3:7.1f} us resid {p.resid_ms*1e3:6.1f} us spmv {p.spmv_ms*1e3:6.1f} us "
+          f"fused resid+fwd {p.fwd_resid_ms*1e3:7.1f} us", flush=True)
     del M
