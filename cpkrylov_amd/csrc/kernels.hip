@@ -1090,6 +1090,9 @@ struct ResArgs {
     const double *val = nullptr;
     const double *y = nullptr;   // the current solution in schedule order
     const double *xs = nullptr;  // the signed input in schedule order
+    // rows [tail0, tail1) above round 0: r (into w) by the workgroups once their blocks are done,
+    // one row per lane, entries summed in order from 0.0 (the residual SpMV's row, without a launch)
+    int64_t tail0 = 0, tail1 = 0;
 };
 
 // ---- upper rounds ------------------------------------------------------------------------------
@@ -1291,7 +1294,21 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     };
     int64_t b = blk0 + (int64_t)blockIdx.x * SPLIT + sub;
     const int64_t bend = blk0 + nblk;
-    if (b >= bend) return;
+    auto tail = [&]() {
+        for (int64_t k = ra.tail0 + (int64_t)blockIdx.x * TPB + tid; k < ra.tail1; k += (int64_t)gridDim.x * TPB) {
+            const uint32_t ka = ra.ptr[k], kz = ra.ptr[k + 1];
+            double acc = 0.0;
+            for (uint32_t e = ka; e < kz; e++) {
+                const double p = ra.val[e] * ra.y[ra.col[e]];
+                acc += p;
+            }
+            w[k] = ra.xs[k] - acc;
+        }
+    };
+    if (b >= bend) {
+        if (RES) tail();
+        return;
+    }
     BlkMeta cur = meta[b];
     issue(cur);
     while (true) {
@@ -1443,6 +1460,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
         b = bn;
         cur = nxt;
     }
+    if (RES) tail();
 }
 
 // threads == 32 in a sweep configuration selects the split kernel: 2 logical blocks of 32 lanes
@@ -1625,7 +1643,9 @@ bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const in
     if (off || tail_nblk < 0 || !F.pipelined || F.ndet != 0 || F.round0_rows < 0 || F.fcol16.n == 0 ||
         F.round_ptr.size() < 2 || Kps.halo())
         return false;
-    const ResArgs ra{Kps.ptr.p, Kps.col.p, Kps.val.p, y, xs};
+    // the rows above round 0 inside the round-0 kernel (CPK_FUSED_TAIL_LAUNCH: a residual launch)
+    const bool tail_launch = getenv("CPK_FUSED_TAIL_LAUNCH") != nullptr;
+    const ResArgs ra{Kps.ptr.p, Kps.col.p, Kps.val.p, y, xs, F.round0_rows, tail_launch ? F.round0_rows : F.N};
     // round 0: r of its rows formed in the sweep (nothing is launched unless a configuration matches)
     if (!(pipe_round<64, 3, 9>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra) ||
           pipe_round<64, 4, 12>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra) ||
@@ -1633,7 +1653,7 @@ bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const in
           pipe_round<64, 6, 18>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra)))
         return false;
     // the rows above round 0: their r by the residual SpMV over those rows, then the upper rounds
-    if (tail_nblk > 0) {
+    if (tail_launch && tail_nblk > 0) {
         const EpiResidSched e{xs, nullptr, 0, r, run};
         const unsigned grid = spmv_grid<EpiResidSched, false>(tail_nblk);
         hipLaunchKernelGGL((spmv_stream<EpiResidSched, false>), dim3(grid), dim3(kBlock), 0, c.stream, Kps.ptr.p,

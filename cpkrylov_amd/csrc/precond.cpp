@@ -363,6 +363,9 @@ double Precond::apply_bytes() const {
         const double bwd_acc = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn + 8 * Nn /*ys*/;
         double b = fwd + (xs.n ? 8 * Nn : 0.0) /*xs written*/ + bwd_keep + steps * (kps + fwd_s + bwd_acc) + (4 + 8) * Nn /*last: perm + scatter*/ +
                    (steps - 1) * 8.0 * Nn /*ys written back in place*/;
+        // fused refinement input (launch_sptrsv_fwd_resid): r is neither written nor read back
+        if (xs.n && kps_tail_nblk >= 0 && dF.pipelined && !getenv("CPK_NO_FUSED_RESID"))
+            b -= steps * 16.0 * Nn;
         return b;
     }
     double b = fwd + bwd;

@@ -298,3 +298,29 @@ def test_precond_apply_fused_residual(gpu_ctx, name, sweep, monkeypatch):
         yo = Mo @ z
         assert np.array_equal(ys[1], yo), np.max(np.abs(ys[1] - yo))
         assert np.array_equal(ys[0], yo), np.max(np.abs(ys[0] - yo))
+
+
+@pytest.mark.parametrize("name", ["cvxqp1_m", "cvxqp2_s", "synthetic"])
+def test_precond_apply_fused_residual_tail_launch(gpu_ctx, name, monkeypatch):
+    """The rows above round 0 take their residual from a separate launch (CPK_FUSED_TAIL_LAUNCH)
+    instead of the round-0 kernel's workgroups: the same bits either way, and as the oracle."""
+    import cpkrylov_amd as cpk
+    from cpkrylov_amd.synthetic import saddle_system
+    if name == "synthetic":
+        S = saddle_system(N=50000)
+        G, B, C = S["G"], S["B"], S["C"]
+    else:
+        P = F.load(name)
+        G, B, C = P["G"], P["B"], P["C"]
+    z = np.random.default_rng(23).standard_normal(G.shape[0] + B.shape[0])
+    ys = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("CPK_FUSED_TAIL_LAUNCH", env)
+        M = cpk.opLDL2(G, B, -C)
+        M.nitref, M.force_itref = 1, True
+        ys.append(M * z)
+    L, D, perm = M.export_factors()
+    Mo = O.LDL2(G, B, -C, factors=(L, D, perm))
+    Mo.set(nitref=1.0, force_itref=1.0)
+    assert np.array_equal(ys[0], ys[1]) and np.array_equal(ys[0], Mo @ z)
