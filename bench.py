@@ -234,6 +234,8 @@ def main():
             spmv_roofline["traffic"] = pmc["resid"]["bytes"]
         if pmc and pmc.get("fwd") and pmc.get("bwd"):
             roofline["traffic"] = pmc["fwd"]["bytes"] + pmc["bwd"]["bytes"]
+        if pmc and pmc.get("fwd_resid") and "fwd_resid" in kernels:
+            kernels["fwd_resid"]["traffic"] = pmc["fwd_resid"]["bytes"]
 
     ms_per_step = dt / args.steps * 1e3
     value = total_iters / dt
@@ -384,6 +386,7 @@ def pmc_probe(args):
     _lib.check(_lib.lib.cpk_profile_kernels(ctx.h, A.h, Cm.h, M.h, PMC_REPS, C.byref(prof)))
     print(json.dumps({"resid_bytes": prof.resid_bytes, "spmv_bytes": prof.spmv_bytes,
                       "fwd_bytes": prof.fwd_bytes, "bwd_bytes": prof.bwd_bytes,
+                      "fwd_resid_bytes": prof.fwd_resid_bytes,
                       "rounds": int(prof.fwd_launches)}), flush=True)
 
 
@@ -442,7 +445,13 @@ def pmc_traffic(args):
             if pl:
                 pl = {kk: (vv * R if kk != "launches" else vv // R) for kk, vv in pl.items()}
             out[k] = pl
-        for k in ("resid", "spmv", "fwd", "bwd"):
+        if probe.get("fwd_resid_bytes", 0) > 0:
+            # the fused residual + forward sweep: the last reps x R sweep launches of the profile
+            pl = per_launch(sweep, lambda v: v[len(v) - R * reps:])
+            if pl:
+                pl = {kk: (vv * R if kk != "launches" else vv // R) for kk, vv in pl.items()}
+            out["fwd_resid"] = pl
+        for k in ("resid", "spmv", "fwd", "bwd", "fwd_resid"):
             if out.get(k):
                 out[k]["algorithmic"] = probe[k + "_bytes"]
                 out[k]["ratio"] = round(out[k]["bytes"] / probe[k + "_bytes"], 3)
