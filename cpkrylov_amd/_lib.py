@@ -93,6 +93,7 @@ _SIGS = {
     "cpk_reg_solve_device": ([vp, C.c_int, vp, vp, vp, vp, vp, P(Opts), vp, P(Stats)], C.c_int),
     "cpk_reg_shift_device": ([vp, vp, vp, vp, vp, vp, vp, vp, P(C.c_int)], C.c_int),
     "cpk_profile_kernels": ([vp, vp, vp, vp, C.c_int, P(Profile)], C.c_int),
+    "cpk_debug_pipe_stamps": ([P(C.c_uint64), C.c_int, P(C.c_int)], C.c_int),
     "cpk_symgivens": ([C.c_double, C.c_double, P(C.c_double), P(C.c_double), P(C.c_double)], C.c_int),
 }
 for _name, (_args, _res) in _SIGS.items():

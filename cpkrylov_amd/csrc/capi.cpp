@@ -552,6 +552,13 @@ int cpk_profile_kernels(cpk_ctx ctx, cpk_mat A, cpk_mat C, cpk_pc M, int reps, c
     API_END
 }
 
+int cpk_debug_pipe_stamps(uint64_t *out, int npairs, int *copied) {
+    API_BEGIN
+    need(out && copied, "NULL argument");
+    *copied = debug_pipe_stamps(out, npairs);
+    API_END
+}
+
 int cpk_pc_sep_info(cpk_pc M, int64_t *info) {
     API_BEGIN
     need(M && info, "NULL argument");

@@ -187,6 +187,7 @@ void launch_spmv_resid_sched(Ctx &c, const DMat &A, const int32_t *perm, const d
 // launch_sptrsv_fwd(sched_in).  False (nothing launched): no matching configuration.
 bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const int32_t *tail_blk, int64_t tail_nblk,
                              const double *xs, const double *y, double *r, const int *run);
+int debug_pipe_stamps(uint64_t *out, int npairs);  // diagnostic build only (CPK_PIPE_STAMPS)
 // Kps row blocks of the rows [row0, nrows) (A.blk with a boundary at row0)
 void make_tail_blk(const DMat &A, int64_t row0, DBuf<int32_t> &blk, int64_t &nblk);
 // out[i] = x[idx[i]]

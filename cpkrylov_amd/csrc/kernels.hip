@@ -1228,6 +1228,11 @@ static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add,
 // (TPB * SPLIT = 64), each with its own LDS image.  A level that occupies a few rows then costs
 // one instruction stream for SPLIT blocks instead of one per block; lanes of different logical
 // blocks never synchronise (within a single wave __syncthreads is a no-op fence).
+#ifdef CPK_PIPE_STAMPS
+// diagnostic build only (make HIPEXTRA=-DCPK_PIPE_STAMPS): per-workgroup start / end of the last
+// round-0 launch (s_memrealtime, 100 MHz), read by cpk_debug_pipe_stamps (tools/pipe_stamps.py)
+__device__ uint64_t g_pipe_stamps[2 * 16384];
+#endif
 template <int TPB, int RPT, int EPT, bool BWD, bool ADD, int SPLIT = 1, bool LOC = false, bool RES = false>
 #ifndef CPK_PIPE_WAVES
 #define CPK_PIPE_WAVES 4  // waves per SIMD the round-0 kernel's registers allow (4: 128 VGPRs)
@@ -1292,6 +1297,16 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
             }
         }
     };
+#ifdef CPK_PIPE_STAMPS
+    const uint64_t t_start = (uint64_t)wall_clock64();
+    struct Stamp {
+        uint64_t t0;
+        __device__ ~Stamp() {
+            if (threadIdx.x == 0 && blockIdx.x < 16384)
+                g_pipe_stamps[2 * blockIdx.x] = t0, g_pipe_stamps[2 * blockIdx.x + 1] = (uint64_t)wall_clock64();
+        }
+    } stamp{t_start};
+#endif
     int64_t b = blk0 + (int64_t)blockIdx.x * SPLIT + sub;
     const int64_t bend = blk0 + nblk;
     auto tail = [&]() {
@@ -1625,6 +1640,20 @@ void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_
     // schedule-order input: no perm gather and no negation (neg_from applies to original indices)
     if (xs && F.ndet > 0) throw Error(CPK_ERR_UNSUPPORTED, "internal: input capture with detached rows");
     fwd_all<0>(c, F, xin, sched_in ? INT64_MAX : neg_from, w, run, active, sched_in ? 1 : 0, xs);
+}
+
+// diagnostic: the per-workgroup stamps of the last round-0 launch (0 unless built with
+// CPK_PIPE_STAMPS); returns the number of pairs copied
+int debug_pipe_stamps(uint64_t *out, int npairs) {
+#ifdef CPK_PIPE_STAMPS
+    npairs = std::min(npairs, 16384);
+    CPK_HIP(hipDeviceSynchronize());
+    CPK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pipe_stamps), (size_t)npairs * 2 * sizeof(uint64_t)));
+    return npairs;
+#else
+    (void)out, (void)npairs;
+    return 0;
+#endif
 }
 
 void make_tail_blk(const DMat &A, int64_t row0, DBuf<int32_t> &blk, int64_t &nblk) {

@@ -251,6 +251,11 @@ typedef struct {
 } cpk_profile;
 int cpk_profile_kernels(cpk_ctx ctx, cpk_mat A, cpk_mat C, cpk_pc M, int reps, cpk_profile *out);
 
+/* Diagnostic (no reference counterpart): per-workgroup (start, end) s_memrealtime stamps of the
+ * last round-0 sweep launch, 100 MHz ticks; *copied = 0 unless the library was built with
+ * -DCPK_PIPE_STAMPS (tools/pipe_stamps.py). */
+int cpk_debug_pipe_stamps(uint64_t *out, int npairs, int *copied);
+
 /* [c, s, d] = SymGivens(a, b)  (util/SymGivens.m:1-29) */
 int cpk_symgivens(double a, double b, double *c, double *s, double *d);
 
