@@ -122,7 +122,8 @@ struct DFactor {
     DBuf<int32_t> lvl_row;  // [nlvl + 1]
     DBuf<int32_t> meta;     // [nblk][8]: r0, r1, l0, l1, fwd e0, e1, bwd e0, e1
     bool pipelined = true;  // round 0 through the persistent pipelined kernel
-    int64_t round0_rows = -1;  // round 0 is the rows [0, round0_rows) (-1: not a leading row range)
+    int64_t round0_rows = -1;
+    DBuf<int32_t> queue;  // round-0 block queue: 8 per-XCD counters + exit counter (opt-in)  // round 0 is the rows [0, round0_rows) (-1: not a leading row range)
     std::vector<int64_t> round_ptr;  // host copy: blocks per round
     std::vector<char> round_fits;    // host: every block of round r fits (sweep_rows[1], sweep_cap[1])
     int sweep_rows[2] = {192, 1024}, sweep_cap[2] = {576, 4096}, sweep_threads[2] = {64, 512};  // round 0 / rest

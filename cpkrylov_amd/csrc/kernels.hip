@@ -170,6 +170,7 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
         m[4] = (int32_t)fptr[r0], m[5] = (int32_t)fptr[r1], m[6] = (int32_t)bptr[r0], m[7] = (int32_t)bptr[r1];
     }
     d.meta.upload(meta);
+    d.queue.upload(std::vector<int32_t>(16, 0));  // round-0 block queue counters (CPK_PIPE_QUEUE)
     d.round0_rows = -1;
     if (s.ndet == 0 && s.round_ptr.size() >= 2) {  // round 0 a leading, contiguous row range?
         int64_t r = 0;
@@ -1242,7 +1243,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,
     int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
-    int skip0, double *xs, const int16_t *__restrict__ col16, ResArgs ra) {
+    int skip0, double *xs, const int16_t *__restrict__ col16, ResArgs ra, int *queue) {
     static_assert(SPLIT == 1 || TPB * SPLIT == 64, "split blocks must share one wave");
     static_assert(!LOC || !BWD, "block-local columns: forward round 0 only");
     static_assert(!RES || (LOC && SPLIT == 1), "fused residual: forward round 0 with block-local columns");
@@ -1309,6 +1310,26 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
 #endif
     int64_t b = blk0 + (int64_t)blockIdx.x * SPLIT + sub;
     const int64_t bend = blk0 + nblk;
+    // queue (opt-in, CPK_PIPE_QUEUE, unsplit blocks): instead of a fixed stride, the workgroups of
+    // XCD x (blockIdx % 8) grab the blocks of the x-th eighth one at a time (queue[x]), so the
+    // launch does not end with the slowest fixed share.  Every grab increments, so every wave
+    // exits; the last workgroup out (queue[8]) resets the counters for the next launch.
+    const bool dyn = SPLIT == 1 && TPB == kWave && queue != nullptr;  // one wave: lane 0 broadcasts
+    const int xcd = (int)(blockIdx.x % 8u);
+    const int64_t qlo = blk0 + nblk * xcd / 8, qhi = blk0 + nblk * (xcd + 1) / 8;
+    auto grab_issue = [&]() {
+        int v = 0;
+        if (tid == 0) v = atomicAdd(&queue[xcd], 1);
+        return v;
+    };
+    // lane 0 holds the grab; readfirstlane keeps the block index uniform (scalar metadata loads)
+    auto grab_take = [&](int v) { return qlo + (int64_t)__builtin_amdgcn_readfirstlane(v); };
+    auto queue_exit = [&]() {
+        if (dyn && tid == 0 && atomicAdd(&queue[8], 1) == (int)gridDim.x - 1)
+            for (int i = 0; i < 9; i++) atomicExch(&queue[i], 0);
+    };
+    int64_t qend = bend;
+    if (dyn) b = grab_take(grab_issue()), qend = qhi;
     auto tail = [&]() {
         for (int64_t k = ra.tail0 + (int64_t)blockIdx.x * TPB + tid; k < ra.tail1; k += (int64_t)gridDim.x * TPB) {
             const uint32_t ka = ra.ptr[k], kz = ra.ptr[k + 1];
@@ -1320,13 +1341,15 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
             w[k] = ra.xs[k] - acc;
         }
     };
-    if (b >= bend) {
+    if (b >= qend) {
+        queue_exit();
         if (RES) tail();
         return;
     }
     BlkMeta cur = meta[b];
     issue(cur);
     while (true) {
+        const int gv = dyn ? grab_issue() : 0;  // the next block's grab, in flight during staging
         const int nr = cur.r1 - cur.r0, nl = cur.l1 - cur.l0;
         const uint32_t e0 = BWD ? (uint32_t)cur.be0 : (uint32_t)cur.fe0;
         const int ne = BWD ? cur.be1 - cur.be0 : cur.fe1 - cur.fe0;
@@ -1449,9 +1472,9 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
             }
         }
         __syncthreads();
-        const int64_t bn = b + G;
+        const int64_t bn = dyn ? grab_take(gv) : b + G;
         BlkMeta nxt;
-        if (bn < bend) {
+        if (bn < qend) {
             nxt = meta[bn];
             issue(nxt);  // in flight during the level phase
         }
@@ -1470,11 +1493,12 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
                 }
             }
         }
-        if (bn >= bend) break;
+        if (bn >= qend) break;
         __syncthreads();
         b = bn;
         cur = nxt;
     }
+    queue_exit();
     if (RES) tail();
 }
 
@@ -1503,31 +1527,33 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>((nb + SPLIT - 1) / SPLIT, (int64_t)occ * cus));
     const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
     const dim3 blk(TPB * SPLIT);
+    static const bool use_queue = getenv("CPK_PIPE_QUEUE") != nullptr;  // opt-in (measurement)
+    int *q = (use_queue && SPLIT == 1 && F.queue.n >= 9) ? F.queue.p : nullptr;
     if (ra)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true, kRes>), dim3((unsigned)grid),
                            blk, lds, c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p,
                            F.D.p, F.perm.p, xin, neg_from, w, out, run, active, 1, ys, 1, xs,
-                           (const int16_t *)F.fcol16.p, *ra);
+                           (const int16_t *)F.fcol16.p, *ra, q);
     else if (loc)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true>), dim3((unsigned)grid), blk,
                            lds, c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, 1, xs,
-                           (const int16_t *)F.fcol16.p, ResArgs{});
+                           (const int16_t *)F.fcol16.p, ResArgs{}, q);
     else if (!bwd)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
-                           (const int16_t *)nullptr, ResArgs{});
+                           (const int16_t *)nullptr, ResArgs{}, q);
     else if (add)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
-                           (const int16_t *)nullptr, ResArgs{});
+                           (const int16_t *)nullptr, ResArgs{}, q);
     else
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
-                           (const int16_t *)nullptr, ResArgs{});
+                           (const int16_t *)nullptr, ResArgs{}, q);
     return true;
 }
 
