@@ -1315,8 +1315,10 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     // launch does not end with the slowest fixed share.  Every grab increments, so every wave
     // exits; the last workgroup out (queue[8]) resets the counters for the next launch.
     const bool dyn = SPLIT == 1 && TPB == kWave && queue != nullptr;  // one wave: lane 0 broadcasts
-    const int xcd = (int)(blockIdx.x % 8u);
-    const int64_t qlo = blk0 + nblk * xcd / 8, qhi = blk0 + nblk * (xcd + 1) / 8;
+    // groups = min(8, grid): a grid smaller than 8 would leave some eighths without a workgroup
+    const int ngrp = (int)min(8u, gridDim.x);
+    const int xcd = (int)(blockIdx.x % (unsigned)ngrp);
+    const int64_t qlo = blk0 + nblk * xcd / ngrp, qhi = blk0 + nblk * (xcd + 1) / ngrp;
     auto grab_issue = [&]() {
         int v = 0;
         if (tid == 0) v = atomicAdd(&queue[xcd], 1);
