@@ -34,7 +34,7 @@ def _dptr(a):
 class Context:
     """One GPU, one HIP stream (and an RCCL communicator when nranks > 1)."""
 
-    def __init__(self, device=None, rank=0, nranks=1, unique_id=None, simgroup=None):
+    def __init__(self, device=None, rank=0, nranks=1, unique_id=None, simgroup=None, options=None):
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         h = C.c_void_p()
@@ -48,6 +48,19 @@ class Context:
             check(lib.cpk_ctx_create(device, rank, nranks, uid, C.byref(h)))
         self.h = h
         self.device, self.rank, self.nranks = device, rank, nranks
+        for k, v in (options or {}).items():
+            self.set_option(k, v)
+
+    def set_option(self, name, value):
+        """Engine option of this context (cpk_ctx_set_option); applies to objects created later."""
+        if isinstance(value, bool):
+            value = "1" if value else "0"
+        check(lib.cpk_ctx_set_option(self.h, name.encode(), str(value).encode()))
+
+    def get_option(self, name):
+        buf = C.create_string_buffer(256)
+        check(lib.cpk_ctx_get_option(self.h, name.encode(), buf, 256))
+        return buf.value.decode()
 
     def synchronize(self):
         check(lib.cpk_ctx_synchronize(self.h))
@@ -86,6 +99,26 @@ def default_context():
     if _default_ctx is None:
         _default_ctx = Context()
     return _default_ctx
+
+
+class engine_options:
+    """Context manager: engine options of a context (default: the default context) for the
+    duration of a block, restored afterwards -- e.g. `with engine_options(sweep="256,768,64"):`."""
+
+    def __init__(self, ctx=None, **kw):
+        self.ctx, self.kw, self.old = ctx, kw, {}
+
+    def __enter__(self):
+        self.ctx = self.ctx or default_context()
+        for k, v in self.kw.items():
+            self.old[k] = self.ctx.get_option(k)
+            self.ctx.set_option(k, v)
+        return self.ctx
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            self.ctx.set_option(k, v)
+        return False
 
 
 def get_unique_id():
@@ -260,6 +293,13 @@ class opLDL2:
         v = (C.c_int64 * 7)()
         check(lib.cpk_pc_sep_info(self.h, v))
         return dict(zip(("dist", "nT", "nlev", "nrec", "lds", "lds_g", "kt"), list(v)))
+
+    def sweep_info(self):
+        """Diagnostic: the sweep schedule as launched (cpk_pc_sweep_info)."""
+        v = (C.c_int64 * 8)()
+        check(lib.cpk_pc_sweep_info(self.h, v))
+        return dict(zip(("rounds", "round0_blocks", "upper_blocks", "round0_assigned", "resid_assigned",
+                         "bwd_assigned", "persistent", "reserved"), list(v)))
 
     def local_dofs(self):
         """Global indices of this rank's local vector entries ([x-part; y-part]) and n_loc."""

@@ -183,6 +183,7 @@ static std::unique_ptr<cpk_ctx_s> ctx_base(int device, int rank, int nranks) {
     if (device >= 0) CPK_HIP(hipSetDevice(device));
     CPK_HIP(hipGetDevice(&c.device));
     c.rank = rank, c.nranks = nranks;
+    c.opts = engine_opts_from_env();
     CPK_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     CPK_HIP(hipEventCreate(&c.ev0));
     CPK_HIP(hipEventCreate(&c.ev1));
@@ -250,6 +251,22 @@ int cpk_ctx_destroy(cpk_ctx ctx) {
     API_END
 }
 
+int cpk_ctx_set_option(cpk_ctx ctx, const char *name, const char *value) {
+    API_BEGIN
+    need(ctx && name && value, "NULL argument");
+    set_engine_option(ctx->c.opts, name, value);
+    API_END
+}
+
+int cpk_ctx_get_option(cpk_ctx ctx, const char *name, char *buf, size_t cap) {
+    API_BEGIN
+    need(ctx && name && buf && cap > 0, "NULL argument");
+    const std::string v = get_engine_option(ctx->c.opts, name);
+    need(v.size() < cap, "buffer too small");
+    std::memcpy(buf, v.c_str(), v.size() + 1);
+    API_END
+}
+
 int cpk_ctx_synchronize(cpk_ctx ctx) {
     API_BEGIN
     need(ctx, "ctx is NULL");
@@ -306,7 +323,7 @@ int cpk_pc_create(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptim
     need(ctx && A11 && B && C22 && out, "opLDL2: Invalid number of arguments.");
     auto pc = std::make_unique<cpk_pc_s>();
     pc->ctx = ctx;
-    if (ctx->c.dist()) pc->p.reset(precond_create_dist(ctx->c, analyze(A11->h, B->h, C22->h)));
+    if (ctx->c.dist()) pc->p.reset(precond_create_dist(ctx->c, analyze(A11->h, B->h, C22->h, ctx->c.opts)));
     else pc->p.reset(precond_create(ctx->c, A11->h, B->h, C22->h));
     if (ptime) *ptime = pc->p->ptime;
     *out = pc.release();
@@ -319,7 +336,8 @@ int cpk_pc_create_hint(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, cpk_mat
     need(ctx && A11 && B && C22 && out, "opLDL2: Invalid number of arguments.");
     auto pc = std::make_unique<cpk_pc_s>();
     pc->ctx = ctx;
-    if (ctx->c.dist()) pc->p.reset(precond_create_dist(ctx->c, analyze(A11->h, B->h, C22->h), Akry ? &Akry->h : nullptr));
+    if (ctx->c.dist())
+        pc->p.reset(precond_create_dist(ctx->c, analyze(A11->h, B->h, C22->h, ctx->c.opts), Akry ? &Akry->h : nullptr));
     else pc->p.reset(precond_create(ctx->c, A11->h, B->h, C22->h));
     if (ptime) *ptime = pc->p->ptime;
     *out = pc.release();
@@ -332,6 +350,8 @@ int cpk_pc_refactor(cpk_pc M, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptime
     Precond &p = *M->p;
     if (A11->h.nrows != p.gn || C22->h.nrows != p.gm || B->h.nrows != p.gm || B->h.ncols != p.gn)
         throw Error(CPK_ERR_DIM, "Incompatible dimensions.");
+    if (p.dist || !p.dl.ready)
+        throw Error(CPK_ERR_UNSUPPORTED, "refactorization needs a single-GPU preconditioner with the device factorization");
     if (pattern_hash(A11->h, B->h, C22->h) != p.pattern_hash)
         throw Error(CPK_ERR_ARGS, "refactor: the sparsity of A11, B or C22 differs from the factored one");
     const double s = precond_refactor(p, A11->dev(), B->dev(), C22->dev());
@@ -559,12 +579,30 @@ int cpk_debug_pipe_stamps(uint64_t *out, int npairs, int *copied) {
     API_END
 }
 
+int cpk_debug_blk_cycles(uint64_t *out, int64_t n, int64_t *copied) {
+    API_BEGIN
+    need(out && copied, "NULL argument");
+    *copied = debug_blk_cycles(out, n);
+    API_END
+}
+
 int cpk_pc_sep_info(cpk_pc M, int64_t *info) {
     API_BEGIN
     need(M && info, "NULL argument");
     const Precond &p = *M->p;
     const DSep &T = p.sep;
     const int64_t v[7] = {p.dist ? 1 : 0, T.nT, T.nlev, T.nrec, (int64_t)T.lds, (int64_t)T.lds_g, T.kt};
+    std::memcpy(info, v, sizeof v);
+    API_END
+}
+
+int cpk_pc_sweep_info(cpk_pc M, int64_t *info) {
+    API_BEGIN
+    need(M && info, "NULL argument");
+    const DFactor &F = M->p->dF;
+    const int64_t nr = (int64_t)F.round_ptr.size() - 1;
+    const int64_t r0 = nr >= 1 ? F.round_ptr[1] - F.round_ptr[0] : 0;
+    const int64_t v[8] = {nr, r0, F.nblk - r0, F.agrid[0], F.agrid[1], F.agrid[2], F.pipelined ? 1 : 0, 0};
     std::memcpy(info, v, sizeof v);
     API_END
 }
@@ -598,7 +636,7 @@ int cpk_reg_solve(cpk_ctx ctx, int method, const double *b, cpk_mat A, cpk_mat B
     check_dist_method(c, method);
     auto pc = std::make_unique<cpk_pc_s>();
     pc->ctx = ctx;
-    if (c.dist()) pc->p.reset(precond_create_dist(c, analyze(G->h, B->h, negC), &A->h));
+    if (c.dist()) pc->p.reset(precond_create_dist(c, analyze(G->h, B->h, negC, c.opts), &A->h));
     else pc->p.reset(precond_create(c, G->h, B->h, negC));
     Precond &p = *pc->p;
     apply_props(p, opts);  // reg_cpkrylov.m:135-148
@@ -622,7 +660,7 @@ int cpk_analyze(cpk_mat A11, cpk_mat B, cpk_mat C22, cpk_analysis *out) {
     API_BEGIN
     need(A11 && B && C22 && out, "NULL argument");
     auto a = std::make_unique<cpk_analysis_s>();
-    a->an = analyze(A11->h, B->h, C22->h);
+    a->an = analyze(A11->h, B->h, C22->h, engine_opts_from_env());
     *out = a.release();
     API_END
 }
@@ -682,7 +720,7 @@ int cpk_analysis_plan(cpk_analysis a, cpk_mat A, cpk_mat C, int nranks, int rank
          "A and C must match the analysis' n and m");
     auto p = std::make_unique<cpk_plan_s>();
     p->n = an.n, p->m = an.m;
-    p->ts = split_tree(an.F0, nranks, split_tol_option(), -1, &A->h);
+    p->ts = split_tree(an.F0, nranks, engine_opts_from_env().split_tol, -1, &A->h);
     p->dm = make_dofmap(an.F0, p->ts, an.n);
     p->rp = make_rank_plan(an.F0, p->ts, p->dm, rank);
     p->kp = dist_csr(an.Kp, p->dm, rank, false);

@@ -65,10 +65,52 @@ struct Comm {
     virtual void allreduce_sum(double *buf, size_t n, hipStream_t s) = 0;
     virtual void allgather(const double *send, double *recv, size_t n, hipStream_t s) = 0;
     virtual bool capturable() const = 0;  // may be captured into a hipGraph
+    virtual bool has_peers() const { return true; }  // false: the timing stand-in (no exchange)
 };
+
+// Sweep configuration: rows and entries staged per block, threads per block, round 0 / upper
+// rounds (engine option "sweep": "rows,cap,threads" for both, or "R0,CAP0,T0,R1,CAP1,T1[,SUB0]").
+struct SweepConfig {
+    int rows[2] = {192, 1024}, cap[2] = {576, 4096}, threads[2] = {64, 512};
+    int sub0 = 0;  // round-0 subtree cap (0: cap[0])
+};
+
+// Engine options of a context (opts.cpp; cpk_ctx_set_option).  None changes a result: they
+// select equivalent execution paths (each is tested bit-exact against the default) or the
+// sweep schedule and the distributed split, which every rank must build identically -- so a
+// distributed preconditioner compares a hash of all of them across ranks before its first
+// collective.  A context starts from the CPK_<NAME> environment variables, read once when it
+// is created; objects built later see its current values.
+struct EngineOpts {
+    SweepConfig sweep;            // sweep:              LDS staging of the sweep schedule
+    bool detach = false;          // detach:             entry-less rows outside the blocks
+    double split_tol = 0.03;      // split_tol:          distributed subtree weight tolerance
+    bool host_factor = false;     // host_factor:        numeric LDL' on the host (reference path)
+    bool no_pipe = false;         // no_pipe:            round 0 one workgroup per block
+    bool no_upper = false;        // no_upper:           upper rounds through the generic kernels
+    bool no_col16 = false;        // no_col16:           round-0 forward columns as int32
+    bool no_sched_resid = false;  // no_sched_resid:     refinement residual in original order
+    bool no_fused_resid = false;  // no_fused_resid:     refinement residual as its own SpMV
+    bool fused_tail_launch = false;  // fused_tail_launch: rows above round 0 by a residual launch
+    bool r0_stride = false;       // r0_stride:          round-0 blocks by stride, not by cost
+    bool tsolve_global = false;   // tsolve_global:      separator records read from HBM
+    bool tsolve_onepass = false;  // tsolve_onepass:     one-pass separator solve
+    bool no_piggy = false;        // no_piggy:           cpminres alpha by its own allreduce
+    bool no_halo_merge = false;   // no_halo_merge:      cpminres beta by its own allreduce
+    bool no_graph = false;        // no_graph:           no hipGraph capture of iterations
+    bool dist_graph = true;       // dist_graph:         capture collectives in the graphs
+    int batch = 0;                // batch:              fixed iterations per graph (0: adaptive)
+    bool profile_fwd_nolevels = false;  // profile_fwd_nolevels: diagnostic (cpk_profile_kernels)
+};
+EngineOpts engine_opts_from_env();
+// name as in the comments above; throws CPK_ERR_ARGS on an unknown name or a bad value
+void set_engine_option(EngineOpts &o, const std::string &name, const std::string &value);
+std::string get_engine_option(const EngineOpts &o, const std::string &name);
+uint64_t engine_opts_hash(const EngineOpts &o);  // FNV-1a over every option
 
 // Execution context: one GPU, one stream, reduction workspace (and a Comm when nranks > 1).
 struct Ctx {
+    EngineOpts opts;
     int device = 0, rank = 0, nranks = 1;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -121,9 +163,19 @@ struct DFactor {
     DBuf<int32_t> blk_lvl;  // [nblk + 1]
     DBuf<int32_t> lvl_row;  // [nlvl + 1]
     DBuf<int32_t> meta;     // [nblk][8]: r0, r1, l0, l1, fwd e0, e1, bwd e0, e1
-    bool pipelined = true;  // round 0 through the persistent pipelined kernel
-    int64_t round0_rows = -1;
-    DBuf<int32_t> queue;  // round-0 block queue: 8 per-XCD counters + exit counter (opt-in)  // round 0 is the rows [0, round0_rows) (-1: not a leading row range)
+    bool pipelined = true;  // round 0 through the persistent pipelined kernel (set before make_dfactor)
+    bool no_upper = false;  // upper rounds through the generic kernels (set before make_dfactor)
+    bool no_col16 = false;  // no int16 round-0 forward columns (set before make_dfactor)
+    // engine options of the preconditioner's context when it was built (launch-time paths)
+    bool no_fused_resid = false, fused_tail_launch = false;
+    int64_t round0_rows = -1;  // round 0 is the rows [0, round0_rows) (-1: not a leading row range)
+    std::vector<int32_t> hmeta;  // host copy of meta
+    // round-0 blocks assigned to the persistent launch's workgroups by modelled cost (plan_round0),
+    // per kernel variant v (0 forward, 1 forward with the fused refinement residual, 2 backward):
+    // workgroup g runs the BlkMeta records ameta[v][aptr[v][g] .. aptr[v][g + 1]); agrid[v] = the
+    // grid they were made for (0: none; the launch then strides over meta)
+    DBuf<int32_t> aptr[3], ameta[3];
+    int agrid[3] = {0, 0, 0};
     std::vector<int64_t> round_ptr;  // host copy: blocks per round
     std::vector<char> round_fits;    // host: every block of round r fits (sweep_rows[1], sweep_cap[1])
     int sweep_rows[2] = {192, 1024}, sweep_cap[2] = {576, 4096}, sweep_threads[2] = {64, 512};  // round 0 / rest
@@ -144,14 +196,9 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
                   const std::vector<std::vector<BwdExtra>> *extra = nullptr, std::vector<int32_t> *fsrc = nullptr,
                   std::vector<int32_t> *bsrc = nullptr);
 size_t sweep_lds_bytes(int R, int CAP);
-// Sweep configuration: rows and entries staged per block, threads per block.
-// CPK_SWEEP="rows,cap,threads" overrides the default.
-// CPK_SWEEP="R0,CAP0,T0,R1,CAP1,T1": round 0 / upper rounds.
-struct SweepConfig {
-    int rows[2] = {192, 1024}, cap[2] = {576, 4096}, threads[2] = {64, 512};
-    int sub0 = 0;  // round-0 subtree cap (0: cap[0])
-};
-SweepConfig sweep_config();
+// the round-0 block assignment of every kernel variant for the grids the launches will use;
+// kps_ptr (optional): row pointers of Kp in schedule order (the fused-residual variant's cost)
+void plan_round0(Ctx &c, DFactor &d, const int64_t *kps_ptr);
 
 // ---- launchers (kernels.hip) -------------------------------------------------------------
 // Flags: a kernel is a no-op when *run == 0 or *active == 0 (either pointer may be null).
@@ -189,6 +236,7 @@ void launch_spmv_resid_sched(Ctx &c, const DMat &A, const int32_t *perm, const d
 bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const int32_t *tail_blk, int64_t tail_nblk,
                              const double *xs, const double *y, double *r, const int *run);
 int debug_pipe_stamps(uint64_t *out, int npairs);  // diagnostic build only (CPK_PIPE_STAMPS)
+int64_t debug_blk_cycles(uint64_t *out, int64_t n);  // likewise: [4][1 << 17] per-block cycles
 // Kps row blocks of the rows [row0, nrows) (A.blk with a boundary at row0)
 void make_tail_blk(const DMat &A, int64_t row0, DBuf<int32_t> &blk, int64_t &nblk);
 // out[i] = x[idx[i]]
@@ -219,6 +267,8 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
 struct DLdl {
     int64_t N = 0, nnz = 0, nf = 0, nb = 0;
     std::vector<int32_t> lev_ptr;  // host: rows by elimination-tree height
+    std::vector<int32_t> lev_long; // host: height l's long rows (one wave each) start at lev_long[l]
+    int64_t max_long = 0;          // longest pattern among them
     DBuf<int32_t> lev_rows, Rp, Rc, Rcsc, Lp, Li, kp_ptr, kp_tgt, fsrc, bsrc, dsrc;
     DBuf<uint32_t> kp_src;
     DBuf<int64_t> kp_from;  // Kp entry -> (block << 40 | entry) of A11 / B / C22 (refactorization)
@@ -231,6 +281,11 @@ void dldl_setup(DLdl &d, const LdlSymbolic &sym, const Factor &f, const std::vec
 // numeric factorization from the device Kp values, then DFactor's sweep values and D;
 // throws CPK_ERR_FACTOR on a zero or NaN pivot
 void dldl_factor(Ctx &c, DLdl &d, const double *kpv, DFactor &dF);
+// the numeric phase alone into caller-owned Lx (CSC order) / D (pivot order); throws on a bad
+// pivot having written only Lx, D and d's scratch (a refactorization commits after it returns)
+void dldl_numeric(Ctx &c, DLdl &d, const double *kpv, double *Lx, double *D);
+// DFactor's sweep values and D from d.Lx / d.D
+void dldl_fill(Ctx &c, const DLdl &d, DFactor &dF);
 // Kp values from the device values of A11, B, C22 through d.kp_from
 void dldl_assemble_kp(Ctx &c, const DLdl &d, const double *a, const double *b, const double *cc, double *kpv);
 
@@ -251,7 +306,7 @@ struct Analysis {
     LdlSymbolic sym;
     std::vector<int32_t> rsrc;  // F's entry t came from F0's entry rsrc[t]
 };
-Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, bool device_numeric = false);
+Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOpts &o, bool device_numeric = false);
 
 // The separator solve of a distributed preconditioner, device copy.
 constexpr int64_t kSepPiggy = 2;  // spare payload slots per rank in the separator exchange
@@ -274,6 +329,7 @@ struct DSep {
     int64_t nsf = 0, nsb = 0, nrec = 0;
     size_t lds = 0;    // LDS bytes of the stepped solve with its records staged, 0 = too large
     size_t lds_g = 0;  // LDS bytes with the records left in HBM; 0 (or no records): one-pass kernel
+    bool tsolve_global = false, tsolve_onepass = false;  // engine options at construction
 };
 struct RankPlan;
 // Split the forward rows of T and build the steps of the separator level solve.

@@ -14,16 +14,6 @@
 
 namespace cpk {
 
-double split_tol_option() {
-    const char *e = getenv("CPK_SPLIT_TOL");
-    if (!e) return kSplitTol;
-    char *end = nullptr;
-    const double v = strtod(e, &end);
-    if (end == e || *end != '\0' || !std::isfinite(v) || !(v > 0 && v < 1))
-        throw Error(CPK_ERR_ARGS, std::string("CPK_SPLIT_TOL must be a number in (0, 1), got '") + e + "'");
-    return v;
-}
-
 TreeSplit split_tree(const Factor &f, int P, double tol, int64_t tmax, const HCsr *Akry) {
     const int64_t N = f.N;
     TreeSplit ts;

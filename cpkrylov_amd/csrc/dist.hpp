@@ -30,9 +30,6 @@ constexpr double kSplitTol = 0.03;
 // entries) then follow the rank of a dof A couples them with, which keeps the Krylov SpMV's
 // halo small (S50's slack rows couple only through A).
 TreeSplit split_tree(const Factor &f, int P, double tol = kSplitTol, int64_t tmax = -1, const HCsr *Akry = nullptr);
-// the diagnostic override CPK_SPLIT_TOL, validated: a finite number in
-// (0, 1), else CPK_ERR_ARGS; kSplitTol when unset.  Read by the callers of split_tree.
-double split_tol_option();
 
 // Dof ownership.  Rank r's local vectors are [owned x-part dofs ascending; owned y-part dofs
 // ascending], so the solvers' [x; y] index ranges keep their meaning locally.

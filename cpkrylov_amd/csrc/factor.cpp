@@ -133,7 +133,7 @@ Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int /*nthrea
 }
 
 Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1, int64_t SUB0,
-                        const std::vector<int64_t> *extra_bwd) {
+                        const std::vector<int64_t> *extra_bwd, bool detach) {
     if (SUB0 <= 0 || SUB0 > CAP0) SUB0 = CAP0;
     const int64_t N = f.N;
     Schedule s;
@@ -176,7 +176,7 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     // (1) Layer peeling: round r takes the maximal subtrees of at most R rows of the tree that
     //     remains after rounds 0..r-1.  On bushy (nested-dissection) trees the remainder
     //     shrinks geometrically and a few rounds suffice.
-    // Detached rows (opt-in, CPK_DETACH=1): rows of L without entries (the G pivots of a
+    // Detached rows (opt-in, engine option detach): rows of L without entries (the G pivots of a
     // G-first ordering, leaves of the elimination tree).  Their forward value is their input and
     // nothing reads them before the backward sweep's last step, so they can stay out of the
     // blocks: they come first in the new order and are solved by one streaming pass per sweep
@@ -184,7 +184,7 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     // (the entry cap binds, not the rows) and the streaming passes cost more than the G rows
     // did inside the blocks, so the default keeps them in.
     std::vector<char> detached(N, 0);
-    if (getenv("CPK_DETACH"))
+    if (detach)
         for (int64_t v = 0; v < N; v++) detached[v] = ent_fwd[v] == 0;
     std::vector<int32_t> alive;
     alive.reserve(N);

@@ -120,8 +120,9 @@ struct Schedule {
 // a block's level count is that of its tallest subtree, so packing several short subtrees
 // per block cuts the barrier-separated level passes per row.
 // extra_bwd[v]: backward entries of row v outside the factor (distributed separators)
+// detach: rows without forward entries stay out of the blocks (engine option detach)
 Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1, int64_t SUB0 = 0,
-                        const std::vector<int64_t> *extra_bwd = nullptr);
+                        const std::vector<int64_t> *extra_bwd = nullptr, bool detach = false);
 // Apply the schedule's relabel to the factor (values unchanged, exact data movement).
 // src (optional): src[t] = index into f.Li / f.Lx of the relabelled factor's entry t.
 Factor relabel(const Factor &f, const Schedule &s, std::vector<int32_t> *src = nullptr);

@@ -170,7 +170,7 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
         m[4] = (int32_t)fptr[r0], m[5] = (int32_t)fptr[r1], m[6] = (int32_t)bptr[r0], m[7] = (int32_t)bptr[r1];
     }
     d.meta.upload(meta);
-    d.queue.upload(std::vector<int32_t>(16, 0));  // round-0 block queue counters (CPK_PIPE_QUEUE)
+    d.hmeta = meta;
     d.round0_rows = -1;
     if (s.ndet == 0 && s.round_ptr.size() >= 2) {  // round 0 a leading, contiguous row range?
         int64_t r = 0;
@@ -178,13 +178,12 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
             r = meta[(size_t)b * 8] == r ? meta[(size_t)b * 8 + 1] : -1;
         d.round0_rows = r;
     }
-    d.pipelined = getenv("CPK_NO_PIPE") == nullptr;
     // round 0's forward entries as 16-bit block-local columns: a round-0 block holds whole
     // subtrees, so a row's forward columns (its descendants) are in its own block unless rows
     // were detached; checked here, and the image is only built when it holds for every block
     d.fcol16.release();
     d.nnz16 = 0;
-    if (s.ndet == 0 && s.round_ptr.size() >= 2 && !getenv("CPK_NO_COL16")) {
+    if (s.ndet == 0 && s.round_ptr.size() >= 2 && !d.no_col16) {
         bool ok = true;
         int64_t e_end = 0;
         for (int64_t b = s.round_ptr[0]; b < s.round_ptr[1] && ok; b++) {
@@ -786,9 +785,9 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
                                    (int)kTsolveMaxLds) == hipSuccess;
     }();
     auto fits = [&](size_t b) { return b && (b <= 64 * 1024 || lds_attr); };
-    const bool grec = getenv("CPK_TSOLVE_GLOBAL") != nullptr || !fits(S.lds);  // diagnostic override
+    const bool grec = S.tsolve_global || !fits(S.lds);  // engine option: records in HBM
     const size_t lds = grec ? S.lds_g : S.lds;
-    if (S.nrec > 0 && fits(lds) && !getenv("CPK_TSOLVE_ONEPASS")) {
+    if (S.nrec > 0 && fits(lds) && !S.tsolve_onepass) {
         hipLaunchKernelGGL(tprefix_kernel, dim3((unsigned)((S.nT + 3) / 4)), dim3(256), 0, c.stream, (int)S.nT,
                            S.tk_ptr.p, S.tk_col.p, S.tk_val.p, S.tr_ptr.p, S.tr_col.p, S.tr_val.p, S.tr_slot.p,
                            S.tf_src.p, S.rbuf.p, S.pre.p, S.rec_v.p, run, active);
@@ -1221,7 +1220,7 @@ static bool upper_round_t(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool ad
 static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add, const double *xin,
                         int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in,
                         double *ys, double *xs) {
-    if (getenv("CPK_NO_UPPER")) return false;
+    if (F.no_upper) return false;
     return upper_round_t<512, 2, 8>(c, F, r, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs);
 }
 
@@ -1233,6 +1232,10 @@ static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add,
 // diagnostic build only (make HIPEXTRA=-DCPK_PIPE_STAMPS): per-workgroup start / end of the last
 // round-0 launch (s_memrealtime, 100 MHz), read by cpk_debug_pipe_stamps (tools/pipe_stamps.py)
 __device__ uint64_t g_pipe_stamps[2 * 16384];
+// per-block cycles (s_memtime) of the last launch of each unsplit variant: [fwd, fwd + fused
+// residual, bwd, bwd accumulating][block] (tools/blk_cycles.py: the round-0 cost model)
+constexpr int kBlkCycMax = 1 << 17;
+__device__ uint64_t g_blk_cyc[4 * kBlkCycMax];
 #endif
 template <int TPB, int RPT, int EPT, bool BWD, bool ADD, int SPLIT = 1, bool LOC = false, bool RES = false>
 #ifndef CPK_PIPE_WAVES
@@ -1243,7 +1246,8 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,
     int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
-    int skip0, double *xs, const int16_t *__restrict__ col16, ResArgs ra, int *queue) {
+    int skip0, double *xs, const int16_t *__restrict__ col16, ResArgs ra, const BlkMeta *__restrict__ ameta,
+    const int32_t *__restrict__ aptr) {
     static_assert(SPLIT == 1 || TPB * SPLIT == 64, "split blocks must share one wave");
     static_assert(!LOC || !BWD, "block-local columns: forward round 0 only");
     static_assert(!RES || (LOC && SPLIT == 1), "fused residual: forward round 0 with block-local columns");
@@ -1308,30 +1312,13 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
         }
     } stamp{t_start};
 #endif
-    int64_t b = blk0 + (int64_t)blockIdx.x * SPLIT + sub;
-    const int64_t bend = blk0 + nblk;
-    // queue (opt-in, CPK_PIPE_QUEUE, unsplit blocks): instead of a fixed stride, the workgroups of
-    // XCD x (blockIdx % 8) grab the blocks of the x-th eighth one at a time (queue[x]), so the
-    // launch does not end with the slowest fixed share.  Every grab increments, so every wave
-    // exits; the last workgroup out (queue[8]) resets the counters for the next launch.
-    const bool dyn = SPLIT == 1 && TPB == kWave && queue != nullptr;  // one wave: lane 0 broadcasts
-    // groups = min(8, grid): a grid smaller than 8 would leave some eighths without a workgroup
-    const int ngrp = (int)min(8u, gridDim.x);
-    const int xcd = (int)(blockIdx.x % (unsigned)ngrp);
-    const int64_t qlo = blk0 + nblk * xcd / ngrp, qhi = blk0 + nblk * (xcd + 1) / ngrp;
-    auto grab_issue = [&]() {
-        int v = 0;
-        if (tid == 0) v = atomicAdd(&queue[xcd], 1);
-        return v;
-    };
-    // lane 0 holds the grab; readfirstlane keeps the block index uniform (scalar metadata loads)
-    auto grab_take = [&](int v) { return qlo + (int64_t)__builtin_amdgcn_readfirstlane(v); };
-    auto queue_exit = [&]() {
-        if (dyn && tid == 0 && atomicAdd(&queue[8], 1) == (int)gridDim.x - 1)
-            for (int i = 0; i < 9; i++) atomicExch(&queue[i], 0);
-    };
-    int64_t qend = bend;
-    if (dyn) b = grab_take(grab_issue()), qend = qhi;
+    // the blocks of this workgroup: the host's assignment (aptr: ameta[aptr[g] .. aptr[g + 1]),
+    // balanced by cost, DFactor::plan_round0) or, without one, every G-th block from blk0 + g
+    const bool asg = aptr != nullptr;
+    int64_t b = asg ? (int64_t)aptr[blockIdx.x] : blk0 + (int64_t)blockIdx.x * SPLIT + sub;
+    const int64_t bend = asg ? (int64_t)aptr[blockIdx.x + 1] : blk0 + nblk;
+    const int64_t bstep = asg ? 1 : G;
+    const BlkMeta *const msrc = asg ? ameta : meta;
     auto tail = [&]() {
         for (int64_t k = ra.tail0 + (int64_t)blockIdx.x * TPB + tid; k < ra.tail1; k += (int64_t)gridDim.x * TPB) {
             const uint32_t ka = ra.ptr[k], kz = ra.ptr[k + 1];
@@ -1343,15 +1330,16 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
             w[k] = ra.xs[k] - acc;
         }
     };
-    if (b >= qend) {
-        queue_exit();
+    if (b >= bend) {
         if (RES) tail();
         return;
     }
-    BlkMeta cur = meta[b];
+    BlkMeta cur = msrc[b];
     issue(cur);
     while (true) {
-        const int gv = dyn ? grab_issue() : 0;  // the next block's grab, in flight during staging
+#ifdef CPK_PIPE_STAMPS
+        const uint64_t tb = (uint64_t)clock64();
+#endif
         const int nr = cur.r1 - cur.r0, nl = cur.l1 - cur.l0;
         const uint32_t e0 = BWD ? (uint32_t)cur.be0 : (uint32_t)cur.fe0;
         const int ne = BWD ? cur.be1 - cur.be0 : cur.fe1 - cur.fe0;
@@ -1474,10 +1462,10 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
             }
         }
         __syncthreads();
-        const int64_t bn = dyn ? grab_take(gv) : b + G;
+        const int64_t bn = b + bstep;
         BlkMeta nxt;
-        if (bn < qend) {
-            nxt = meta[bn];
+        if (bn < bend) {
+            nxt = msrc[bn];
             issue(nxt);  // in flight during the level phase
         }
         // skip0: level 0 holds only rows without entries (no detached rows: the G pivots are in
@@ -1495,12 +1483,15 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
                 }
             }
         }
-        if (bn >= qend) break;
+#ifdef CPK_PIPE_STAMPS
+        if (SPLIT == 1 && tid == 0 && !asg && b < kBlkCycMax)
+            g_blk_cyc[(BWD ? (ADD ? 3 : 2) : (RES ? 1 : 0)) * kBlkCycMax + b] = (uint64_t)clock64() - tb;
+#endif
+        if (bn >= bend) break;
         __syncthreads();
         b = bn;
         cur = nxt;
     }
-    queue_exit();
     if (RES) tail();
 }
 
@@ -1509,7 +1500,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
 template <int TPB, int RPT, int EPT, int SPLIT = 1>
 static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
                        double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
-                       double *xs, const ResArgs *ra = nullptr) {
+                       double *xs, const ResArgs *ra = nullptr, int64_t *plan_grid = nullptr) {
     if (F.sweep_threads[0] != TPB || F.sweep_rows[0] != RPT * TPB || F.sweep_cap[0] != EPT * TPB) return false;
     if (ra && (bwd || F.fcol16.n == 0 || SPLIT != 1)) return false;  // fused residual: one instantiation
     const int64_t nb = F.round_ptr[1] - F.round_ptr[0];
@@ -1527,53 +1518,135 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>((nb + SPLIT - 1) / SPLIT, (int64_t)occ * cus));
+    if (plan_grid) {  // plan_round0: the grid this launch would use (no assignment for split blocks)
+        *plan_grid = SPLIT == 1 ? grid : 0;
+        return true;
+    }
     const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
     const dim3 blk(TPB * SPLIT);
-    static const bool use_queue = getenv("CPK_PIPE_QUEUE") != nullptr;  // opt-in (measurement)
-    int *q = (use_queue && SPLIT == 1 && F.queue.n >= 9) ? F.queue.p : nullptr;
+    // the host's balanced assignment of this variant, when it was made for this grid
+    const int v = ra ? 1 : (bwd ? 2 : 0);
+    const bool use_asg = SPLIT == 1 && F.agrid[v] == grid && F.aptr[v].n == (size_t)grid + 1;
+    const BlkMeta *am = use_asg ? reinterpret_cast<const BlkMeta *>(F.ameta[v].p) : nullptr;
+    const int32_t *ap = use_asg ? F.aptr[v].p : nullptr;
     if (ra)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true, kRes>), dim3((unsigned)grid),
                            blk, lds, c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p,
                            F.D.p, F.perm.p, xin, neg_from, w, out, run, active, 1, ys, 1, xs,
-                           (const int16_t *)F.fcol16.p, *ra, q);
+                           (const int16_t *)F.fcol16.p, *ra, am, ap);
     else if (loc)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true>), dim3((unsigned)grid), blk,
                            lds, c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, 1, xs,
-                           (const int16_t *)F.fcol16.p, ResArgs{}, q);
+                           (const int16_t *)F.fcol16.p, ResArgs{}, am, ap);
     else if (!bwd)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
-                           (const int16_t *)nullptr, ResArgs{}, q);
+                           (const int16_t *)nullptr, ResArgs{}, am, ap);
     else if (add)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
-                           (const int16_t *)nullptr, ResArgs{}, q);
+                           (const int16_t *)nullptr, ResArgs{}, am, ap);
     else
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
-                           (const int16_t *)nullptr, ResArgs{}, q);
+                           (const int16_t *)nullptr, ResArgs{}, am, ap);
     return true;
 }
 
 // round 0 through the pipelined kernel when its configuration is one of the instantiated ones
+// (plan_grid: nothing is launched, the grid of the matching instantiation is returned)
 static bool pipe_round0(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
                         double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
-                        double *xs) {
+                        double *xs, int64_t *plan_grid = nullptr) {
     if (!F.pipelined || F.round_ptr.size() < 2) return false;
-    return pipe_round<32, 6, 18, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
-           pipe_round<32, 4, 12, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
-           pipe_round<32, 8, 24, 2>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
-           pipe_round<128, 2, 6>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
-           pipe_round<64, 3, 9>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
-           pipe_round<64, 4, 12>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
-           pipe_round<64, 6, 18>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
-           pipe_round<64, 8, 24>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
-           pipe_round<128, 1, 4>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs) ||
-           pipe_round<256, 1, 3>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs);
+#define CPK_PR(...) pipe_round<__VA_ARGS__>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs, nullptr, plan_grid)
+    return CPK_PR(32, 6, 18, 2) || CPK_PR(32, 4, 12, 2) || CPK_PR(32, 8, 24, 2) || CPK_PR(128, 2, 6) ||
+           CPK_PR(64, 3, 9) || CPK_PR(64, 4, 12) || CPK_PR(64, 6, 18) || CPK_PR(64, 8, 24) || CPK_PR(128, 1, 4) ||
+           CPK_PR(256, 1, 3);
+#undef CPK_PR
+}
+
+// the fused-residual round-0 instantiations (launch_sptrsv_fwd_resid)
+static bool pipe_round0_resid(Ctx &c, const DFactor &F, double *r, const int *run, const ResArgs &ra,
+                              int64_t *plan_grid = nullptr) {
+#define CPK_PR(...) pipe_round<__VA_ARGS__>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra, plan_grid)
+    return CPK_PR(64, 3, 9) || CPK_PR(64, 4, 12) || CPK_PR(128, 2, 6) || CPK_PR(64, 6, 18);
+#undef CPK_PR
+}
+
+// ---- round-0 block assignment (longest processing time first) ---------------------------------
+// A persistent round-0 workgroup used to take every G-th block, so the launch ended with the
+// workgroup whose fixed share happened to cost most: 9-13 % of each launch was tail (DESIGN.md
+// 7a, per-workgroup stamps).  Block costs are static, so the host assigns the blocks to the
+// launch's G workgroups once: blocks by descending modelled cost, each to the least loaded
+// workgroup so far; a workgroup then walks its blocks in ascending order.  The arithmetic of
+// every block is unchanged (bit-identical), only which workgroup runs it and when.
+// Cost model: c0 + c1 levels + c2 rows + c3 entries (+ c4 Kps entries) per block and variant.
+static const double kR0Cost[3][5] = {
+    // The s_memtime stamps (tools/blk_cycles.py, profiles/r03_blk_cycles_v0.log) fit poorly per
+    // block (R^2 0.1-0.6: a block's time depends on what shares its CU), but the level count
+    // dominates every fit (~1500-1900 cycles per level) and, replayed on the measured cycles,
+    // LPT by levels alone gave the lowest maximum: 1.07-1.12 x the median workgroup against
+    // 1.12-1.18 for the stride.  Rows break ties.
+    {0.0, 1.0, 1e-3, 0.0, 0.0},  // forward
+    {0.0, 1.0, 1e-3, 0.0, 0.0},  // forward with the fused refinement residual
+    {0.0, 1.0, 1e-3, 0.0, 0.0},  // backward
+};
+
+void plan_round0(Ctx &c, DFactor &d, const int64_t *kps_ptr) {
+    for (int v = 0; v < 3; v++) d.agrid[v] = 0, d.aptr[v].release(), d.ameta[v].release();
+    if (!d.pipelined || d.round_ptr.size() < 2 || c.opts.r0_stride) return;
+    const int64_t b0 = d.round_ptr[0], nb = d.round_ptr[1] - b0;
+    if (nb <= 0 || d.hmeta.size() < (size_t)(b0 + nb) * 8) return;
+    int64_t grid[3] = {0, 0, 0};
+    pipe_round0(c, d, false, false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, &grid[0]);
+    pipe_round0(c, d, true, false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, &grid[2]);
+    if (kps_ptr && d.fcol16.n > 0 && d.ndet == 0) pipe_round0_resid(c, d, nullptr, nullptr, ResArgs{}, &grid[1]);
+    for (int v = 0; v < 3; v++) {
+        const int64_t G = grid[v];
+        if (G <= 1 || G >= nb) continue;
+        const double *k = kR0Cost[v];
+        std::vector<double> cost(nb);
+        for (int64_t i = 0; i < nb; i++) {
+            const int32_t *m = &d.hmeta[(size_t)(b0 + i) * 8];
+            const double ent = v == 2 ? m[7] - m[6] : m[5] - m[4];
+            const double ke = (v == 1) ? (double)(kps_ptr[m[1]] - kps_ptr[m[0]]) : 0.0;
+            cost[i] = k[0] + k[1] * (m[3] - m[2]) + k[2] * (m[1] - m[0]) + k[3] * ent + k[4] * ke;
+        }
+        std::vector<int64_t> ord(nb);
+        for (int64_t i = 0; i < nb; i++) ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return cost[a] > cost[b]; });
+        // min-heap of (load, workgroup)
+        std::vector<std::pair<double, int32_t>> heap((size_t)G);
+        for (int64_t g = 0; g < G; g++) heap[g] = {0.0, (int32_t)g};
+        auto gt = [](const std::pair<double, int32_t> &a, const std::pair<double, int32_t> &b) {
+            return a.first > b.first || (a.first == b.first && a.second > b.second);
+        };
+        std::make_heap(heap.begin(), heap.end(), gt);
+        std::vector<int32_t> owner(nb);
+        for (int64_t i : ord) {
+            std::pop_heap(heap.begin(), heap.end(), gt);
+            auto &h = heap.back();
+            owner[i] = h.second;
+            h.first += cost[i];
+            std::push_heap(heap.begin(), heap.end(), gt);
+        }
+        std::vector<int32_t> ptr((size_t)G + 1, 0), am((size_t)nb * 8);
+        for (int64_t i = 0; i < nb; i++) ptr[owner[i] + 1]++;
+        for (int64_t g = 0; g < G; g++) ptr[g + 1] += ptr[g];
+        std::vector<int32_t> nx(ptr.begin(), ptr.end() - 1);
+        for (int64_t i = 0; i < nb; i++) {  // ascending block order within a workgroup
+            const int32_t q = nx[owner[i]]++;
+            std::copy_n(&d.hmeta[(size_t)(b0 + i) * 8], 8, &am[(size_t)q * 8]);
+        }
+        d.aptr[v].upload(ptr);
+        d.ameta[v].upload(am);
+        d.agrid[v] = (int)G;
+    }
 }
 
 template <int TPB, int MODE>
@@ -1672,6 +1745,18 @@ void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_
 
 // diagnostic: the per-workgroup stamps of the last round-0 launch (0 unless built with
 // CPK_PIPE_STAMPS); returns the number of pairs copied
+int64_t debug_blk_cycles(uint64_t *out, int64_t n) {
+#ifdef CPK_PIPE_STAMPS
+    n = std::min<int64_t>(n, 4 * (int64_t)kBlkCycMax);
+    CPK_HIP(hipDeviceSynchronize());
+    CPK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blk_cyc), (size_t)n * sizeof(uint64_t)));
+    return n;
+#else
+    (void)out, (void)n;
+    return 0;
+#endif
+}
+
 int debug_pipe_stamps(uint64_t *out, int npairs) {
 #ifdef CPK_PIPE_STAMPS
     npairs = std::min(npairs, 16384);
@@ -1696,19 +1781,15 @@ void make_tail_blk(const DMat &A, int64_t row0, DBuf<int32_t> &blk, int64_t &nbl
 
 bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const int32_t *tail_blk, int64_t tail_nblk,
                              const double *xs, const double *y, double *r, const int *run) {
-    const bool off = getenv("CPK_NO_FUSED_RESID") != nullptr;  // A/B switch: separate residual SpMV
+    const bool off = F.no_fused_resid;  // A/B switch: separate residual SpMV
     if (off || tail_nblk < 0 || !F.pipelined || F.ndet != 0 || F.round0_rows < 0 || F.fcol16.n == 0 ||
         F.round_ptr.size() < 2 || Kps.halo())
         return false;
-    // the rows above round 0 inside the round-0 kernel (CPK_FUSED_TAIL_LAUNCH: a residual launch)
-    const bool tail_launch = getenv("CPK_FUSED_TAIL_LAUNCH") != nullptr;
+    // the rows above round 0 inside the round-0 kernel (fused_tail_launch: a residual launch)
+    const bool tail_launch = F.fused_tail_launch;
     const ResArgs ra{Kps.ptr.p, Kps.col.p, Kps.val.p, y, xs, F.round0_rows, tail_launch ? F.round0_rows : F.N};
     // round 0: r of its rows formed in the sweep (nothing is launched unless a configuration matches)
-    if (!(pipe_round<64, 3, 9>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra) ||
-          pipe_round<64, 4, 12>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra) ||
-          pipe_round<128, 2, 6>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra) ||
-          pipe_round<64, 6, 18>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra)))
-        return false;
+    if (!pipe_round0_resid(c, F, r, run, ra)) return false;
     // the rows above round 0: their r by the residual SpMV over those rows, then the upper rounds
     if (tail_launch && tail_nblk > 0) {
         const EpiResidSched e{xs, nullptr, 0, r, run};

@@ -34,25 +34,7 @@ struct PhaseClock {
     }
 };
 
-SweepConfig sweep_config() {
-    SweepConfig cfg;
-    if (const char *e = getenv("CPK_SWEEP")) {
-        int v[7] = {0, 0, 0, 0, 0, 0, 0};
-        const int got = sscanf(e, "%d,%d,%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5], &v[6]);
-        if (got == 3) v[3] = v[0], v[4] = v[1], v[5] = v[2];
-        auto ok = [](int r, int c, int t) {
-            return r > 0 && r <= 16384 && c > 0 && c <= 16384 && (t == 32 || t == 64 || t == 128 || t == 256 || t == 512 || t == 1024) &&
-                   sweep_lds_bytes(r, c) <= 160 * 1024;
-        };
-        if ((got == 3 || got == 6 || got == 7) && ok(v[0], v[1], v[2]) && ok(v[3], v[4], v[5])) {
-            for (int i = 0; i < 2; i++) cfg.rows[i] = v[3 * i], cfg.cap[i] = v[3 * i + 1], cfg.threads[i] = v[3 * i + 2];
-            cfg.sub0 = got == 7 ? v[6] : 0;
-        }
-    }
-    return cfg;
-}
-
-Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, bool device_numeric) {
+Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOpts &o, bool device_numeric) {
     auto t0 = std::chrono::steady_clock::now();
     PhaseClock pc("analyze");
     Analysis an;
@@ -64,8 +46,9 @@ Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, bool device_nu
     an.device_numeric = device_numeric;
     Factor f0 = ldl_factor(an.Kp, perm, 1, device_numeric ? &an.sym : nullptr, !device_numeric);
     pc.lap(device_numeric ? "factor (symbolic)" : "factor");
-    an.sweep = sweep_config();
-    an.S = build_schedule(f0, an.sweep.rows[0], an.sweep.cap[0], an.sweep.rows[1], an.sweep.cap[1], an.sweep.sub0);
+    an.sweep = o.sweep;
+    an.S = build_schedule(f0, an.sweep.rows[0], an.sweep.cap[0], an.sweep.rows[1], an.sweep.cap[1], an.sweep.sub0,
+                          nullptr, o.detach);
     pc.lap("schedule");
     an.F = relabel(f0, an.S, device_numeric ? &an.rsrc : nullptr);
     an.F0 = std::move(f0);
@@ -88,6 +71,8 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
     for (int i = 0; i < 2; i++)  // before make_dfactor: the device layout follows the configuration
         pc->dF.sweep_rows[i] = an.sweep.rows[i], pc->dF.sweep_cap[i] = an.sweep.cap[i],
         pc->dF.sweep_threads[i] = an.sweep.threads[i];
+    pc->dF.pipelined = !c.opts.no_pipe, pc->dF.no_upper = c.opts.no_upper, pc->dF.no_col16 = c.opts.no_col16;
+    pc->dF.no_fused_resid = c.opts.no_fused_resid, pc->dF.fused_tail_launch = c.opts.fused_tail_launch;
     {
         const std::vector<int64_t> key(pc->S.order.begin(), pc->S.order.end());
         if (an.device_numeric) {
@@ -106,7 +91,7 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
         CPK_HIP(hipStreamSynchronize(c.stream));
         clk.lap("numeric factorization (device)");
     }
-    pc->no_sched = getenv("CPK_NO_SCHED_RESID") != nullptr;
+    pc->no_sched = c.opts.no_sched_resid;
     if (pc->Kp.nnz() <= (int64_t)INT32_MAX) {
         // Kp in schedule order: row q = Kp row perm_s[q] with its entries in Kp's order, columns
         // renumbered to schedule positions (perm_s = the relabelled factor's pivot order)
@@ -130,6 +115,9 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
         });
         make_dmat(ks, pc->dKps);
         pc->kps_from.upload(from);
+        plan_round0(c, pc->dF, ks.ptr.data());
+    } else {
+        plan_round0(c, pc->dF, nullptr);
     }
     if (pc->dKps.nnz && pc->dF.ndet == 0) pc->xs.alloc(pc->N);
     if (pc->dKps.nnz && pc->dF.round0_rows >= 0 && pc->dF.fcol16.n > 0)
@@ -146,6 +134,40 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
     return pc.release();
 }
 
+// Every rank builds the global analysis and its share of the plan on its own (DESIGN.md
+// section 7), so all of them must agree on the inputs, the split and every engine option (the
+// schedule, the separator exchange and the solvers' collective sequence follow from them).
+// Before the first collective of any apply, the ranks allgather a hash of all of it; on a
+// mismatch every rank throws the same error instead of exchanging mismatched payloads.
+uint64_t plan_hash(const Ctx &c, const Analysis &an, const TreeSplit &ts) {
+    uint64_t h = engine_opts_hash(c.opts);
+    auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+    mix((uint64_t)c.nranks), mix((uint64_t)an.n), mix((uint64_t)an.m), mix((uint64_t)an.Kp.nnz());
+    for (int32_t v : an.F0.perm) mix((uint32_t)v);
+    for (int64_t v : an.F0.Lp) mix((uint64_t)v);
+    for (int32_t v : ts.node_rank) mix((uint32_t)v);
+    for (int32_t v : ts.T) mix((uint32_t)v);
+    return h;
+}
+
+void check_plan_agreement(Ctx &c, uint64_t h) {
+    if (!c.comm->has_peers()) return;
+    const double mine[2] = {(double)(h >> 32), (double)(h & 0xffffffffull)};  // exact in fp64
+    DBuf<double> snd, rcv;
+    snd.alloc(2), rcv.alloc((size_t)2 * c.nranks);
+    CPK_HIP(hipMemcpy(snd.p, mine, sizeof mine, hipMemcpyHostToDevice));
+    c.comm->allgather(snd.p, rcv.p, 2, c.stream);
+    std::vector<double> all((size_t)2 * c.nranks);
+    CPK_HIP(hipMemcpyAsync(all.data(), rcv.p, rcv.bytes(), hipMemcpyDeviceToHost, c.stream));
+    CPK_HIP(hipStreamSynchronize(c.stream));
+    std::string bad;
+    for (int r = 0; r < c.nranks; r++)
+        if (all[2 * r] != all[0] || all[2 * r + 1] != all[1]) bad += (bad.empty() ? "" : ", ") + std::to_string(r);
+    if (!bad.empty())
+        throw Error(CPK_ERR_ARGS, "distributed preconditioner: the plan of rank(s) " + bad +
+                                      " differs from rank 0's (inputs or engine options differ between ranks)");
+}
+
 Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     auto t0 = std::chrono::steady_clock::now();
     auto pc = std::make_unique<Precond>();
@@ -153,7 +175,8 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     pc->dist = true;
     pc->gn = an.n, pc->gm = an.m, pc->gN = an.N;
     pc->ordering = an.ordering;
-    const TreeSplit ts = split_tree(an.F0, c.nranks, split_tol_option(), -1, Akry);
+    const TreeSplit ts = split_tree(an.F0, c.nranks, c.opts.split_tol, -1, Akry);
+    check_plan_agreement(c, plan_hash(c, an, ts));
     auto dm = std::make_shared<DofMap>(make_dofmap(an.F0, ts, an.n));
     RankPlan rp = make_rank_plan(an.F0, ts, *dm, c.rank);
     pc->n = dm->n_loc[c.rank], pc->m = dm->m_loc[c.rank], pc->N = pc->n + pc->m;
@@ -164,9 +187,11 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     std::vector<int64_t> nextra(rp.nsub);
     for (int64_t j = 0; j < rp.nsub; j++) nextra[j] = (int64_t)rp.extra[j].size();
     const SweepConfig &sw = an.sweep;
-    Schedule S = build_schedule(rp.Fsub, sw.rows[0], sw.cap[0], sw.rows[1], sw.cap[1], sw.sub0, &nextra);
+    Schedule S = build_schedule(rp.Fsub, sw.rows[0], sw.cap[0], sw.rows[1], sw.cap[1], sw.sub0, &nextra, c.opts.detach);
     for (int i = 0; i < 2; i++)
         pc->dF.sweep_rows[i] = sw.rows[i], pc->dF.sweep_cap[i] = sw.cap[i], pc->dF.sweep_threads[i] = sw.threads[i];
+    pc->dF.pipelined = !c.opts.no_pipe, pc->dF.no_upper = c.opts.no_upper, pc->dF.no_col16 = c.opts.no_col16;
+    pc->dF.no_fused_resid = c.opts.no_fused_resid, pc->dF.fused_tail_launch = c.opts.fused_tail_launch;
     {
         Factor Fl = relabel(rp.Fsub, S);
         std::vector<int64_t> key(rp.nsub);
@@ -178,6 +203,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
             pos[S.order[q]] = (int32_t)q;
         }
         make_dfactor(Fl, S, pc->dF, &key, &extra);
+        plan_round0(c, pc->dF, nullptr);
         std::vector<int32_t> send(rp.tsend.size());
         for (size_t i = 0; i < send.size(); i++) send[i] = pos[rp.tsend[i]];
         pc->sep.send.upload(send);
@@ -197,6 +223,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
         rp.kt = kt1;
     }
     T.nT = rp.nT, T.kt = rp.kt, T.nlev = (int64_t)rp.tlev_ptr.size() - 1, T.ntdof = (int64_t)rp.tdof.size();
+    T.tsolve_global = c.opts.tsolve_global, T.tsolve_onepass = c.opts.tsolve_onepass;
     T.kt_data = rp.kt > 0 ? rp.kt - kSepPiggy : 0;
     auto i32 = [](const std::vector<int64_t> &v) { return std::vector<int32_t>(v.begin(), v.end()); };
     T.tf_ptr.upload(i32(rp.tf_ptr)), T.tf_col.upload(rp.tf_col), T.tf_val.upload(rp.tf_val);
@@ -235,10 +262,10 @@ uint64_t pattern_hash(const HCsr &A11, const HCsr &B, const HCsr &C22) {
 }
 
 // Single GPU: the host does the symbolic analysis, the device the numeric factorization
-// (CPK_HOST_FACTOR=1: host numeric, the reference path of the device one's parity tests).
+// (engine option host_factor: host numeric, the reference path of the device one's parity tests).
 Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22) {
-    const bool dev = getenv("CPK_HOST_FACTOR") == nullptr;
-    Analysis an = analyze(A11, B, C22, dev);
+    const bool dev = !c.opts.host_factor;
+    Analysis an = analyze(A11, B, C22, c.opts, dev);
     std::vector<int64_t> src;
     if (dev) src = kp_value_sources(A11, B, C22);
     Precond *pc = precond_create(c, std::move(an));
@@ -252,9 +279,22 @@ double precond_refactor(Precond &p, const DMat &A11, const DMat &B, const DMat &
         throw Error(CPK_ERR_UNSUPPORTED, "refactorization needs a single-GPU preconditioner with the device factorization");
     auto t0 = std::chrono::steady_clock::now();
     Ctx &c = *p.ctx;
-    dldl_assemble_kp(c, p.dl, A11.val.p, B.val.p, C22.val.p, p.dKp.val.p);
+    // all or nothing: the new Kp and factor are formed in scratch buffers; a bad pivot throws
+    // before anything the preconditioner holds (Kp, Kps, L, D, the sweep values) is touched
+    DBuf<double> kpv, Lx, D;
+    kpv.alloc((size_t)std::max<int64_t>(p.dKp.nnz, 1));
+    Lx.alloc(p.dl.Lx.n);
+    D.alloc(p.dl.D.n);
+    dldl_assemble_kp(c, p.dl, A11.val.p, B.val.p, C22.val.p, kpv.p);
+    dldl_numeric(c, p.dl, kpv.p, Lx.p, D.p);
+    // commit (copies, not buffer swaps: captured solver graphs hold these addresses)
+    if (p.dKp.nnz) CPK_HIP(hipMemcpyAsync(p.dKp.val.p, kpv.p, p.dKp.val.bytes(), hipMemcpyDeviceToDevice, c.stream));
+    CPK_HIP(hipMemcpyAsync(p.dl.Lx.p, Lx.p, Lx.bytes(), hipMemcpyDeviceToDevice, c.stream));
+    CPK_HIP(hipMemcpyAsync(p.dl.D.p, D.p, D.bytes(), hipMemcpyDeviceToDevice, c.stream));
     if (p.dKps.nnz) launch_gather(c, p.dKp.val.p, p.kps_from.p, p.dKps.nnz, p.dKps.val.p);
-    dldl_factor(c, p.dl, p.dKp.val.p, p.dF);
+    dldl_fill(c, p.dl, p.dF);
+    // a rebuilt opLDL2 starts with op.Aty = op.Cy = 0 (opLDL2.m:90-91): so does the handle state
+    if (p.handle && p.ghn.n) p.ghn.zero(c.stream);
     // the host copy of Kp follows (divide / export read the device copies; the distributed
     // shift rows, built from the host copy, do not exist on one GPU)
     if (!p.Kp.val.empty())
@@ -364,7 +404,7 @@ double Precond::apply_bytes() const {
         double b = fwd + (xs.n ? 8 * Nn : 0.0) /*xs written*/ + bwd_keep + steps * (kps + fwd_s + bwd_acc) + (4 + 8) * Nn /*last: perm + scatter*/ +
                    (steps - 1) * 8.0 * Nn /*ys written back in place*/;
         // fused refinement input (launch_sptrsv_fwd_resid): r is neither written nor read back
-        if (xs.n && kps_tail_nblk >= 0 && dF.pipelined && !getenv("CPK_NO_FUSED_RESID"))
+        if (xs.n && kps_tail_nblk >= 0 && dF.pipelined && !dF.no_fused_resid)
             b -= steps * 16.0 * Nn;
         return b;
     }

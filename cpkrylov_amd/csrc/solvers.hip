@@ -1366,12 +1366,10 @@ struct SolveCore {
             if (o->has_mem) mem = std::max(1.0, o->mem);  // cpdqgmres.m:116-118
             if (o->has_print) print = o->print != 0;
         }
-        use_graph = true;
-        if (const char *e = getenv("CPK_NO_GRAPH")) use_graph = atoi(e) == 0;
-        if (c.dist() && !c.comm->capturable()) use_graph = false;
+        use_graph = !c.opts.no_graph;
+        if (c.dist() && !(c.comm->capturable() && c.opts.dist_graph)) use_graph = false;
         if (c.rank != 0) print = false;
-        batch = 16;
-        if (const char *e = getenv("CPK_BATCH")) batch = std::max(1, atoi(e));
+        batch = c.opts.batch > 0 ? c.opts.batch : 16;
         printed = 0;
         ring_next = 0;
     }
@@ -1480,7 +1478,7 @@ struct SolveCore {
         if (h.stop) return;
         const int64_t guard = h.k + (int64_t)std::min(itmax, 4.0e9) + 2 * batch + 2;
         int b = pow2_at_least(batch, 64);
-        const bool adapt = getenv("CPK_BATCH") == nullptr;
+        const bool adapt = c.opts.batch <= 0;
         for (;;) {
             const double res0 = h.residNorm;
             const int64_t k0 = h.k;
@@ -1602,9 +1600,9 @@ void SolveCore::minres_like(int kind, const double *b, double *xy, cpk_stats *st
         }
         // distributed: vprec = M*[u; -t] does not depend on alpha (cpminres.m:187-190), so alpha's
         // partials ride in the preconditioner's first separator allgather instead of an allreduce
-        const bool piggy = c.dist() && M.piggyback_ok() && !getenv("CPK_NO_PIGGY");
+        const bool piggy = c.dist() && M.piggyback_ok() && !c.opts.no_piggy;
         // and beta's partials ride in the next Lanczos vector's halo exchange (spare slots)
-        const bool hmerge = piggy && AC.halo() && AC.kstride >= AC.kmax + 2 && !getenv("CPK_NO_HALO_MERGE");
+        const bool hmerge = piggy && AC.halo() && AC.kstride >= AC.kmax + 2 && !c.opts.no_halo_merge;
         const PolLanczosSpmv<0> pol{VQ, N, 0};
         if (hmerge) launch_krylov_halo(c, AC, st, pol);  // v1's halo, before the first iteration
         auto body = [&]() {
@@ -1879,13 +1877,13 @@ static std::string solver_key(const Ctx &c, const Precond &M, const DMat &AC, in
     char buf[512];
     const double restart = o && o->has_restart ? o->restart : 50, mem = o && o->has_mem ? o->mem : 50;
     const double itmax = o && o->has_itmax ? o->itmax : -1;
-    snprintf(buf, sizeof buf, "%d|%llu|%p|%p|%p|%p|%p|%.17g|%.17g|%.17g|%d|%.17g|%.17g|%.17g|%s|%s|%d%d", method,
+    // the context's engine options enter through their hash (graphs captured under one set of
+    // options are not replayed under another)
+    snprintf(buf, sizeof buf, "%d|%llu|%p|%p|%p|%p|%p|%.17g|%.17g|%.17g|%d|%.17g|%.17g|%.17g|%llx", method,
              (unsigned long long)AC.gen, (const void *)d_b, (const void *)d_xy, (const void *)c.partials.p,
              (const void *)c.counter.p, (const void *)c.red.p, M.nitref, M.force_itref, M.itref_tol,
              (M.residual_update != 0 && M.handle) ? 1 : 0, restart, mem,
-             method == CPK_DQGMRES ? itmax : 0.0, getenv("CPK_BATCH") ? getenv("CPK_BATCH") : "",
-             getenv("CPK_NO_GRAPH") ? getenv("CPK_NO_GRAPH") : "", getenv("CPK_NO_PIGGY") ? 1 : 0,
-             getenv("CPK_NO_HALO_MERGE") ? 1 : 0);
+             method == CPK_DQGMRES ? itmax : 0.0, (unsigned long long)engine_opts_hash(c.opts));
     return buf;
 }
 
@@ -2004,7 +2002,7 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
         out->resid_ms = timeit([&]() { launch_spmv_resid(c, M.dKp, x.p, M.n, y.p, z.p, nullptr, nullptr); });
         out->resid_bytes = 12.0 * M.dKp.nnz + 4.0 * (Nn + 1) + 8.0 * Nn /*y*/ + 8.0 * Nn /*x*/ + 8.0 * Nn /*r*/;
     }
-    if (getenv("CPK_PROFILE_FWD_NOLEVELS"))
+    if (c.opts.profile_fwd_nolevels)
         out->fwd_ms = timeit([&]() { launch_sptrsv_fwd_diag(c, M.dF, x.p, M.n, M.w.p); });
     else
         out->fwd_ms = timeit([&]() { launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr); });

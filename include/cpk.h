@@ -115,6 +115,18 @@ typedef struct cpk_simgroup_s *cpk_simgroup;
 int cpk_simgroup_create(int nranks, cpk_simgroup *out);
 int cpk_simgroup_destroy(cpk_simgroup g);
 int cpk_ctx_create_sim(int device, cpk_simgroup group, int rank, int nranks, cpk_ctx *out);
+/* Engine options of a context (no reference counterpart: they choose among execution paths
+ * that give identical results, and the sweep schedule / distributed split that every rank
+ * must build identically).  A context starts from the CPK_<NAME> environment variables, read
+ * once at creation; a change applies to preconditioners and solves created afterwards.
+ * Names: sweep ("rows,cap,threads[,rows,cap,threads[,sub0]]"), detach, split_tol, host_factor,
+ * no_pipe, no_upper, no_col16, no_sched_resid, no_fused_resid, fused_tail_launch, r0_stride,
+ * tsolve_global, tsolve_onepass, no_piggy, no_halo_merge, no_graph, dist_graph, batch,
+ * profile_fwd_nolevels.  Booleans as "0"/"1".  A distributed preconditioner allgathers a hash
+ * of its plan and of every option at creation and fails (CPK_ERR_ARGS) on every rank unless
+ * all ranks agree. */
+int cpk_ctx_set_option(cpk_ctx ctx, const char *name, const char *value);
+int cpk_ctx_get_option(cpk_ctx ctx, const char *name, char *buf, size_t cap);
 int cpk_ctx_destroy(cpk_ctx ctx);
 int cpk_ctx_synchronize(cpk_ctx ctx);
 
@@ -175,6 +187,10 @@ int cpk_pc_get_info(cpk_pc M, cpk_pc_info *info);
  * info[7] = {distributed, separator rows, levels, step records, LDS bytes with the records
  * staged (0: they do not fit), LDS bytes with the records left in HBM, payload per rank}. */
 int cpk_pc_sep_info(cpk_pc M, int64_t *info);
+/* Diagnostic (not in the reference): the sweep schedule as launched, info[8] = {rounds, round-0
+ * blocks, blocks above round 0, grid of the cost-balanced round-0 assignment of the forward /
+ * fused-residual forward / backward kernel (0: the launch strides), round 0 persistent, 0}. */
+int cpk_pc_sweep_info(cpk_pc M, int64_t *info);
 int cpk_pc_local_dofs(cpk_pc M, int64_t *n_loc, int64_t *m_loc, int32_t *dofs);
 /* Export the factors P'*Kp*P = L*D*L': strict-lower L in CSC (Lcolptr[N+1], Lrowind[nnz_l],
  * Lval[nnz_l]), D[N], perm[N] (perm[k] = original index of pivot k).  Any pointer may be NULL. */
@@ -255,6 +271,10 @@ int cpk_profile_kernels(cpk_ctx ctx, cpk_mat A, cpk_mat C, cpk_pc M, int reps, c
  * last round-0 sweep launch, 100 MHz ticks; *copied = 0 unless the library was built with
  * -DCPK_PIPE_STAMPS (tools/pipe_stamps.py). */
 int cpk_debug_pipe_stamps(uint64_t *out, int npairs, int *copied);
+/* Diagnostic: per-block s_memtime cycles of the last round-0 launch of each kernel variant,
+ * out[v * 131072 + block] for v = forward, forward with the fused refinement residual, backward,
+ * backward accumulating; *copied = 0 unless built with -DCPK_PIPE_STAMPS (tools/blk_cycles.py). */
+int cpk_debug_blk_cycles(uint64_t *out, int64_t n, int64_t *copied);
 
 /* [c, s, d] = SymGivens(a, b)  (util/SymGivens.m:1-29) */
 int cpk_symgivens(double a, double b, double *c, double *s, double *d);

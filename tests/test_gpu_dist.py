@@ -25,13 +25,15 @@ FLOOR = 1e-8
 SAFETY = 10.0
 
 
-def _run_ranks(P, fn):
-    """fn(ctx, rank) on P simulated ranks; returns the list of results."""
+def _run_ranks(P, fn, options=None):
+    """fn(ctx, rank) on P simulated ranks; returns the list of results.  options: engine options
+    of every rank's context (a dict), or a function rank -> dict."""
     import cpkrylov_amd as cpk
     g = cpk.SimGroup(P)
 
     def one(r):
-        ctx = cpk.Context(device=0, rank=r, nranks=P, simgroup=g)
+        opt = options(r) if callable(options) else options
+        ctx = cpk.Context(device=0, rank=r, nranks=P, simgroup=g, options=opt)
         try:
             return fn(ctx, r)
         finally:
@@ -207,7 +209,7 @@ def test_dist_more_ranks_than_subtrees(P):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("P", [2, 3])
-def test_dist_minres_merged_exchanges(P, monkeypatch):
+def test_dist_minres_merged_exchanges(P):
     """cpminres's scalar exchanges ride in other collectives (alpha's partials in the first
     separator allgather, beta's in the next Lanczos vector's halo allgather, which the owners'
     normalisation is then applied to).  Each partial sum is then taken in rank order; the
@@ -216,20 +218,16 @@ def test_dist_minres_merged_exchanges(P, monkeypatch):
     Pd = F.load("cvxqp1_m")
     opts = dict(F.EXPROG_OPTS)
 
-    def run():
+    def run(options):
         def work(ctx, r):
             x, stats, flag = cpk.reg_cpkrylov(cpk.cpminres, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts,
                                               ctx=ctx)
             return x, stats["residHistory"], stats["niters"]
-        return _run_ranks(P, work)[0]
+        return _run_ranks(P, work, options)[0]
 
     variants = {}
-    for name, env in [("merged", {}), ("no_halo_merge", {"CPK_NO_HALO_MERGE": "1"}), ("plain", {"CPK_NO_PIGGY": "1"})]:
-        for k in ("CPK_NO_HALO_MERGE", "CPK_NO_PIGGY"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        variants[name] = run()
+    for name, options in [("merged", {}), ("no_halo_merge", {"no_halo_merge": 1}), ("plain", {"no_piggy": 1})]:
+        variants[name] = run(options)
     x0, h0, n0 = variants["plain"]
     for name in ("merged", "no_halo_merge"):
         x, h, n = variants[name]
@@ -239,22 +237,21 @@ def test_dist_minres_merged_exchanges(P, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["CPK_TSOLVE_GLOBAL", "CPK_TSOLVE_ONEPASS"])
+@pytest.mark.parametrize("path", ["tsolve_global", "tsolve_onepass"])
 @pytest.mark.parametrize("P", [2, 4])
-def test_dist_apply_separator_fallbacks_bitexact(P, path, monkeypatch):
+def test_dist_apply_separator_fallbacks_bitexact(P, path):
     """The separator solve's fallbacks (records left in HBM for a separator too large for LDS;
     the one-pass global kernel) give the same bits as the staged solve and the oracle."""
     import cpkrylov_amd as cpk
     S = _system("synthetic20k")
     z = np.random.default_rng(7).standard_normal(S["n"] + S["m"])
-    monkeypatch.setenv(path, "1")
 
     def work(ctx, r):
         M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
         M.nitref, M.force_itref = 1, True
         return M * z, M.export_factors() if r == 0 else None
 
-    res = _run_ranks(P, work)
+    res = _run_ranks(P, work, {path: 1})
     L, D, perm = res[0][1]
     Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=(L, D, perm))
     Mo.set(nitref=1.0, force_itref=1.0)
@@ -263,24 +260,22 @@ def test_dist_apply_separator_fallbacks_bitexact(P, path, monkeypatch):
         assert np.array_equal(y, yo), np.max(np.abs(y - yo))
 
 
-def test_dist_apply_separator_records_overflow_lds(monkeypatch):
+def test_dist_apply_separator_records_overflow_lds():
     """A separator whose step records really exceed the 160 KB of LDS (a small split tolerance
     grows T): the stepped solve reads its records from HBM (lds == 0, lds_g > 0), and the
-    apply still equals the oracle's bit for bit.  (The CPK_TSOLVE_GLOBAL test above forces
+    apply still equals the oracle's bit for bit.  (The tsolve_global test above forces
     that path on a separator that would fit.)"""
     import cpkrylov_amd as cpk
     S = saddle_system(N=400000, seed=21)
     z = np.random.default_rng(8).standard_normal(S["n"] + S["m"])
     P = 4
     for tol in ("0.002", "0.0005", "0.0002", "0.0001"):
-        monkeypatch.setenv("CPK_SPLIT_TOL", tol)
-
         def work(ctx, r):
             M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
             M.nitref, M.force_itref = 1, True
             return M * z, M.sep_info(), M.export_factors() if r == 0 else None
 
-        res = _run_ranks(P, work)
+        res = _run_ranks(P, work, {"split_tol": tol})
         info = res[0][1]
         if info["lds"] == 0:
             break
@@ -324,3 +319,25 @@ def test_dist_placement_hint_nonsym(P):
     h, ho = st["residHistory"], so["residHistory"]
     assert len(h) == len(ho) and np.max(np.abs(h - ho)) <= 1e-8 * ho[0]
     assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
+
+
+@pytest.mark.parametrize("option,value", [("sweep", "256,768,64"), ("split_tol", "0.06"), ("no_piggy", 1)])
+def test_dist_plan_mismatch_fails_on_every_rank(option, value):
+    """Every rank builds the global plan on its own, so ranks whose engine options differ would
+    exchange mismatched payloads.  At setup the ranks allgather a hash of the plan and of every
+    option: with one rank's option changed, every rank fails with the same clean error before
+    any apply (no hang, no wrong answer)."""
+    import cpkrylov_amd as cpk
+    S = _system("synthetic20k")
+
+    def work(ctx, r):
+        try:
+            cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+        except cpk.CpkError as e:
+            return str(e)
+        return None
+
+    res = _run_ranks(2, work, lambda r: {option: value} if r == 1 else {})
+    assert all(m is not None and "plan of rank(s) 1 differs" in m for m in res), res
+    # the same options on every rank: no error
+    assert _run_ranks(2, work, {option: value}) == [None, None]

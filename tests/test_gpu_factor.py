@@ -121,9 +121,39 @@ def test_refactor_zero_pivot_reported(gpu_ctx):
     M = cpk.opLDL2(S["G"], S["B"], -S["C"])
     G0 = S["G"].copy()
     G0.data = G0.data * 0.0
+    M.nitref, M.force_itref = 1, True
+    z = np.random.default_rng(4).standard_normal(M.n)
+    y0, k0 = M * z, M.divide(z)
+    L0, D0, _ = M.export_factors()
     with pytest.raises(cpk.CpkError) as e:
         M.refactor(G0, S["B"], -S["C"])
     assert "pivot" in str(e.value)
+    # all or nothing: the failed refactorization left Kp, the factors and the sweeps untouched
+    L1, D1, _ = M.export_factors()
+    assert np.array_equal(L1.data, L0.data) and np.array_equal(D1, D0)
+    assert np.array_equal(M * z, y0)
+    assert np.array_equal(M.divide(z), k0)
+
+
+def test_refactor_resets_handle_state(gpu_ctx):
+    """A refactorization is a rebuilt opLDL2, whose constructor zeroes op.Aty and op.Cy
+    (opLDL2.m:90-91): with handle semantics on, the first apply after it equals the first
+    apply of a fresh preconditioner."""
+    import cpkrylov_amd as cpk
+    S = _system("cvxqp2_s")
+    rng = np.random.default_rng(6)
+    z1, z2 = rng.standard_normal(S["G"].shape[0] + S["B"].shape[0]), rng.standard_normal(S["G"].shape[0] + S["B"].shape[0])
+    M = cpk.opLDL2(S["G"], S["B"], -S["C"])
+    M.residual_update, M.nitref = True, 1
+    M.handle_semantics = True
+    M * z1  # leaves a nonzero state
+    G2 = S["G"].copy()
+    G2.data = G2.data * 1.5
+    M.refactor(G2, S["B"], -S["C"])
+    F = cpk.opLDL2(G2, S["B"], -S["C"])
+    F.residual_update, F.nitref = True, 1
+    F.handle_semantics = True
+    assert np.array_equal(M * z2, F * z2)
 
 
 def test_minres_after_refactor_matches_oracle(gpu_ctx):

@@ -142,6 +142,26 @@ def test_csc_boundary_matches_csr():
     assert a["info"] == b["info"]
 
 
+def test_engine_option_from_env_validated(monkeypatch):
+    """Engine options start from CPK_<NAME> (read when a context or a host-only analysis is
+    made); a malformed value is an error, not a silent default, and a valid sweep option changes
+    the schedule."""
+    S = saddle_system(N=20000, seed=3)
+    for bad in ("abc", "0,0,64", "192,576,48", "100000,576,64"):
+        monkeypatch.setenv("CPK_SWEEP", bad)
+        with pytest.raises(cpk.CpkError):
+            cpk.analyze(S["G"], S["B"], -S["C"])
+    monkeypatch.setenv("CPK_SWEEP", "64,128,64")
+    small = cpk.analyze(S["G"], S["B"], -S["C"])["info"]
+    monkeypatch.delenv("CPK_SWEEP")
+    monkeypatch.setenv("CPK_NO_PIPE", "maybe")
+    with pytest.raises(cpk.CpkError):
+        cpk.analyze(S["G"], S["B"], -S["C"])
+    monkeypatch.delenv("CPK_NO_PIPE")
+    default = cpk.analyze(S["G"], S["B"], -S["C"])["info"]
+    assert small["nblocks"] > default["nblocks"]
+
+
 def test_split_tol_option_validated(monkeypatch):
     """CPK_SPLIT_TOL (a diagnostic of the distributed plan) must be a finite number in (0, 1):
     every rank builds the same plan from it, so a malformed value is an error, not a default."""
