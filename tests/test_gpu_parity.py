@@ -312,14 +312,16 @@ def test_precond_apply_fused_residual(gpu_ctx, name, sweep):
         assert np.array_equal(ys[0], yo), np.max(np.abs(ys[0] - yo))
 
 
-@pytest.mark.parametrize("name", ["cvxqp1_m", "synthetic"])
-def test_precond_apply_round0_assignment(gpu_ctx, name):
+def test_precond_apply_round0_assignment(gpu_ctx):
     """Round 0's blocks run in the host's cost-balanced assignment to the persistent launch's
     workgroups (default) or every G-th block per workgroup (engine option r0_stride): which
     workgroup runs a block changes nothing in it -- the same bits either way, and as the oracle
-    (forward, fused-residual forward and backward variants: one refinement step)."""
+    (forward, fused-residual forward and backward variants: one refinement step).  1M dofs:
+    more round-0 blocks than the launch has workgroups, so the assignment exists."""
     import cpkrylov_amd as cpk
-    G, B, C = _system_gbc(name)
+    from cpkrylov_amd.synthetic import saddle_system
+    S = saddle_system(N=1_000_000, seed=7)
+    G, B, C = S["G"], S["B"], S["C"]
     z = np.random.default_rng(29).standard_normal(G.shape[0] + B.shape[0])
     ys = []
     for stride in (False, True):
@@ -328,7 +330,9 @@ def test_precond_apply_round0_assignment(gpu_ctx, name):
         M.nitref, M.force_itref = 1, True
         ys.append(M * z)
         info = M.sweep_info()
-        assert (info["round0_assigned"] == 0) == stride or info["round0_blocks"] < 2, info
+        assert info["round0_blocks"] > 4096, info
+        for k in ("round0_assigned", "resid_assigned", "bwd_assigned"):
+            assert (info[k] == 0) == stride, info
     L, D, perm = M.export_factors()
     Mo = O.LDL2(G, B, -C, factors=(L, D, perm))
     Mo.set(nitref=1.0, force_itref=1.0)

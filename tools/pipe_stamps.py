@@ -39,6 +39,14 @@ def stamps(label):
                       "wg_dur_mean_min_max_us": [round(float(dur.mean()), 2), round(float(dur.min()), 2),
                                                  round(float(dur.max()), 2)],
                       "tail_after_p50_us": round(float(q[3] - q[0]), 2)}), flush=True)
+    # per XCD (blocks b and b + 8 share one) and per dispatch round (blockIdx // 2048): is the
+    # spread of workgroup durations tied to where a workgroup runs?
+    g = np.arange(len(dur))
+    xcd = [round(float(dur[g % 8 == x].mean()), 1) for x in range(8)]
+    xmax = [round(float(dur[g % 8 == x].max()), 1) for x in range(8)]
+    half = [round(float(dur[(g // 256) == h].mean()), 1) for h in range(min(16, (len(dur) + 255) // 256))]
+    print(json.dumps({"launch": label, "dur_mean_by_xcd": xcd, "dur_max_by_xcd": xmax,
+                      "dur_mean_by_256_block_group": half}), flush=True)
 
 
 p = _lib.Profile()
