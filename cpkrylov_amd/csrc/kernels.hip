@@ -937,6 +937,61 @@ __device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_firs
     }
 }
 
+// The level phase of the persistent round-0 kernel with rows OWNED by lanes: lane tid owns the
+// block rows tid + j * TPB (j < RPT) and holds their entry ranges and accumulators in registers
+// from the start of the phase, so a level costs the gathers of its rows' terms and one store,
+// without first reading each row's bounds and value from LDS (sweep_levels walks row a + tid of
+// each level and reads them per level).  Rows are contiguous by level, so a level's rows are the
+// owned rows inside [lv[l], lv[l + 1]).  Same terms, same order, same chunking against the 1.0
+// slot as sweep_levels<..., ONE>: bit-identical.
+// A one-wave workgroup (TPB = 64) needs no barrier between levels: a wave's LDS operations are
+// processed in issue order, so the next level's gathers read this level's stores; only the
+// compiler must keep the order (a memory clobber), and no s_waitcnt drains the stores first.
+// CPK_LEVEL_OWN (A/B builds): 0 sweep_levels, 1 owned rows with a barrier per level, 2 owned
+// rows, one-wave levels without it.
+#ifndef CPK_LEVEL_OWN
+#define CPK_LEVEL_OWN 2
+#endif
+template <int TPB, int RPT, bool BWD, int CH>
+__device__ __forceinline__ void levels_owned(SweepLds &S, int nl, int nr, bool skip_first, int tid) {
+    static_assert(CH <= kSweepPad, "chunk wider than the padding");
+    uint32_t pe[RPT];  // e0 | e1 << 16 of each owned row
+    double acc[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; j++) {
+        const int k = tid + j * TPB;
+        pe[j] = 0u, acc[j] = 0.0;
+        if (k < nr) pe[j] = (uint32_t)(uint16_t)S.p[k] | ((uint32_t)(uint16_t)S.p[k + 1] << 16), acc[j] = S.w[k];
+    }
+    int li0 = 0;
+    if (skip_first && !BWD) li0 = 1;
+    for (int li = li0; li < nl; li++) {
+        const int l = BWD ? nl - 1 - li : li;
+        const int a = S.lv[l], z = S.lv[l + 1];
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const int k = tid + j * TPB;
+            if (k >= a && k < z) {
+                double ac = acc[j];
+                const int e1 = (int)(pe[j] >> 16);
+                for (int e = (int)(pe[j] & 0xffffu); e < e1; e += CH) {
+                    int c[CH];
+                    double v[CH], x[CH];
+#pragma unroll
+                    for (int i = 0; i < CH; i++) c[i] = S.c[e + i], v[i] = S.v[e + i];
+#pragma unroll
+                    for (int i = 0; i < CH; i++) x[i] = S.w[c[i]];
+#pragma unroll
+                    for (int i = 0; i < CH; i++) ac -= (e + i < e1) ? v[i] * x[i] : 0.0;
+                }
+                S.w[k] = ac;
+            }
+        }
+        if (CPK_LEVEL_OWN >= 2 && TPB == kWave) asm volatile("" ::: "memory");
+        else __syncthreads();
+    }
+}
+
 // Backward write-back of row k (schedule order) with value z:
 //   out != null: out[perm[k]] = z, or (ADD) base + z with base = ys[k] when ys is given (the
 //                previous solution kept in schedule order), else out[perm[k]];
@@ -1470,7 +1525,10 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
         }
         // skip0: level 0 holds only rows without entries (no detached rows: the G pivots are in
         // the blocks); with detached rows a block's level 0 subtracts their (outside) terms
-        sweep_levels<TPB, BWD, false, CPK_PIPE_CH, false, true>(S, nl, skip0 != 0, tid);
+        // lane-owned rows for the backward sweep only: A/B at S10 (profiles/r03_level_ab_v2.txt),
+        // backward 193.9 -> 186.7 us, but forward 211 -> 232 us and the fused forward 270 -> 286
+        if (CPK_LEVEL_OWN && SPLIT == 1 && BWD) levels_owned<TPB, RPT, BWD, CPK_PIPE_CH>(S, nl, nr, skip0 != 0, tid);
+        else sweep_levels<TPB, BWD, false, CPK_PIPE_CH, false, true>(S, nl, skip0 != 0, tid);
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             const int i = tid + j * TPB;
@@ -1597,12 +1655,24 @@ static const double kR0Cost[3][5] = {
     {0.0, 1.0, 1e-3, 0.0, 0.0},  // backward
 };
 
+// Relative speed of the workgroups of each dispatch slot: with four workgroups on every SIMD,
+// the first dispatched on each SIMD (blockIdx < 4 x CUs) runs fastest and the fourth slowest --
+// the SIMD issues older waves first.  Per-workgroup stamps at S10 with equal modelled work per
+// workgroup (profiles/r03_stamps_v2.log): forward 210 / 213 / 221 / 230 us, backward 139 / 148 /
+// 157 / 166 us by slot, whatever the XCD (means per XCD within 1 %).  Work is assigned in
+// proportion.  [forward (both variants), backward][slot]
+constexpr int kR0Slots = 4;
+static const double kR0SlotSpeed[2][kR0Slots] = {{1.0, 0.987, 0.952, 0.914}, {1.0, 0.946, 0.891, 0.838}};
+
 void plan_round0(Ctx &c, DFactor &d, const int64_t *kps_ptr) {
     for (int v = 0; v < 3; v++) d.agrid[v] = 0, d.aptr[v].release(), d.ameta[v].release();
     if (!d.pipelined || d.round_ptr.size() < 2 || c.opts.r0_stride) return;
     const int64_t b0 = d.round_ptr[0], nb = d.round_ptr[1] - b0;
     if (nb <= 0 || d.hmeta.size() < (size_t)(b0 + nb) * 8) return;
     int64_t grid[3] = {0, 0, 0};
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     pipe_round0(c, d, false, false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, &grid[0]);
     pipe_round0(c, d, true, false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, &grid[2]);
     if (kps_ptr && d.fcol16.n > 0 && d.ndet == 0) pipe_round0_resid(c, d, nullptr, nullptr, ResArgs{}, &grid[1]);
@@ -1620,20 +1690,30 @@ void plan_round0(Ctx &c, DFactor &d, const int64_t *kps_ptr) {
         std::vector<int64_t> ord(nb);
         for (int64_t i = 0; i < nb; i++) ord[i] = i;
         std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return cost[a] > cost[b]; });
-        // min-heap of (load, workgroup)
-        std::vector<std::pair<double, int32_t>> heap((size_t)G);
-        for (int64_t g = 0; g < G; g++) heap[g] = {0.0, (int32_t)g};
-        auto gt = [](const std::pair<double, int32_t> &a, const std::pair<double, int32_t> &b) {
-            return a.first > b.first || (a.first == b.first && a.second > b.second);
-        };
-        std::make_heap(heap.begin(), heap.end(), gt);
+        // workgroups by dispatch slot (the j-th workgroup of every SIMD), each slot with its
+        // relative speed; a block goes to the workgroup that would finish it first:
+        // min over slots of (load + cost) / speed, the least loaded workgroup of each slot a heap top
+        const int64_t per_slot = std::max<int64_t>(1, (int64_t)cus * 4);
+        const int nslot = (int)std::min<int64_t>(kR0Slots, (G + per_slot - 1) / per_slot);
+        using HE = std::pair<double, int32_t>;  // (load, workgroup)
+        auto gt = [](const HE &a, const HE &b) { return a.first > b.first || (a.first == b.first && a.second > b.second); };
+        std::vector<std::vector<HE>> heaps(nslot);
+        for (int64_t g = 0; g < G; g++) heaps[(size_t)std::min<int64_t>(g / per_slot, nslot - 1)].push_back({0.0, (int32_t)g});
+        for (auto &h : heaps) std::make_heap(h.begin(), h.end(), gt);
         std::vector<int32_t> owner(nb);
         for (int64_t i : ord) {
-            std::pop_heap(heap.begin(), heap.end(), gt);
-            auto &h = heap.back();
-            owner[i] = h.second;
-            h.first += cost[i];
-            std::push_heap(heap.begin(), heap.end(), gt);
+            int best = -1;
+            double bt = 0.0;
+            for (int s = 0; s < nslot; s++) {
+                if (heaps[s].empty()) continue;
+                const double t = (heaps[s].front().first + cost[i]) / kR0SlotSpeed[v == 2 ? 1 : 0][s];
+                if (best < 0 || t < bt) best = s, bt = t;
+            }
+            auto &h = heaps[best];
+            std::pop_heap(h.begin(), h.end(), gt);
+            owner[i] = h.back().second;
+            h.back().first += cost[i];
+            std::push_heap(h.begin(), h.end(), gt);
         }
         std::vector<int32_t> ptr((size_t)G + 1, 0), am((size_t)nb * 8);
         for (int64_t i = 0; i < nb; i++) ptr[owner[i] + 1]++;
