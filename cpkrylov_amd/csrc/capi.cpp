@@ -323,7 +323,7 @@ int cpk_pc_create(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptim
     need(ctx && A11 && B && C22 && out, "opLDL2: Invalid number of arguments.");
     auto pc = std::make_unique<cpk_pc_s>();
     pc->ctx = ctx;
-    if (ctx->c.dist()) pc->p.reset(precond_create_dist(ctx->c, analyze(A11->h, B->h, C22->h, ctx->c.opts)));
+    if (ctx->c.dist()) pc->p.reset(precond_create_dist(ctx->c, A11->h, B->h, C22->h, nullptr));
     else pc->p.reset(precond_create(ctx->c, A11->h, B->h, C22->h));
     if (ptime) *ptime = pc->p->ptime;
     *out = pc.release();
@@ -337,7 +337,7 @@ int cpk_pc_create_hint(cpk_ctx ctx, cpk_mat A11, cpk_mat B, cpk_mat C22, cpk_mat
     auto pc = std::make_unique<cpk_pc_s>();
     pc->ctx = ctx;
     if (ctx->c.dist())
-        pc->p.reset(precond_create_dist(ctx->c, analyze(A11->h, B->h, C22->h, ctx->c.opts), Akry ? &Akry->h : nullptr));
+        pc->p.reset(precond_create_dist(ctx->c, A11->h, B->h, C22->h, Akry ? &Akry->h : nullptr));
     else pc->p.reset(precond_create(ctx->c, A11->h, B->h, C22->h));
     if (ptime) *ptime = pc->p->ptime;
     *out = pc.release();
@@ -350,8 +350,8 @@ int cpk_pc_refactor(cpk_pc M, cpk_mat A11, cpk_mat B, cpk_mat C22, double *ptime
     Precond &p = *M->p;
     if (A11->h.nrows != p.gn || C22->h.nrows != p.gm || B->h.nrows != p.gm || B->h.ncols != p.gn)
         throw Error(CPK_ERR_DIM, "Incompatible dimensions.");
-    if (p.dist || !p.dl.ready)
-        throw Error(CPK_ERR_UNSUPPORTED, "refactorization needs a single-GPU preconditioner with the device factorization");
+    if (!p.dl.ready)
+        throw Error(CPK_ERR_UNSUPPORTED, "refactorization needs the device factorization (engine option host_factor off)");
     if (pattern_hash(A11->h, B->h, C22->h) != p.pattern_hash)
         throw Error(CPK_ERR_ARGS, "refactor: the sparsity of A11, B or C22 differs from the factored one");
     const double s = precond_refactor(p, A11->dev(), B->dev(), C22->dev());
@@ -636,7 +636,7 @@ int cpk_reg_solve(cpk_ctx ctx, int method, const double *b, cpk_mat A, cpk_mat B
     check_dist_method(c, method);
     auto pc = std::make_unique<cpk_pc_s>();
     pc->ctx = ctx;
-    if (c.dist()) pc->p.reset(precond_create_dist(c, analyze(G->h, B->h, negC, c.opts), &A->h));
+    if (c.dist()) pc->p.reset(precond_create_dist(c, G->h, B->h, negC, &A->h));
     else pc->p.reset(precond_create(c, G->h, B->h, negC));
     Precond &p = *pc->p;
     apply_props(p, opts);  // reg_cpkrylov.m:135-148

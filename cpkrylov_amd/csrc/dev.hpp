@@ -286,6 +286,11 @@ void dldl_factor(Ctx &c, DLdl &d, const double *kpv, DFactor &dF);
 void dldl_numeric(Ctx &c, DLdl &d, const double *kpv, double *Lx, double *D);
 // DFactor's sweep values and D from d.Lx / d.D
 void dldl_fill(Ctx &c, const DLdl &d, DFactor &dF);
+// Value maps (distributed preconditioner): a device array built from index-valued factor data
+// (value = source index + 1, 0 = no source) is captured as map[q] = value - 1 and refilled as
+// x[q] = map[q] >= 0 ? src[map[q]] : 0.0
+void vmap_capture(Ctx &c, const double *x, size_t n, DBuf<int32_t> &map);
+void vmap_fill(Ctx &c, const int32_t *map, size_t n, const double *src, double *x);
 // Kp values from the device values of A11, B, C22 through d.kp_from
 void dldl_assemble_kp(Ctx &c, const DLdl &d, const double *a, const double *b, const double *cc, double *kpv);
 
@@ -371,6 +376,18 @@ struct Precond {
     bool handle = false;
     DBuf<double> ghn, t;
     double ptime = 0;
+    // distributed preconditioner with the device factorization: every rank factors the whole
+    // system on its own GPU (dl, global Kp values kpg) and gathers its share of the values --
+    // local sweeps, separator solve, Kp rows -- through value maps built at construction
+    DBuf<double> kpg;
+    struct VMap {
+        double *dst = nullptr;
+        size_t n = 0;
+        int src = 0;  // 0: L (CSC order), 1: D (pivot order), 2: Kp entries
+        DBuf<int32_t> map;
+    };
+    std::vector<VMap> vmaps;
+    void fill_vmaps();  // every mapped array from dl.Lx, dl.D, kpg
     // cached solvers (workspace + captured iteration graphs), keyed; see solvers.hip
     std::vector<std::pair<std::string, std::shared_ptr<void>>> solvers;
     // distributed rows of the Krylov operator and the shift products, which follow this
@@ -400,5 +417,8 @@ Precond *precond_create(Ctx &c, Analysis &&an);
 // distributed preconditioner of rank c.rank out of c.nranks
 // Akry (optional): the Krylov operator's A, a placement hint for isolated rows (split_tree)
 Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry = nullptr);
+// the same from the blocks: analysis (structure only unless host_factor), device factorization
+// of the whole system on every rank, refactorization support
+Precond *precond_create_dist(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22, const HCsr *Akry);
 
 }  // namespace cpk

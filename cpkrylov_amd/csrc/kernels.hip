@@ -1660,9 +1660,12 @@ static const double kR0Cost[3][5] = {
 // the SIMD issues older waves first.  Per-workgroup stamps at S10 with equal modelled work per
 // workgroup (profiles/r03_stamps_v2.log): forward 210 / 213 / 221 / 230 us, backward 139 / 148 /
 // 157 / 166 us by slot, whatever the XCD (means per XCD within 1 %).  Work is assigned in
-// proportion.  [forward (both variants), backward][slot]
+// proportion; with those speeds the slots finished at 202 / 206 / 199 / 202 (forward) and 144 /
+// 150 / 149 / 153 us (backward, profiles/r03_stamps_v3.log), the launch tails fell from 20-25 to
+// 12 us and S10 went 820 -> 846-854 it/s (profiles/r03_assign_ab_v3.txt); the speeds below are
+// that run's, corrected once more by its finish times.  [forward (both variants), backward][slot]
 constexpr int kR0Slots = 4;
-static const double kR0SlotSpeed[2][kR0Slots] = {{1.0, 0.987, 0.952, 0.914}, {1.0, 0.946, 0.891, 0.838}};
+static const double kR0SlotSpeed[2][kR0Slots] = {{1.0, 0.970, 0.964, 0.914}, {1.0, 0.906, 0.856, 0.789}};
 
 void plan_round0(Ctx &c, DFactor &d, const int64_t *kps_ptr) {
     for (int v = 0; v < 3; v++) d.agrid[v] = 0, d.aptr[v].release(), d.ameta[v].release();

@@ -246,6 +246,34 @@ void dldl_fill(Ctx &c, const DLdl &d, DFactor &dF) {
     CPK_HIP(hipGetLastError());
 }
 
+__global__ void vmap_capture_kernel(const double *__restrict__ x, int64_t n, int32_t *__restrict__ map) {
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
+        map[q] = (int32_t)x[q] - 1;  // exact: indices < 2^31
+}
+
+__global__ void vmap_fill_kernel(const int32_t *__restrict__ map, int64_t n, const double *__restrict__ src,
+                                 double *__restrict__ x) {
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t s = map[q];
+        x[q] = s >= 0 ? src[s] : 0.0;
+    }
+}
+
+void vmap_capture(Ctx &c, const double *x, size_t n, DBuf<int32_t> &map) {
+    map.alloc(n);
+    if (!n) return;
+    const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(vmap_capture_kernel, dim3(grid), dim3(256), 0, c.stream, x, (int64_t)n, map.p);
+    CPK_HIP(hipGetLastError());
+}
+
+void vmap_fill(Ctx &c, const int32_t *map, size_t n, const double *src, double *x) {
+    if (!n) return;
+    const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(vmap_fill_kernel, dim3(grid), dim3(256), 0, c.stream, map, (int64_t)n, src, x);
+    CPK_HIP(hipGetLastError());
+}
+
 void dldl_factor(Ctx &c, DLdl &d, const double *kpv, DFactor &dF) {
     dldl_numeric(c, d, kpv, d.Lx.p, d.D.p);
     dldl_fill(c, d, dF);

@@ -170,6 +170,19 @@ void check_plan_agreement(Ctx &c, uint64_t h) {
 
 Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     auto t0 = std::chrono::steady_clock::now();
+    PhaseClock clk("precond_create_dist");
+    // device factorization (an.device_numeric): the host analysis holds the structure only; the
+    // plan is built from an INDEX-valued factor (L entry p -> p + 1, D row v -> v + 1, Kp entry
+    // q -> q + 1), so every value array of this rank's plan holds where its values come from.
+    // Those become value maps (vmap_capture), and the device factorization of the whole system
+    // fills them (fill_vmaps): the values a host-factored plan would copy, bit for bit.
+    const bool devnum = an.device_numeric;
+    if (devnum) {
+        an.F0.Lx.resize(an.F0.Li.size());
+        for (size_t p = 0; p < an.F0.Lx.size(); p++) an.F0.Lx[p] = (double)(p + 1);
+        an.F0.D.resize((size_t)an.F0.N);
+        for (int64_t v = 0; v < an.F0.N; v++) an.F0.D[v] = (double)(v + 1);
+    }
     auto pc = std::make_unique<Precond>();
     pc->ctx = &c;
     pc->dist = true;
@@ -235,7 +248,33 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     T.sbuf.zero(c.stream);
     T.rbuf.alloc((size_t)std::max<int64_t>(T.kt * c.nranks, 1));
     // refinement residual rows of Kp with their halo
-    make_dist_dmat(dist_csr(an.Kp, *dm, c.rank, false), c.nranks, pc->dKp);
+    if (devnum) {
+        HCsr kidx = an.Kp;
+        for (size_t q = 0; q < kidx.val.size(); q++) kidx.val[q] = (double)(q + 1);
+        make_dist_dmat(dist_csr(kidx, *dm, c.rank, false), c.nranks, pc->dKp);
+    } else {
+        make_dist_dmat(dist_csr(an.Kp, *dm, c.rank, false), c.nranks, pc->dKp);
+    }
+    clk.lap("rank plan + upload");
+    if (devnum) {
+        auto add = [&](DBuf<double> &x, int src) {
+            if (!x.n) return;
+            Precond::VMap m;
+            m.dst = x.p, m.n = x.n, m.src = src;
+            vmap_capture(c, x.p, x.n, m.map);
+            pc->vmaps.push_back(std::move(m));
+        };
+        add(pc->dF.fval, 0), add(pc->dF.bval, 0), add(pc->dF.D, 1);
+        add(T.tf_val, 0), add(T.tb_val, 0), add(T.DT, 1), add(T.tk_val, 0), add(T.tr_val, 0), add(T.rec_v, 0);
+        add(pc->dKp.val, 2);
+        dldl_setup(pc->dl, an.sym, an.F0, {}, {}, {});
+        pc->kpg.upload(an.Kp.val);
+        dldl_numeric(c, pc->dl, pc->kpg.p, pc->dl.Lx.p, pc->dl.D.p);
+        pc->fill_vmaps();
+        CPK_HIP(hipStreamSynchronize(c.stream));
+        an.F0.Lx.clear(), an.F0.D.clear();  // the exported values come from the device (dl)
+        clk.lap("numeric factorization (device, whole system) + value maps");
+    }
     pc->Kp = std::move(an.Kp);
     pc->S = std::move(S);
     pc->F = std::move(an.F0);
@@ -248,6 +287,19 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     CPK_HIP(hipDeviceSynchronize());
     pc->ptime = an.seconds + std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return pc.release();
+}
+
+Precond *precond_create_dist(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22, const HCsr *Akry) {
+    const bool dev = !c.opts.host_factor;
+    Precond *pc = precond_create_dist(c, analyze(A11, B, C22, c.opts, dev), Akry);
+    pc->pattern_hash = pattern_hash(A11, B, C22);
+    if (dev) pc->dl.kp_from.upload(kp_value_sources(A11, B, C22));
+    return pc;
+}
+
+void Precond::fill_vmaps() {
+    for (const VMap &m : vmaps)
+        vmap_fill(*ctx, m.map.p, m.n, m.src == 0 ? dl.Lx.p : (m.src == 1 ? dl.D.p : kpg.p), m.dst);
 }
 
 uint64_t pattern_hash(const HCsr &A11, const HCsr &B, const HCsr &C22) {
@@ -275,10 +327,36 @@ Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22)
 }
 
 double precond_refactor(Precond &p, const DMat &A11, const DMat &B, const DMat &C22) {
-    if (p.dist || !p.dl.ready)
-        throw Error(CPK_ERR_UNSUPPORTED, "refactorization needs a single-GPU preconditioner with the device factorization");
+    if (!p.dl.ready)
+        throw Error(CPK_ERR_UNSUPPORTED, "refactorization needs the device factorization (engine option host_factor off)");
     auto t0 = std::chrono::steady_clock::now();
     Ctx &c = *p.ctx;
+    if (p.dist) {
+        // every rank refactors the whole system (as at construction) into scratch, then commits
+        // its maps' values; collective-free, so each rank's result is the single-GPU one
+        DBuf<double> kpv, Lx, D;
+        kpv.alloc(std::max<size_t>(p.kpg.n, 1));
+        Lx.alloc(p.dl.Lx.n);
+        D.alloc(p.dl.D.n);
+        dldl_assemble_kp(c, p.dl, A11.val.p, B.val.p, C22.val.p, kpv.p);
+        dldl_numeric(c, p.dl, kpv.p, Lx.p, D.p);
+        if (p.kpg.n) CPK_HIP(hipMemcpyAsync(p.kpg.p, kpv.p, p.kpg.bytes(), hipMemcpyDeviceToDevice, c.stream));
+        CPK_HIP(hipMemcpyAsync(p.dl.Lx.p, Lx.p, Lx.bytes(), hipMemcpyDeviceToDevice, c.stream));
+        CPK_HIP(hipMemcpyAsync(p.dl.D.p, D.p, D.bytes(), hipMemcpyDeviceToDevice, c.stream));
+        p.fill_vmaps();
+        if (!p.Kp.val.empty())
+            CPK_HIP(hipMemcpyAsync(p.Kp.val.data(), p.kpg.p, p.Kp.val.size() * sizeof(double), hipMemcpyDeviceToHost,
+                                   c.stream));
+        CPK_HIP(hipStreamSynchronize(c.stream));
+        // the shift's B' rows were built from the host Kp: rebuilt on next use (with the solvers
+        // whose captured graphs may reference them)
+        for (auto it = p.dist_ops.begin(); it != p.dist_ops.end();)
+            it = std::get<0>(it->first) == 'B' ? p.dist_ops.erase(it) : std::next(it);
+        p.solvers.clear();
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        p.ptime = s;
+        return s;
+    }
     // all or nothing: the new Kp and factor are formed in scratch buffers; a bad pivot throws
     // before anything the preconditioner holds (Kp, Kps, L, D, the sweep values) is touched
     DBuf<double> kpv, Lx, D;

@@ -341,3 +341,82 @@ def test_dist_plan_mismatch_fails_on_every_rank(option, value):
     assert all(m is not None and "plan of rank(s) 1 differs" in m for m in res), res
     # the same options on every rank: no error
     assert _run_ranks(2, work, {option: value}) == [None, None]
+
+
+def _new_values(S, seed):
+    """IPM-like new values with the same sparsity: G rescaled, B and C scaled."""
+    rng = np.random.default_rng(seed)
+    G2 = S["G"].copy()
+    G2.data = G2.data * rng.uniform(0.5, 2.0, G2.data.shape[0])
+    B2 = S["B"].copy()
+    B2.data = B2.data * rng.uniform(0.8, 1.25, B2.data.shape[0])
+    C2 = S["C"].copy()
+    C2.data = C2.data * 3.0
+    return G2, B2, C2
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_dist_refactor_equals_fresh_single_gpu(P):
+    """Distributed device factorization (opLDL2.m:81-82 rebuilt per IPM
+    iteration, reg_cpkrylov.m:128-132): every rank factors the whole system on its GPU and takes
+    its values through maps.  A refactorization with new G, B, C gives factors bit-identical to a
+    fresh single-GPU construction on those values, and every rank's M*z equals the oracle's
+    multiply with them; a cpminres solve after it matches the oracle."""
+    import cpkrylov_amd as cpk
+    S = _system("synthetic20k")
+    G2, B2, C2 = _new_values(S, 17)
+    z = np.random.default_rng(3).standard_normal(S["n"] + S["m"])
+    opts = dict(F.EXPROG_OPTS)
+    b = S["rhs"][:S["n"]]
+
+    def work(ctx, r):
+        M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+        M.nitref, M.force_itref = 1, True
+        y0 = M * z  # the caches built before the refactorization must not survive it
+        x0 = cpk.cpminres(b, S["Q"], S["C"], M, dict(opts, itmax=5))[0]
+        t = M.refactor(G2, B2, -C2)
+        y = M * z
+        x, yy, st = cpk.cpminres(b, S["Q"], S["C"], M, opts)[:3]
+        return y, M.export_factors() if r == 0 else None, x, st["niters"], st["residHistory"], t, y0, x0
+
+    res = _run_ranks(P, work)
+    ref = cpk.opLDL2(G2, B2, -C2)
+    L, D, perm = ref.export_factors()
+    Ld, Dd, permd = res[0][1]
+    assert np.array_equal(perm, permd) and np.array_equal(L.indptr, Ld.indptr) and np.array_equal(L.indices, Ld.indices)
+    assert np.array_equal(L.data, Ld.data) and np.array_equal(D, Dd)
+    Mo = O.LDL2(G2, B2, -C2, factors=(L, D, perm))
+    Mo.set(nitref=1.0, force_itref=1.0)
+    yo = Mo @ z
+    for y, *_ in res:
+        assert np.array_equal(y, yo), np.max(np.abs(y - yo))
+    xo, yyo, so = O.method("minres", b, S["Q"], S["C"], Mo, opts)
+    _, _, x, it, h, t, _, _ = res[0]
+    assert t > 0 and it == so["niters"]
+    assert len(h) == len(so["residHistory"]) and np.max(np.abs(h - so["residHistory"])) <= 1e-8 * so["residHistory"][0]
+    assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
+
+
+def test_dist_refactor_failure_leaves_preconditioner_intact():
+    """A zero pivot in a distributed refactorization fails on every rank and changes nothing:
+    M*z afterwards equals M*z before it, bit for bit."""
+    import cpkrylov_amd as cpk
+    S = _system("synthetic20k")
+    G0 = S["G"].copy()
+    G0.data = G0.data * 0.0
+    z = np.random.default_rng(4).standard_normal(S["n"] + S["m"])
+
+    def work(ctx, r):
+        M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+        M.nitref, M.force_itref = 1, True
+        y0 = M * z
+        try:
+            M.refactor(G0, S["B"], -S["C"])
+            err = None
+        except cpk.CpkError as e:
+            err = str(e)
+        return y0, M * z, err
+
+    for y0, y1, err in _run_ranks(2, work):
+        assert err is not None and "pivot" in err
+        assert np.array_equal(y0, y1)
