@@ -992,6 +992,69 @@ __device__ __forceinline__ void levels_owned(SweepLds &S, int nl, int nr, bool s
     }
 }
 
+// Forward levels of the persistent round-0 kernel (one 64-lane wave) with lane GROUPS per row.
+// Round 0's deep forward levels hold 1-4 rows of ~9-13 terms each (the S fill of a subtree's
+// top), which one lane per row walks two terms per pair of dependent LDS trips, while the other
+// lanes idle.  A level of nr <= 16 rows instead gives each row a group of G = 16, 8 or 4 lanes
+// (within one 16-lane DPP row): lane j of the group forms the product of the row's term c0 + j,
+// all at once, and the group's first lane subtracts them in the row's order, shifted to it one
+// lane at a time by DPP row_shl:1 (lanes past the row's end contribute 0.0 -- an exact no-op,
+// as the padded chunks of sweep_levels).  Wider levels keep one lane per row.  Same products,
+// same subtraction order: bit-identical.
+#ifndef CPK_LEVEL_GROUP
+#define CPK_LEVEL_GROUP 1
+#endif
+__device__ __forceinline__ double row_next_lane(double x) {  // lane i + 1 of its 16-lane row (15: 0)
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x101, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x101, 0xf, 0xf, true);
+    return __hiloint2double(hi, lo);
+}
+
+template <int CH>
+__device__ __forceinline__ void levels_grouped_fwd(SweepLds &S, int nl, bool skip_first, int lane) {
+    for (int l = skip_first ? 1 : 0; l < nl; l++) {
+        const int a = S.lv[l], z = S.lv[l + 1], nr = z - a;
+        if (nr > 16) {  // one lane per row, two terms per LDS round trip (sweep_levels)
+            for (int k = a + lane; k < z; k += kWave) {
+                const int e1 = S.p[k + 1];
+                double acc = S.w[k];
+                for (int e = S.p[k]; e < e1; e += CH) {
+                    int c[CH];
+                    double v[CH], x[CH];
+#pragma unroll
+                    for (int j = 0; j < CH; j++) c[j] = S.c[e + j], v[j] = S.v[e + j];
+#pragma unroll
+                    for (int j = 0; j < CH; j++) x[j] = S.w[c[j]];
+#pragma unroll
+                    for (int j = 0; j < CH; j++) acc -= (e + j < e1) ? v[j] * x[j] : 0.0;
+                }
+                S.w[k] = acc;
+            }
+        } else {
+            const int lg = nr <= 4 ? 4 : (nr <= 8 ? 3 : 2);  // log2 G
+            const int G = 1 << lg, g = lane >> lg, j = lane & (G - 1);
+            const bool row = g < nr;
+            const int k = a + (row ? g : 0);
+            const int e0 = S.p[k], e1 = row ? (int)S.p[k + 1] : e0;
+            double acc = S.w[k];
+            for (int c0 = 0;; c0 += G) {
+                const int e = e0 + c0 + j;
+                if (!__any(e0 + c0 < e1)) break;
+                const int ec = e < e1 ? e : e0;  // clamped: a valid entry of the block
+                const double xv = S.v[ec] * S.w[S.c[ec]];
+                double x = e < e1 ? xv : 0.0;
+                acc -= x;
+                for (int s = 1; s < G; s++) {
+                    x = row_next_lane(x);
+                    acc -= x;
+                }
+            }
+            if (row && j == 0) S.w[k] = acc;
+        }
+        asm volatile("" ::: "memory");  // one wave: LDS in issue order (levels_owned)
+    }
+}
+
 // Backward write-back of row k (schedule order) with value z:
 //   out != null: out[perm[k]] = z, or (ADD) base + z with base = ys[k] when ys is given (the
 //                previous solution kept in schedule order), else out[perm[k]];
@@ -1528,6 +1591,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
         // lane-owned rows for the backward sweep only: A/B at S10 (profiles/r03_level_ab_v2.txt),
         // backward 193.9 -> 186.7 us, but forward 211 -> 232 us and the fused forward 270 -> 286
         if (CPK_LEVEL_OWN && SPLIT == 1 && BWD) levels_owned<TPB, RPT, BWD, CPK_PIPE_CH>(S, nl, nr, skip0 != 0, tid);
+        else if (CPK_LEVEL_GROUP && SPLIT == 1 && TPB == kWave && !BWD) levels_grouped_fwd<CPK_PIPE_CH>(S, nl, skip0 != 0, tid);
         else sweep_levels<TPB, BWD, false, CPK_PIPE_CH, false, true>(S, nl, skip0 != 0, tid);
 #pragma unroll
         for (int j = 0; j < RPT; j++) {

@@ -369,6 +369,9 @@ def test_dist_refactor_equals_fresh_single_gpu(P):
     opts = dict(F.EXPROG_OPTS)
     b = S["rhs"][:S["n"]]
 
+    G3 = S["G"].copy()
+    G3.data = G3.data * 1.7  # a second refactorization, to values the solve converges on
+
     def work(ctx, r):
         M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
         M.nitref, M.force_itref = 1, True
@@ -376,8 +379,10 @@ def test_dist_refactor_equals_fresh_single_gpu(P):
         x0 = cpk.cpminres(b, S["Q"], S["C"], M, dict(opts, itmax=5))[0]
         t = M.refactor(G2, B2, -C2)
         y = M * z
+        f = M.export_factors() if r == 0 else None
+        M.refactor(G3, S["B"], -S["C"])
         x, yy, st = cpk.cpminres(b, S["Q"], S["C"], M, opts)[:3]
-        return y, M.export_factors() if r == 0 else None, x, st["niters"], st["residHistory"], t, y0, x0
+        return y, f, x, st["niters"], st["residHistory"], t, y0, x0
 
     res = _run_ranks(P, work)
     ref = cpk.opLDL2(G2, B2, -C2)
@@ -390,7 +395,11 @@ def test_dist_refactor_equals_fresh_single_gpu(P):
     yo = Mo @ z
     for y, *_ in res:
         assert np.array_equal(y, yo), np.max(np.abs(y - yo))
+    M3 = cpk.opLDL2(G3, S["B"], -S["C"])
+    Mo = O.LDL2(G3, S["B"], -S["C"], factors=M3.export_factors())
+    Mo.set(nitref=1.0, force_itref=1.0)
     xo, yyo, so = O.method("minres", b, S["Q"], S["C"], Mo, opts)
+    assert so["solved"]
     _, _, x, it, h, t, _, _ = res[0]
     assert t > 0 and it == so["niters"]
     assert len(h) == len(so["residHistory"]) and np.max(np.abs(h - so["residHistory"])) <= 1e-8 * so["residHistory"][0]
