@@ -200,14 +200,15 @@ def main():
     _lib.check(_lib.lib.cpk_profile_kernels(ctx.h, A.h, Cm.h, M.h, args.profile_reps, C.byref(prof)))
     gbs = lambda byts, ms: byts / (ms * 1e-3) / 1e9  # noqa: E731
     # the dominant kernel: the triangular sweeps of one LDL' solve (forward + backward, every
-    # round: sptrsv_pipe_kernel for round 0 and sptrsv_upper_kernel above), 4 per M*z
+    # round: sptrsv_pipe_kernel for round 0, sptrsv_upper_kernel above, sptrsv_last_kernel for
+    # the last round's forward + backward), 2 per M*z
     sweep_ms, sweep_bytes = prof.fwd_ms + prof.bwd_ms, prof.fwd_bytes + prof.bwd_bytes
     achieved = gbs(sweep_bytes, sweep_ms)
-    roofline = {"bound": "hbm", "kernel": "sptrsv_pipe_kernel + sptrsv_upper_kernel: one LDL' solve "
-                                          "(forward + backward sweep, all rounds)",
+    roofline = {"bound": "hbm", "kernel": "sptrsv_pipe_kernel + sptrsv_upper_kernel + sptrsv_last_kernel: one "
+                                          "LDL' solve (forward + backward sweep, all rounds)",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "bytes_per_launch": sweep_bytes,
-                "avg_ms": round(sweep_ms, 5), "launches": 2 * int(prof.fwd_launches)}
+                "avg_ms": round(sweep_ms, 5), "launches": int(prof.fwd_launches) + int(prof.bwd_launches)}
     # the metric's "SpMV GB/s": the saddle-point SpMV inside every M*z (refinement residual)
     spmv_achieved = gbs(prof.resid_bytes, prof.resid_ms)
     spmv_roofline = {"kernel": "spmv_stream<EpiResidSched> (r = x - P'Kp P y, all in schedule order)",
@@ -217,7 +218,7 @@ def main():
     kernels = {k: {"avg_ms": round(getattr(prof, k + "_ms"), 5), "bytes": getattr(prof, k + "_bytes"),
                    "GBps": round(gbs(getattr(prof, k + "_bytes"), getattr(prof, k + "_ms")), 1)}
                for k in ("spmv", "resid", "fwd", "bwd", "apply")}
-    kernels["fwd"]["launches"] = kernels["bwd"]["launches"] = int(prof.fwd_launches)
+    kernels["fwd"]["launches"], kernels["bwd"]["launches"] = int(prof.fwd_launches), int(prof.bwd_launches)
     if prof.fwd_resid_ms > 0:  # the refinement's residual + forward sweep, fused (launch_sptrsv_fwd_resid)
         kernels["fwd_resid"] = {"avg_ms": round(prof.fwd_resid_ms, 5), "bytes": prof.fwd_resid_bytes,
                                 "GBps": round(gbs(prof.fwd_resid_bytes, prof.fwd_resid_ms), 1),
@@ -387,7 +388,7 @@ def pmc_probe(args):
     print(json.dumps({"resid_bytes": prof.resid_bytes, "spmv_bytes": prof.spmv_bytes,
                       "fwd_bytes": prof.fwd_bytes, "bwd_bytes": prof.bwd_bytes,
                       "fwd_resid_bytes": prof.fwd_resid_bytes,
-                      "rounds": int(prof.fwd_launches)}), flush=True)
+                      "fwd_launches": int(prof.fwd_launches), "bwd_launches": int(prof.bwd_launches)}), flush=True)
 
 
 def pmc_traffic(args):
@@ -424,33 +425,35 @@ def pmc_traffic(args):
             counts[ctr] = rows
         kib = 1024.0
 
-        def per_launch(name_pred, sel):
+        def per_call(name_pred, sel, calls):
+            """bytes per call: the selected launches' counters summed, divided by the calls"""
             f = [float(q["Counter_Value"]) for q in counts["FETCH_SIZE"] if name_pred(q["Kernel_Name"])]
             w = [float(q["Counter_Value"]) for q in counts["WRITE_SIZE"] if name_pred(q["Kernel_Name"])]
             f, w = sel(f), sel(w)
             if not f or len(f) != len(w):
                 return None
-            fb, wb = 2.0 * kib * sum(f) / len(f), kib * sum(w) / len(w)
-            return {"fetch": round(fb), "write": round(wb), "bytes": round(fb + wb), "launches": len(f)}
+            fb, wb = 2.0 * kib * sum(f) / calls, kib * sum(w) / calls
+            return {"fetch": round(fb), "write": round(wb), "bytes": round(fb + wb), "launches": len(f) // calls}
 
         spmv = lambda nm: nm.split("<")[0].split("(")[0].strip().endswith("spmv_stream")  # noqa: E731
         # launch order of cpk_profile_kernels: (1 + reps) Krylov SpMVs, (1 + reps) residual SpMVs
-        R = probe["rounds"]
-        out["resid"] = per_launch(spmv, lambda v: v[reps + 2:2 * reps + 2])
-        out["spmv"] = per_launch(spmv, lambda v: v[1:reps + 1])
-        # sweeps: (1 + reps) x R launches each; sum the rounds of one sweep
-        sweep = lambda nm: "sptrsv" in nm  # noqa: E731  (round-0 pipe kernel included)
-        for k, lo in (("fwd", R), ("bwd", R * (reps + 1) + R)):
-            pl = per_launch(sweep, lambda v, lo=lo: v[lo:lo + R * reps])
-            if pl:
-                pl = {kk: (vv * R if kk != "launches" else vv // R) for kk, vv in pl.items()}
-            out[k] = pl
+        out["resid"] = per_call(spmv, lambda v: v[reps + 2:2 * reps + 2], reps)
+        out["spmv"] = per_call(spmv, lambda v: v[1:reps + 1], reps)
+        # sweeps (round-0 pipe, upper-round and fused last-round kernels): (1 + reps) forward
+        # sweeps of Lf launches, then (1 + reps) pairs of Lf + Lb launches (the forward again,
+        # then the backward, whose Lb launches include the fused last round when there is one)
+        Lf, Lb = probe["fwd_launches"], probe["bwd_launches"]
+        sweep = lambda nm: "sptrsv" in nm  # noqa: E731
+        out["fwd"] = per_call(sweep, lambda v: v[Lf:Lf * (reps + 1)], reps)
+        p0 = Lf * (reps + 1) + (Lf + Lb)  # the pairs after the warm-up pair
+
+        def bwd_of_pairs(v):
+            return [x for i in range(reps) for x in v[p0 + i * (Lf + Lb) + Lf:p0 + (i + 1) * (Lf + Lb)]]
+        out["bwd"] = per_call(sweep, bwd_of_pairs, reps)
         if probe.get("fwd_resid_bytes", 0) > 0:
-            # the fused residual + forward sweep: the last reps x R sweep launches of the profile
-            pl = per_launch(sweep, lambda v: v[len(v) - R * reps:])
-            if pl:
-                pl = {kk: (vv * R if kk != "launches" else vv // R) for kk, vv in pl.items()}
-            out["fwd_resid"] = pl
+            # the fused residual + forward sweep (all rounds, nothing deferred): the last reps calls
+            R = Lb
+            out["fwd_resid"] = per_call(sweep, lambda v: v[len(v) - R * reps:], reps)
         for k in ("resid", "spmv", "fwd", "bwd", "fwd_resid"):
             if out.get(k):
                 out[k]["algorithmic"] = probe[k + "_bytes"]

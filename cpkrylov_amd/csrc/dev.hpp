@@ -98,6 +98,7 @@ struct EngineOpts {
     bool no_piggy = false;        // no_piggy:           cpminres alpha by its own allreduce
     bool no_halo_merge = false;   // no_halo_merge:      cpminres beta by its own allreduce
     bool no_graph = false;        // no_graph:           no hipGraph capture of iterations
+    bool no_fuse_last = false;    // no_fuse_last:       the last sweep round as two launches
     bool dist_graph = true;       // dist_graph:         capture collectives in the graphs
     int batch = 0;                // batch:              fixed iterations per graph (0: adaptive)
     bool profile_fwd_nolevels = false;  // profile_fwd_nolevels: diagnostic (cpk_profile_kernels)
@@ -168,6 +169,7 @@ struct DFactor {
     bool no_col16 = false;  // no int16 round-0 forward columns (set before make_dfactor)
     // engine options of the preconditioner's context when it was built (launch-time paths)
     bool no_fused_resid = false, fused_tail_launch = false;
+    bool fuse_last = false;  // single GPU, no entries outside the factor: the last round fwd + bwd in one launch
     int64_t round0_rows = -1;  // round 0 is the rows [0, round0_rows) (-1: not a leading row range)
     std::vector<int32_t> hmeta;  // host copy of meta
     // round-0 blocks assigned to the persistent launch's workgroups by modelled cost (plan_round0),
@@ -215,14 +217,25 @@ void launch_spmv_colmask(Ctx &c, const DMat &A, int64_t col_min, const double *x
 // forward sweep w = L \ (P' * xin), backward sweep out (=|+=) P * (L' \ (D \ w))
 // sched_in: xin is already in schedule order (no perm gather, no negation)
 // xs (optional): also store the signed input in schedule order (the refinement residual's x)
+// the forward input of a deferred last round (launch_sptrsv_fwd's defer, launch_sptrsv_bwd's last)
+struct FwdIn {
+    const double *xin = nullptr;
+    int64_t neg_from = 0;
+    int sched_in = 0;
+    double *xs = nullptr;
+    bool valid = false;
+};
+bool fuse_last_ok(const DFactor &F);
+// defer (optional): the last round is left to the backward sweep (sptrsv_last_kernel solves it
+// forward and backward in one launch); *defer then says how, for launch_sptrsv_bwd's last
 void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                       const int *active, bool sched_in = false, double *xs = nullptr);
+                       const int *active, bool sched_in = false, double *xs = nullptr, FwdIn *defer = nullptr);
 // diagnostic: the forward sweep without its level phase (staging + write-back only)
 void launch_sptrsv_fwd_diag(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w);
 // out == null: the solution stays in schedule order in w (and with add, ys += it in place);
 // add with ys: out = P * (ys + solution), ys the previous solution in schedule order
 void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
-                       const int *active, double *ys = nullptr);
+                       const int *active, double *ys = nullptr, const FwdIn *last = nullptr);
 // r = xin(perm) - A*y with A = P'*Kp*P in schedule order (rows and columns), y in schedule
 // order (perm null: xin is the signed input already in schedule order, see launch_sptrsv_fwd);
 // order; each row sums its entries in Kp's column order, so r(k) equals row perm(k) of the
@@ -234,7 +247,7 @@ void launch_spmv_resid_sched(Ctx &c, const DMat &A, const int32_t *perm, const d
 // round0_rows) through the residual SpMV.  Bit-identical to launch_spmv_resid_sched +
 // launch_sptrsv_fwd(sched_in).  False (nothing launched): no matching configuration.
 bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const int32_t *tail_blk, int64_t tail_nblk,
-                             const double *xs, const double *y, double *r, const int *run);
+                             const double *xs, const double *y, double *r, const int *run, FwdIn *defer = nullptr);
 int debug_pipe_stamps(uint64_t *out, int npairs);  // diagnostic build only (CPK_PIPE_STAMPS)
 int64_t debug_blk_cycles(uint64_t *out, int64_t n);  // likewise: [4][1 << 17] per-block cycles
 // Kps row blocks of the rows [row0, nrows) (A.blk with a boundary at row0)

@@ -1298,6 +1298,149 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
     }
 }
 
+// The last round's forward and backward sweeps in one launch (single GPU).  The sweeps meet at
+// the top of the tree: forward rounds 0 .. R-1, then backward R-1 .. 0, so the last round's
+// blocks are solved forward and at once backward; a block holds whole subtrees of the last
+// remaining tree, so its backward terms stay inside it.  One workgroup per block stages the
+// forward and backward entries together (every independent load in flight at once), runs the
+// forward fold and levels, divides by D in LDS and runs the backward levels -- the operations of
+// sptrsv_upper_kernel forward, its write-back and w / D, and sptrsv_upper_kernel backward, in
+// that order: bit-identical, one launch and one staging round trip fewer per solve.
+template <int TPB, int RPU, int EPU, bool ADD>
+__global__ __launch_bounds__(TPB) void sptrsv_last_kernel(
+    int64_t blk0, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
+    const uint32_t *__restrict__ fptr, const int32_t *__restrict__ fcol, const double *__restrict__ fval,
+    const uint32_t *__restrict__ bptr, const int32_t *__restrict__ bcol, const double *__restrict__ bval,
+    const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
+    int sched_in, double *xs, double *w, double *out, const int *run, const int *active, double *ys) {
+    constexpr int R = RPU * TPB, CAP = EPU * TPB;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (skip(run, active)) return;
+    const BlkMeta m = meta[blk0 + blockIdx.x];
+    const int r0 = m.r0, r1 = m.r1, nr = r1 - r0, nl = m.l1 - m.l0;
+    const int nef = m.fe1 - m.fe0, neb = m.be1 - m.be0;
+    const int tid = threadIdx.x;
+    SweepLds S(smem, R, CAP);
+    uint32_t qf[RPU], qb[RPU];
+    int32_t sp[RPU], dp[RPU];
+    double a[RPU], d[RPU];
+    int32_t cf[EPU], cb[EPU];
+    double vf[EPU], vb[EPU], g[EPU];
+#pragma unroll
+    for (int j = 0; j < RPU; j++) {
+        const int i = tid + j * TPB, rr = r0 + (i < nr ? i : nr - 1);
+        qf[j] = fptr[rr], qb[j] = bptr[rr], d[j] = D[rr];
+        sp[j] = sched_in ? rr : perm[rr];
+        dp[j] = out ? perm[rr] : rr;
+    }
+#pragma unroll
+    for (int u = 0; u < EPU; u++) {
+        const int e = tid + u * TPB;
+        const uint32_t ef = (uint32_t)m.fe0 + (uint32_t)(e < nef ? e : 0), eb = (uint32_t)m.be0 + (uint32_t)(e < neb ? e : 0);
+        cf[u] = __builtin_nontemporal_load(fcol + ef), vf[u] = __builtin_nontemporal_load(fval + ef);
+        cb[u] = __builtin_nontemporal_load(bcol + eb), vb[u] = __builtin_nontemporal_load(bval + eb);
+    }
+    for (int l = tid; l <= nl; l += TPB) S.lv[l] = (int16_t)(lvl_row[m.l0 + l] - r0);
+#pragma unroll
+    for (int j = 0; j < RPU; j++) a[j] = xin[sp[j]];
+#pragma unroll
+    for (int u = 0; u < EPU; u++) g[u] = w[(cf[u] >= r0 && cf[u] < r1) ? r0 : cf[u]];
+    // ---- forward (sptrsv_upper_kernel<..., false, false>)
+#pragma unroll
+    for (int j = 0; j < RPU; j++) {
+        const int i = tid + j * TPB;
+        if (i < nr) {
+            S.p[i] = (int16_t)(qf[j] - (uint32_t)m.fe0);
+            S.w[i] = (sp[j] >= neg_from) ? -a[j] : a[j];
+            if (xs) xs[r0 + i] = S.w[i];
+        }
+    }
+    if (tid == 0) S.p[nr] = (int16_t)nef, S.w[R] = 1.0;
+    if (tid < kSweepPad) S.c[nef + tid] = (int16_t)R;
+#pragma unroll
+    for (int u = 0; u < EPU; u++) {
+        const int e = tid + u * TPB;
+        if (e < nef) {
+            const bool local = cf[u] >= r0 && cf[u] < r1;
+            S.c[e] = local ? (int16_t)(cf[u] - r0) : (int16_t)R;
+            S.v[e] = local ? vf[u] : vf[u] * g[u];
+        }
+    }
+    __syncthreads();
+    fold_prefix<TPB, 1>(S, nr, -1, R);
+    if (tid < kWave) sweep_levels<kWave, false, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
+    __syncthreads();
+    // ---- backward (sptrsv_upper_kernel<..., true, ADD>): w / D, the entries, fold, levels; the
+    // backward terms of a last-round block are its own rows (the 1.0 slot path is kept for any other)
+#pragma unroll
+    for (int u = 0; u < EPU; u++) g[u] = (tid + u * TPB < neb && (cb[u] < r0 || cb[u] >= r1)) ? w[cb[u]] : 0.0;
+#pragma unroll
+    for (int j = 0; j < RPU; j++) {
+        const int i = tid + j * TPB;
+        if (i < nr) {
+            S.w[i] = S.w[i] / d[j];
+            S.p[i] = (int16_t)(qb[j] - (uint32_t)m.be0);
+        }
+    }
+    if (tid == 0) S.p[nr] = (int16_t)neb;
+    if (tid < kSweepPad) S.c[neb + tid] = (int16_t)R;
+#pragma unroll
+    for (int u = 0; u < EPU; u++) {
+        const int e = tid + u * TPB;
+        if (e < neb) {
+            const bool local = cb[u] >= r0 && cb[u] < r1;
+            S.c[e] = local ? (int16_t)(cb[u] - r0) : (int16_t)R;
+            S.v[e] = local ? vb[u] : vb[u] * g[u];
+        }
+    }
+    __syncthreads();
+    fold_prefix<TPB, 1>(S, nr, -1, R);
+    if (tid < kWave) sweep_levels<kWave, true, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RPU; j++) {
+        const int i = tid + j * TPB;
+        if (i < nr) {
+            const double z = S.w[i];
+            w[r0 + i] = z;
+            if (out) out[dp[j]] = ADD ? (ys ? ys[r0 + i] : out[dp[j]]) + z : z;
+            else if (ADD) ys[r0 + i] = ys[r0 + i] + z;
+        }
+    }
+}
+
+// the last round fused (fwd + bwd) when it is an upper round whose blocks fit sptrsv_last_kernel
+bool fuse_last_ok(const DFactor &F) {
+    const int64_t R = (int64_t)F.round_ptr.size() - 1;
+    return F.fuse_last && R >= 2 && F.sweep_threads[1] == 512 && F.sweep_rows[1] <= 1024 && F.sweep_cap[1] <= 4096 &&
+           (int64_t)F.round_fits.size() >= R && F.round_fits[R - 1] && !F.no_upper;
+}
+
+static void launch_last(Ctx &c, const DFactor &F, const FwdIn &in, double *w, double *out, bool add,
+                        const int *run, const int *active, double *ys) {
+    constexpr int TPB = 512, RPU = 2, EPU = 8;
+    const int64_t R = (int64_t)F.round_ptr.size() - 1;
+    const int64_t b0 = F.round_ptr[R - 1], nb = F.round_ptr[R] - b0;
+    if (!nb) return;
+    const size_t lds = sweep_lds_bytes(RPU * TPB, EPU * TPB);
+    static const bool lds_ok = lds <= 64 * 1024 ||
+        (hipFuncSetAttribute((const void *)sptrsv_last_kernel<TPB, RPU, EPU, false>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
+         hipFuncSetAttribute((const void *)sptrsv_last_kernel<TPB, RPU, EPU, true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess);
+    if (!lds_ok) throw Error(CPK_ERR_HIP, "sptrsv_last_kernel: LDS image not admitted");
+    const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
+    if (add)
+        hipLaunchKernelGGL((sptrsv_last_kernel<TPB, RPU, EPU, true>), dim3((unsigned)nb), dim3(TPB), lds, c.stream, b0,
+                           meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p,
+                           in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys);
+    else
+        hipLaunchKernelGGL((sptrsv_last_kernel<TPB, RPU, EPU, false>), dim3((unsigned)nb), dim3(TPB), lds, c.stream, b0,
+                           meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p,
+                           in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys);
+    CPK_HIP(hipGetLastError());
+}
+
 template <int TPB, int RPU, int EPU>
 static bool upper_round_t(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add, const double *xin,
                           int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in,
@@ -1855,8 +1998,12 @@ static inline unsigned det_grid(int64_t n) { return (unsigned)std::min<int64_t>(
 
 template <int MODE>
 static void fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                    const int *active, int sched_in, double *xs = nullptr, int64_t rfirst = 0) {
-    const int64_t R = (int64_t)F.round_ptr.size() - 1;
+                    const int *active, int sched_in, double *xs = nullptr, int64_t rfirst = 0, FwdIn *defer = nullptr) {
+    int64_t R = (int64_t)F.round_ptr.size() - 1;
+    if (defer && MODE == 0 && fuse_last_ok(F)) {  // the last round runs with the backward sweep
+        *defer = FwdIn{xin, neg_from, sched_in, xs, true};
+        R -= 1;
+    }
     if (F.ndet > 0 && !(sched_in && xin == w) && rfirst == 0)  // in place in schedule order: already there
         hipLaunchKernelGGL(det_fwd_kernel, dim3(det_grid(F.ndet)), dim3(kBlock), 0, c.stream, F.ndet, F.perm.p, xin,
                            neg_from, sched_in, w, run, active);
@@ -1884,10 +2031,11 @@ void launch_sptrsv_fwd_diag(Ctx &c, const DFactor &F, const double *xin, int64_t
 }
 
 void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                       const int *active, bool sched_in, double *xs) {
+                       const int *active, bool sched_in, double *xs, FwdIn *defer) {
     // schedule-order input: no perm gather and no negation (neg_from applies to original indices)
     if (xs && F.ndet > 0) throw Error(CPK_ERR_UNSUPPORTED, "internal: input capture with detached rows");
-    fwd_all<0>(c, F, xin, sched_in ? INT64_MAX : neg_from, w, run, active, sched_in ? 1 : 0, xs);
+    if (defer) defer->valid = false;
+    fwd_all<0>(c, F, xin, sched_in ? INT64_MAX : neg_from, w, run, active, sched_in ? 1 : 0, xs, 0, defer);
 }
 
 // diagnostic: the per-workgroup stamps of the last round-0 launch (0 unless built with
@@ -1927,7 +2075,8 @@ void make_tail_blk(const DMat &A, int64_t row0, DBuf<int32_t> &blk, int64_t &nbl
 }
 
 bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const int32_t *tail_blk, int64_t tail_nblk,
-                             const double *xs, const double *y, double *r, const int *run) {
+                             const double *xs, const double *y, double *r, const int *run, FwdIn *defer) {
+    if (defer) defer->valid = false;
     const bool off = F.no_fused_resid;  // A/B switch: separate residual SpMV
     if (off || tail_nblk < 0 || !F.pipelined || F.ndet != 0 || F.round0_rows < 0 || F.fcol16.n == 0 ||
         F.round_ptr.size() < 2 || Kps.halo())
@@ -1945,14 +2094,18 @@ bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const in
                            Kps.col.p, Kps.val.p, tail_blk, tail_nblk, y, (int64_t)0, e, (const double *)nullptr,
                            (int64_t)0);
     }
-    fwd_all<0>(c, F, r, INT64_MAX, r, run, nullptr, 1, nullptr, 1);
+    fwd_all<0>(c, F, r, INT64_MAX, r, run, nullptr, 1, nullptr, 1, defer);
     return true;
 }
 
 void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
-                       const int *active, double *ys) {
+                       const int *active, double *ys, const FwdIn *last) {
     if (!out && add && !ys) throw Error(CPK_ERR_ARGS, "internal: accumulating backward sweep without a base");
-    const int64_t R = (int64_t)F.round_ptr.size() - 1;
+    int64_t R = (int64_t)F.round_ptr.size() - 1;
+    if (last && last->valid) {  // the deferred last round, forward and backward (sptrsv_last_kernel)
+        launch_last(c, F, *last, w, out, add, run, active, ys);
+        R -= 1;
+    }
     for (int64_t r = R - 1; r >= 0; r--) {
         if (r == 0 && pipe_round0(c, F, true, add, nullptr, 0, w, out, run, active, 0, ys, nullptr)) continue;
         if (r > 0 && upper_round(c, F, r, true, add, nullptr, 0, w, out, run, active, 0, ys, nullptr)) continue;

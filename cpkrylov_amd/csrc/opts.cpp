@@ -66,6 +66,7 @@ const BoolOpt kBool[] = {
     {"no_piggy", &EngineOpts::no_piggy},
     {"no_halo_merge", &EngineOpts::no_halo_merge},
     {"no_graph", &EngineOpts::no_graph},
+    {"no_fuse_last", &EngineOpts::no_fuse_last},
     {"dist_graph", &EngineOpts::dist_graph},
     {"profile_fwd_nolevels", &EngineOpts::profile_fwd_nolevels},
 };

@@ -73,6 +73,7 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
         pc->dF.sweep_threads[i] = an.sweep.threads[i];
     pc->dF.pipelined = !c.opts.no_pipe, pc->dF.no_upper = c.opts.no_upper, pc->dF.no_col16 = c.opts.no_col16;
     pc->dF.no_fused_resid = c.opts.no_fused_resid, pc->dF.fused_tail_launch = c.opts.fused_tail_launch;
+    pc->dF.fuse_last = !c.opts.no_fuse_last;  // single GPU: no entries outside the factor
     {
         const std::vector<int64_t> key(pc->S.order.begin(), pc->S.order.end());
         if (an.device_numeric) {
@@ -388,12 +389,13 @@ double precond_refactor(Precond &p, const DMat &A11, const DMat &B, const DMat &
 void Precond::ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run,
                         const int *act, const double *piggy_src) {
     Ctx &c = *ctx;
-    launch_sptrsv_fwd(c, dF, xin, neg_from, w.p, run, act);
+    FwdIn last;  // single GPU: the last round forward + backward in one launch (sptrsv_last_kernel)
+    launch_sptrsv_fwd(c, dF, xin, neg_from, w.p, run, act, false, nullptr, dist ? nullptr : &last);
     if (dist) {
         launch_sep_exchange(c, sep, w.p, xin, neg_from, piggy_src);
         launch_sep_solve(c, sep, w.p + nsub, y, add, run, act);
     }
-    launch_sptrsv_bwd(c, dF, w.p, y, add, run, act);
+    launch_sptrsv_bwd(c, dF, w.p, y, add, run, act, nullptr, &last);
 }
 
 void Precond::set_handle(bool on) {
@@ -418,9 +420,10 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
     } else if (nitref >= 1 && force_itref != 0 && sched_path()) {
         // y = op.LDL * x kept in schedule order (w) for the refinement below: no scatter; the
         // forward sweep also leaves the signed input in schedule order (xs) for the residual
-        launch_sptrsv_fwd(c, dF, x, neg_from, w.p, run, nullptr, false, xs.n ? xs.p : nullptr);
+        FwdIn last;
+        launch_sptrsv_fwd(c, dF, x, neg_from, w.p, run, nullptr, false, xs.n ? xs.p : nullptr, &last);
         have_xs = xs.n > 0;
-        launch_sptrsv_bwd(c, dF, w.p, nullptr, false, run, nullptr);
+        launch_sptrsv_bwd(c, dF, w.p, nullptr, false, run, nullptr, nullptr, &last);
     } else {
         // y = op.LDL * x   (opLDL2.m:165-167); the residual-update branch subtracts the zero
         // state of a value object and its SpMVs are dead: skipped
@@ -434,12 +437,13 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
         for (int64_t s = 0; s < steps; s++) {
             // r = x - op.A*y; the refinement solve runs in place on r (each row reads its own
             // input before it writes, detached rows keep theirs); y += op.LDL*r
-            if (!(have_xs && launch_sptrsv_fwd_resid(c, dF, dKps, kps_tail_blk.p, kps_tail_nblk, xs.p, w.p, r.p, run))) {
+            FwdIn last;
+            if (!(have_xs && launch_sptrsv_fwd_resid(c, dF, dKps, kps_tail_blk.p, kps_tail_nblk, xs.p, w.p, r.p, run, &last))) {
                 if (have_xs) launch_spmv_resid_sched(c, dKps, nullptr, xs.p, 0, w.p, r.p, run);
                 else launch_spmv_resid_sched(c, dKps, dF.perm.p, x, neg_from, w.p, r.p, run);
-                launch_sptrsv_fwd(c, dF, r.p, N, r.p, run, nullptr, true);
+                launch_sptrsv_fwd(c, dF, r.p, N, r.p, run, nullptr, true, nullptr, &last);
             }
-            launch_sptrsv_bwd(c, dF, r.p, s + 1 == steps ? y : nullptr, true, run, nullptr, w.p);
+            launch_sptrsv_bwd(c, dF, r.p, s + 1 == steps ? y : nullptr, true, run, nullptr, w.p, &last);
         }
         return;
     }

@@ -2002,17 +2002,26 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
         out->resid_ms = timeit([&]() { launch_spmv_resid(c, M.dKp, x.p, M.n, y.p, z.p, nullptr, nullptr); });
         out->resid_bytes = 12.0 * M.dKp.nnz + 4.0 * (Nn + 1) + 8.0 * Nn /*y*/ + 8.0 * Nn /*x*/ + 8.0 * Nn /*r*/;
     }
+    // one LDL solve as the apply runs it: the forward sweep (its last round deferred when fused),
+    // then the pair forward + backward; the backward's time is the pair's minus the forward's.
+    // Launch order (bench.py's PMC parser): (1 + reps) forward sweeps, (1 + reps) pairs
+    FwdIn last;
     if (c.opts.profile_fwd_nolevels)
         out->fwd_ms = timeit([&]() { launch_sptrsv_fwd_diag(c, M.dF, x.p, M.n, M.w.p); });
     else
-        out->fwd_ms = timeit([&]() { launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr); });
+        out->fwd_ms = timeit([&]() { launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr, false, nullptr, &last); });
     out->fwd_bytes = 12.0 * l - 2.0 * (double)M.dF.nnz16 + 4.0 * (Nn + 1) + 4.0 * Nn /*perm*/ + 8.0 * Nn /*x*/ + 8.0 * Nn /*w*/;
-    out->bwd_ms = timeit([&]() { launch_sptrsv_bwd(c, M.dF, M.w.p, z.p, false, nullptr, nullptr); });
+    const double pair_ms = timeit([&]() {
+        launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr, false, nullptr, &last);
+        launch_sptrsv_bwd(c, M.dF, M.w.p, z.p, false, nullptr, nullptr, nullptr, &last);
+    });
+    out->bwd_ms = pair_ms - out->fwd_ms;
     out->bwd_bytes = 12.0 * l + 4.0 * (Nn + 1) + 4.0 * Nn + 8.0 * Nn /*D*/ + 8.0 * Nn /*w in*/ + 8.0 * Nn /*w out*/ +
                      8.0 * Nn /*y*/;
     out->apply_ms = timeit([&]() { M.apply(x.p, M.n, z.p, nullptr); });
     out->apply_bytes = M.apply_bytes();
     out->fwd_launches = out->bwd_launches = (int64_t)M.dF.round_ptr.size() - 1;
+    if (last.valid) out->fwd_launches -= 1;  // the last round: one launch inside the backward count
     out->fwd_resid_ms = out->fwd_resid_bytes = 0;
     if (M.sched_path() && M.xs.n &&
         launch_sptrsv_fwd_resid(c, M.dF, M.dKps, M.kps_tail_blk.p, M.kps_tail_nblk, x.p, y.p, z.p, nullptr)) {

@@ -357,3 +357,26 @@ def test_precond_apply_fused_residual_tail_launch(gpu_ctx, name):
     Mo = O.LDL2(G, B, -C, factors=(L, D, perm))
     Mo.set(nitref=1.0, force_itref=1.0)
     assert np.array_equal(ys[0], ys[1]) and np.array_equal(ys[0], Mo @ z)
+
+
+@pytest.mark.parametrize("name", ["cvxqp1_m", "cvxqp2_s", "synthetic"])
+@pytest.mark.parametrize("props", [dict(nitref=0), dict(nitref=1, force_itref=True), dict(nitref=2, force_itref=True),
+                                   dict(nitref=2, force_itref=False, itref_tol=1e-30)])
+def test_precond_apply_fused_last_round(gpu_ctx, name, props):
+    """The last sweep round forward and backward in one launch (sptrsv_last_kernel) against two
+    launches (engine option no_fuse_last) and the oracle, in every apply path: plain, forced
+    refinement in schedule order with the fused residual, data-dependent refinement."""
+    import cpkrylov_amd as cpk
+    G, B, C = _system_gbc(name)
+    z = np.random.default_rng(31).standard_normal(G.shape[0] + B.shape[0])
+    ys = []
+    for off in (False, True):
+        with cpk.engine_options(no_fuse_last=off):
+            M = cpk.opLDL2(G, B, -C)
+        for k, v in props.items():
+            setattr(M, k, v)
+        ys.append(M * z)
+    L, D, perm = M.export_factors()
+    Mo = O.LDL2(G, B, -C, factors=(L, D, perm))
+    Mo.set(**{k: float(v) for k, v in props.items()})
+    assert np.array_equal(ys[0], ys[1]) and np.array_equal(ys[0], Mo @ z)
