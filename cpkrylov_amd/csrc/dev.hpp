@@ -145,7 +145,7 @@ void make_dmat(const HCsr &a, DMat &d);
 struct DistCsr;
 void make_dist_dmat(const DistCsr &a, int nranks, DMat &d);
 // allgather the halo of x (local vector) into A.rbuf
-void launch_halo(Ctx &c, const DMat &A, const double *x);
+void launch_halo(Ctx &c, const DMat &A, const double *x, bool packed = false);
 
 // HBM-resident factor + sweep schedule (rows in schedule order).
 struct DFactor {
@@ -206,17 +206,28 @@ void plan_round0(Ctx &c, DFactor &d, const int64_t *kps_ptr);
 // Flags: a kernel is a no-op when *run == 0 or *active == 0 (either pointer may be null).
 // neg_from: input entries with index >= neg_from are negated on load (the reference's [u; -t]).
 void launch_spmv(Ctx &c, const DMat &A, const double *x, double *y, const int *run);
-// r = xin - A*y
+// r = xin - A*y  (halo_packed: y's halo payload is already in A.sbuf, allgather only)
 void launch_spmv_resid(Ctx &c, const DMat &A, const double *xin, int64_t neg_from, const double *y, double *r,
-                       const int *run, const int *active);
+                       const int *run, const int *active, bool halo_packed = false);
 // r = xin - A*y, and *active = (||r|| >= tol*||xin||) computed on device (opLDL2.m:176-177,183)
 void launch_spmv_resid_norm(Ctx &c, const DMat &A, const double *xin, int64_t neg_from, const double *y, double *r,
-                            double tol, int *active_out, const int *run, const int *active);
+                            double tol, int *active_out, const int *run, const int *active, bool halo_packed = false);
 // y = A*x restricted to columns >= col_min (B'*v from the first n rows of Kp)
 void launch_spmv_colmask(Ctx &c, const DMat &A, int64_t col_min, const double *x, double *y, const int *run);
 // forward sweep w = L \ (P' * xin), backward sweep out (=|+=) P * (L' \ (D \ w))
 // sched_in: xin is already in schedule order (no perm gather, no negation)
 // xs (optional): also store the signed input in schedule order (the refinement residual's x)
+// Distributed payloads packed by the sweeps' write-back (kernels.hip: PackArgs users)
+struct PackArgs {
+    const int32_t *slot = nullptr;
+    double *buf = nullptr;
+    const int32_t *tdof = nullptr;
+    int ntdof = 0, nsend = 0, kt_data = 0;
+    const double *x = nullptr;
+    int64_t neg_from = 0;
+    const double *piggy = nullptr;
+};
+
 // the forward input of a deferred last round (launch_sptrsv_fwd's defer, launch_sptrsv_bwd's last)
 struct FwdIn {
     const double *xin = nullptr;
@@ -228,14 +239,19 @@ struct FwdIn {
 bool fuse_last_ok(const DFactor &F);
 // defer (optional): the last round is left to the backward sweep (sptrsv_last_kernel solves it
 // forward and backward in one launch); *defer then says how, for launch_sptrsv_bwd's last
-void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                       const int *active, bool sched_in = false, double *xs = nullptr, FwdIn *defer = nullptr);
+// pk (optional, distributed): the separator payload packed by the write-back; returns whether
+// every round packed (else the caller packs with tpack_kernel)
+bool launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
+                       const int *active, bool sched_in = false, double *xs = nullptr, FwdIn *defer = nullptr,
+                       const PackArgs *pk = nullptr);
 // diagnostic: the forward sweep without its level phase (staging + write-back only)
 void launch_sptrsv_fwd_diag(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w);
 // out == null: the solution stays in schedule order in w (and with add, ys += it in place);
 // add with ys: out = P * (ys + solution), ys the previous solution in schedule order
-void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
-                       const int *active, double *ys = nullptr, const FwdIn *last = nullptr);
+// pk (optional, distributed): the Kp halo of the output packed by the write-back; returns whether
+// every round packed
+bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
+                       const int *active, double *ys = nullptr, const FwdIn *last = nullptr, const PackArgs *pk = nullptr);
 // r = xin(perm) - A*y with A = P'*Kp*P in schedule order (rows and columns), y in schedule
 // order (perm null: xin is the signed input already in schedule order, see launch_sptrsv_fwd);
 // order; each row sums its entries in Kp's column order, so r(k) equals row perm(k) of the
@@ -271,8 +287,9 @@ struct DSep;
 // t = x_eff - g with x_eff[i] = (i >= neg_from ? -x[i] : x[i])  (the GHN residual update)
 void launch_sub_state(Ctx &c, const double *x, int64_t neg_from, const double *g, int64_t N, double *t,
                       const int *run);
+// packed: the payload is already in S.sbuf (the forward sweep packed it): the allgather only
 void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x, int64_t neg_from,
-                         const double *piggy_src = nullptr);
+                         const double *piggy_src = nullptr, bool packed = false);
 // redundant separator solve into wT (= w + nsub); rank 0 writes (add: accumulates) y at the T dofs
 void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active);
 
@@ -342,6 +359,7 @@ struct DSep {
     // tprefix_kernel writes the row prefixes into pre (pre[nT] = 1.0) and the rest's payload
     // terms (tr_*, pre-multiplied) into their records' values (tr_slot)
     DBuf<int32_t> tk_ptr, tk_col, tr_ptr, tr_col, tr_slot, steps;
+    DBuf<int32_t> tslot;  // local schedule row -> payload slot (-1: not sent): the forward sweep packs
     DBuf<double> tk_val, tr_val, pre, rec_v;
     DBuf<uint32_t> rec_m;
     int64_t nsf = 0, nsb = 0, nrec = 0;
@@ -416,8 +434,10 @@ struct Precond {
     bool sched_path() const { return !dist && dKps.nnz > 0 && !no_sched; }
     bool no_sched = false;
     void set_handle(bool on);  // enabling or disabling clears the state
-    void ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run, const int *act,
+    // returns whether the backward sweep packed y's Kp halo (distributed: the residual's gather)
+    bool ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run, const int *act,
                    const double *piggy_src = nullptr);
+    DBuf<int32_t> hslot;  // distributed: local output index -> Kp halo slot (-1: none); empty: no packing
     // algorithmic HBM bytes of one apply
     double apply_bytes() const;
 };

@@ -304,9 +304,9 @@ void launch_gather(Ctx &c, const double *x, const int32_t *idx, int64_t n, doubl
     CPK_HIP(hipGetLastError());
 }
 
-void launch_halo(Ctx &c, const DMat &A, const double *x) {
+void launch_halo(Ctx &c, const DMat &A, const double *x, bool packed) {
     if (!A.halo() || A.kmax == 0) return;
-    launch_gather(c, x, A.send.p, A.nsend, A.sbuf.p);
+    if (!packed) launch_gather(c, x, A.send.p, A.nsend, A.sbuf.p);
     c.comm->allgather(A.sbuf.p, A.rbuf.p, (size_t)A.kstride, c.stream);
 }
 
@@ -347,8 +347,8 @@ void launch_spmv_colmask(Ctx &c, const DMat &A, int64_t col_min, const double *x
 }
 
 void launch_spmv_resid(Ctx &c, const DMat &A, const double *xin, int64_t neg_from, const double *y, double *r,
-                       const int *run, const int *active) {
-    launch_halo(c, A, y);
+                       const int *run, const int *active, bool halo_packed) {
+    launch_halo(c, A, y, halo_packed);
     if (!A.nblk) return;
     spmv_launch(c, A, y, 0, EpiResid{xin, neg_from, r, run, active});
 }
@@ -367,8 +367,8 @@ __global__ void resid_norm_fin_kernel(const double *tot, double tol, int *active
 }
 
 void launch_spmv_resid_norm(Ctx &c, const DMat &A, const double *xin, int64_t neg_from, const double *y, double *r,
-                            double tol, int *active_out, const int *run, const int *active) {
-    launch_halo(c, A, y);
+                            double tol, int *active_out, const int *run, const int *active, bool halo_packed) {
+    launch_halo(c, A, y, halo_packed);
     const bool dist = c.dist();
     if (A.nblk) {
         c.ensure_partials((size_t)A.nblk * 2);
@@ -766,10 +766,10 @@ __global__ void tpack_kernel(const double *__restrict__ w, const int32_t *__rest
 }
 
 void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x, int64_t neg_from,
-                         const double *piggy_src) {
+                         const double *piggy_src, bool packed) {
     if (S.kt == 0) return;
     const int64_t n = std::max<int64_t>(S.nsend + S.ntdof, piggy_src ? 1 : 0);
-    if (n > 0)
+    if (n > 0 && !packed)
         hipLaunchKernelGGL(tpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c.stream, w, S.send.p,
                            (int)S.nsend, x, neg_from, S.tdof.p, (int)S.ntdof, S.sbuf.p, piggy_src, (int)S.kt_data);
     CPK_HIP(hipGetLastError());
@@ -1213,6 +1213,28 @@ struct ResArgs {
     int64_t tail0 = 0, tail1 = 0;
 };
 
+// Distributed payloads packed by the sweeps' write-back instead of a gather launch:
+//   forward: the separator exchange's payload -- slot[schedule row] (-1: not sent) -> buf, and
+//            (workgroup 0 of the round-0 launch) rank 0's T inputs +-x[tdof] and the piggyback
+//            values: what tpack_kernel writes;
+//   backward: the residual SpMV's Kp halo -- slot[output index] -> buf, the value written to
+//            the output: what launch_halo's gather writes.
+__device__ __forceinline__ void pack_put(const PackArgs &pk, int64_t key, double z) {
+    if (pk.slot) {
+        const int32_t s = pk.slot[key];
+        if (s >= 0) pk.buf[s] = z;
+    }
+}
+__device__ __forceinline__ void pack_inputs(const PackArgs &pk, int tid, int nthreads) {
+    if (!pk.buf) return;
+    for (int t = tid; t < pk.ntdof; t += nthreads) {
+        const int32_t d = pk.tdof[t];
+        const double v = pk.x[d];
+        pk.buf[pk.nsend + t] = d >= pk.neg_from ? -v : v;
+    }
+    if (pk.piggy && tid < (int)kSepPiggy) pk.buf[pk.kt_data + tid] = pk.piggy[tid];
+}
+
 // ---- upper rounds ------------------------------------------------------------------------------
 // One workgroup per block, as sptrsv_fwd_kernel / sptrsv_bwd_kernel, with the staging laid out
 // for memory-level parallelism: the block's 32-byte record is one scalar load, every thread
@@ -1224,7 +1246,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
     int64_t blk0, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
-    double *w, double *out, const int *run, const int *active, int sched_in, double *ys, double *xs) {
+    double *w, double *out, const int *run, const int *active, int sched_in, double *ys, double *xs, PackArgs pk) {
     constexpr int R = RPU * TPB, CAP = EPU * TPB;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
@@ -1291,8 +1313,15 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
             const double z = S.w[i];
             w[r0 + i] = z;
             if (BWD) {
-                if (out) out[sp[j]] = ADD ? (ys ? ys[r0 + i] : out[sp[j]]) + z : z;
-                else if (ADD) ys[r0 + i] = ys[r0 + i] + z;
+                if (out) {
+                    const double o = ADD ? (ys ? ys[r0 + i] : out[sp[j]]) + z : z;
+                    out[sp[j]] = o;
+                    pack_put(pk, sp[j], o);
+                } else if (ADD) {
+                    ys[r0 + i] = ys[r0 + i] + z;
+                }
+            } else {
+                pack_put(pk, r0 + i, z);
             }
         }
     }
@@ -1444,7 +1473,7 @@ static void launch_last(Ctx &c, const DFactor &F, const FwdIn &in, double *w, do
 template <int TPB, int RPU, int EPU>
 static bool upper_round_t(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add, const double *xin,
                           int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in,
-                          double *ys, double *xs) {
+                          double *ys, double *xs, const PackArgs &pk) {
     if (F.sweep_threads[1] != TPB || F.sweep_rows[1] > RPU * TPB || F.sweep_cap[1] > EPU * TPB ||
         r >= (int64_t)F.round_fits.size() || !F.round_fits[r])
         return false;
@@ -1463,15 +1492,15 @@ static bool upper_round_t(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool ad
     if (!bwd)
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, false, false>), dim3((unsigned)nb), dim3(TPB), lds,
                            c.stream, b0, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active, sched_in, ys, xs);
+                           neg_from, w, out, run, active, sched_in, ys, xs, pk);
     else if (add)
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, true>), dim3((unsigned)nb), dim3(TPB), lds,
                            c.stream, b0, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active, sched_in, ys, xs);
+                           neg_from, w, out, run, active, sched_in, ys, xs, pk);
     else
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, false>), dim3((unsigned)nb), dim3(TPB), lds,
                            c.stream, b0, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active, sched_in, ys, xs);
+                           neg_from, w, out, run, active, sched_in, ys, xs, pk);
     return true;
 }
 
@@ -1480,9 +1509,9 @@ static bool upper_round_t(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool ad
 // threads with blocks of 1536 / 6144 and 2048 / 8192 (still 4 rounds; sweeps 2-7 % slower).
 static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add, const double *xin,
                         int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in,
-                        double *ys, double *xs) {
+                        double *ys, double *xs, const PackArgs &pk) {
     if (F.no_upper) return false;
-    return upper_round_t<512, 2, 8>(c, F, r, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs);
+    return upper_round_t<512, 2, 8>(c, F, r, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs, pk);
 }
 
 // SPLIT > 1: the workgroup is one wave holding SPLIT independent logical blocks of TPB lanes
@@ -1508,7 +1537,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,
     int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
     int skip0, double *xs, const int16_t *__restrict__ col16, ResArgs ra, const BlkMeta *__restrict__ ameta,
-    const int32_t *__restrict__ aptr) {
+    const int32_t *__restrict__ aptr, PackArgs pk) {
     static_assert(SPLIT == 1 || TPB * SPLIT == 64, "split blocks must share one wave");
     static_assert(!LOC || !BWD, "block-local columns: forward round 0 only");
     static_assert(!RES || (LOC && SPLIT == 1), "fused residual: forward round 0 with block-local columns");
@@ -1518,6 +1547,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     constexpr int R = RPT * TPB, CAP = EPT * TPB;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
+    if (!BWD && blockIdx.x == 0) pack_inputs(pk, threadIdx.x, TPB * SPLIT);  // rank 0's T inputs, piggyback
     const int sub = SPLIT > 1 ? (int)threadIdx.x / TPB : 0;
     SweepLds S(smem + (SPLIT > 1 ? sub * (int)sweep_lds_bytes_dev(R, CAP) : 0), R, CAP);
     const int tid = SPLIT > 1 ? (int)threadIdx.x % TPB : (int)threadIdx.x;
@@ -1743,8 +1773,15 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
                 const double z = S.w[i];
                 w[r0 + i] = z;
                 if (BWD) {
-                    if (out) out[dst[j]] = ADD ? xg[j] + z : z;
-                    else if (ADD) ys[r0 + i] = xg[j] + z;
+                    if (out) {
+                        const double o = ADD ? xg[j] + z : z;
+                        out[dst[j]] = o;
+                        pack_put(pk, dst[j], o);
+                    } else if (ADD) {
+                        ys[r0 + i] = xg[j] + z;
+                    }
+                } else {
+                    pack_put(pk, r0 + i, z);
                 }
             }
         }
@@ -1765,7 +1802,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
 template <int TPB, int RPT, int EPT, int SPLIT = 1>
 static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
                        double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
-                       double *xs, const ResArgs *ra = nullptr, int64_t *plan_grid = nullptr) {
+                       double *xs, const ResArgs *ra = nullptr, int64_t *plan_grid = nullptr, const PackArgs *pk = nullptr) {
     if (F.sweep_threads[0] != TPB || F.sweep_rows[0] != RPT * TPB || F.sweep_cap[0] != EPT * TPB) return false;
     if (ra && (bwd || F.fcol16.n == 0 || SPLIT != 1)) return false;  // fused residual: one instantiation
     const int64_t nb = F.round_ptr[1] - F.round_ptr[0];
@@ -1798,27 +1835,27 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true, kRes>), dim3((unsigned)grid),
                            blk, lds, c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p,
                            F.D.p, F.perm.p, xin, neg_from, w, out, run, active, 1, ys, 1, xs,
-                           (const int16_t *)F.fcol16.p, *ra, am, ap);
+                           (const int16_t *)F.fcol16.p, *ra, am, ap, PackArgs{});
     else if (loc)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true>), dim3((unsigned)grid), blk,
                            lds, c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, 1, xs,
-                           (const int16_t *)F.fcol16.p, ResArgs{}, am, ap);
+                           (const int16_t *)F.fcol16.p, ResArgs{}, am, ap, pk ? *pk : PackArgs{});
     else if (!bwd)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
-                           (const int16_t *)nullptr, ResArgs{}, am, ap);
+                           (const int16_t *)nullptr, ResArgs{}, am, ap, pk ? *pk : PackArgs{});
     else if (add)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
-                           (const int16_t *)nullptr, ResArgs{}, am, ap);
+                           (const int16_t *)nullptr, ResArgs{}, am, ap, pk ? *pk : PackArgs{});
     else
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
                            F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
-                           (const int16_t *)nullptr, ResArgs{}, am, ap);
+                           (const int16_t *)nullptr, ResArgs{}, am, ap, pk ? *pk : PackArgs{});
     return true;
 }
 
@@ -1826,9 +1863,9 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
 // (plan_grid: nothing is launched, the grid of the matching instantiation is returned)
 static bool pipe_round0(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
                         double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
-                        double *xs, int64_t *plan_grid = nullptr) {
+                        double *xs, int64_t *plan_grid = nullptr, const PackArgs *pk = nullptr) {
     if (!F.pipelined || F.round_ptr.size() < 2) return false;
-#define CPK_PR(...) pipe_round<__VA_ARGS__>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs, nullptr, plan_grid)
+#define CPK_PR(...) pipe_round<__VA_ARGS__>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs, nullptr, plan_grid, pk)
     return CPK_PR(32, 6, 18, 2) || CPK_PR(32, 4, 12, 2) || CPK_PR(32, 8, 24, 2) || CPK_PR(128, 2, 6) ||
            CPK_PR(64, 3, 9) || CPK_PR(64, 4, 12) || CPK_PR(64, 6, 18) || CPK_PR(64, 8, 24) || CPK_PR(128, 1, 4) ||
            CPK_PR(256, 1, 3);
@@ -1997,9 +2034,11 @@ __global__ void det_bwd_kernel(int64_t ndet, const uint32_t *__restrict__ bptr, 
 static inline unsigned det_grid(int64_t n) { return (unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 8192); }
 
 template <int MODE>
-static void fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                    const int *active, int sched_in, double *xs = nullptr, int64_t rfirst = 0, FwdIn *defer = nullptr) {
+static bool fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
+                    const int *active, int sched_in, double *xs = nullptr, int64_t rfirst = 0, FwdIn *defer = nullptr,
+                    const PackArgs *pk = nullptr) {
     int64_t R = (int64_t)F.round_ptr.size() - 1;
+    bool packed = pk != nullptr && F.ndet == 0 && rfirst == 0;  // every round through a packing kernel
     if (defer && MODE == 0 && fuse_last_ok(F)) {  // the last round runs with the backward sweep
         *defer = FwdIn{xin, neg_from, sched_in, xs, true};
         R -= 1;
@@ -2007,13 +2046,16 @@ static void fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
     if (F.ndet > 0 && !(sched_in && xin == w) && rfirst == 0)  // in place in schedule order: already there
         hipLaunchKernelGGL(det_fwd_kernel, dim3(det_grid(F.ndet)), dim3(kBlock), 0, c.stream, F.ndet, F.perm.p, xin,
                            neg_from, sched_in, w, run, active);
+    const PackArgs none{};
     for (int64_t r = rfirst; r < R; r++) {
         if (r == 0 && MODE == 0 &&
-            pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr, xs))
+            pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr, xs, nullptr, pk))
             continue;
         if (r > 0 && MODE == 0 &&
-            upper_round(c, F, r, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr, xs))
+            upper_round(c, F, r, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr, xs,
+                        pk ? *pk : none))
             continue;
+        packed = false;
         switch (F.sweep_threads[r == 0 ? 0 : 1]) {
         case 32: fwd_round<32, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
         case 64: fwd_round<64, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
@@ -2024,18 +2066,19 @@ static void fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
         }
     }
     CPK_HIP(hipGetLastError());
+    return packed && R > 0;
 }
 
 void launch_sptrsv_fwd_diag(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w) {
     fwd_all<1>(c, F, xin, neg_from, w, nullptr, nullptr, 0);
 }
 
-void launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
-                       const int *active, bool sched_in, double *xs, FwdIn *defer) {
+bool launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
+                       const int *active, bool sched_in, double *xs, FwdIn *defer, const PackArgs *pk) {
     // schedule-order input: no perm gather and no negation (neg_from applies to original indices)
     if (xs && F.ndet > 0) throw Error(CPK_ERR_UNSUPPORTED, "internal: input capture with detached rows");
     if (defer) defer->valid = false;
-    fwd_all<0>(c, F, xin, sched_in ? INT64_MAX : neg_from, w, run, active, sched_in ? 1 : 0, xs, 0, defer);
+    return fwd_all<0>(c, F, xin, sched_in ? INT64_MAX : neg_from, w, run, active, sched_in ? 1 : 0, xs, 0, defer, pk);
 }
 
 // diagnostic: the per-workgroup stamps of the last round-0 launch (0 unless built with
@@ -2098,17 +2141,21 @@ bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const in
     return true;
 }
 
-void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
-                       const int *active, double *ys, const FwdIn *last) {
+bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
+                       const int *active, double *ys, const FwdIn *last, const PackArgs *pk) {
     if (!out && add && !ys) throw Error(CPK_ERR_ARGS, "internal: accumulating backward sweep without a base");
     int64_t R = (int64_t)F.round_ptr.size() - 1;
+    bool packed = pk != nullptr && out != nullptr && F.ndet == 0 && !(last && last->valid);
+    const PackArgs none{};
     if (last && last->valid) {  // the deferred last round, forward and backward (sptrsv_last_kernel)
         launch_last(c, F, *last, w, out, add, run, active, ys);
         R -= 1;
     }
     for (int64_t r = R - 1; r >= 0; r--) {
-        if (r == 0 && pipe_round0(c, F, true, add, nullptr, 0, w, out, run, active, 0, ys, nullptr)) continue;
-        if (r > 0 && upper_round(c, F, r, true, add, nullptr, 0, w, out, run, active, 0, ys, nullptr)) continue;
+        if (r == 0 && pipe_round0(c, F, true, add, nullptr, 0, w, out, run, active, 0, ys, nullptr, nullptr, pk)) continue;
+        if (r > 0 && upper_round(c, F, r, true, add, nullptr, 0, w, out, run, active, 0, ys, nullptr, pk ? *pk : none))
+            continue;
+        packed = false;
         switch (F.sweep_threads[r == 0 ? 0 : 1] * 2 + (add ? 1 : 0)) {
         case 64: bwd_round<32, false>(c, F, r, w, out, run, active, ys); break;
         case 65: bwd_round<32, true>(c, F, r, w, out, run, active, ys); break;
@@ -2133,6 +2180,7 @@ void launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
                                F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, w, out, ys, run, active);
     }
     CPK_HIP(hipGetLastError());
+    return packed && R > 0;
 }
 
 // ---- small helpers ---------------------------------------------------------------------------

@@ -222,6 +222,10 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
         for (size_t i = 0; i < send.size(); i++) send[i] = pos[rp.tsend[i]];
         pc->sep.send.upload(send);
         pc->sep.nsend = (int64_t)send.size();
+        // the forward sweep's write-back packs the payload: schedule row -> payload slot
+        std::vector<int32_t> tsl((size_t)std::max<int64_t>(rp.nsub, 1), -1);
+        for (size_t i = 0; i < send.size(); i++) tsl[send[i]] = (int32_t)i;
+        pc->sep.tslot.upload(tsl);
     }
     // separator solve
     DSep &T = pc->sep;
@@ -249,12 +253,25 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     T.sbuf.zero(c.stream);
     T.rbuf.alloc((size_t)std::max<int64_t>(T.kt * c.nranks, 1));
     // refinement residual rows of Kp with their halo
+    std::vector<int32_t> kp_send;
     if (devnum) {
         HCsr kidx = an.Kp;
         for (size_t q = 0; q < kidx.val.size(); q++) kidx.val[q] = (double)(q + 1);
-        make_dist_dmat(dist_csr(kidx, *dm, c.rank, false), c.nranks, pc->dKp);
+        DistCsr dk = dist_csr(kidx, *dm, c.rank, false);
+        kp_send = dk.send;
+        make_dist_dmat(dk, c.nranks, pc->dKp);
     } else {
-        make_dist_dmat(dist_csr(an.Kp, *dm, c.rank, false), c.nranks, pc->dKp);
+        DistCsr dk = dist_csr(an.Kp, *dm, c.rank, false);
+        kp_send = dk.send;
+        make_dist_dmat(dk, c.nranks, pc->dKp);
+    }
+    {   // the backward sweep's write-back packs the residual's Kp halo: output index -> slot;
+        // not where a halo value is a separator dof (rank 0: the separator solve writes those)
+        std::vector<int32_t> hs((size_t)std::max<int64_t>(pc->N, 1), -1);
+        for (size_t i = 0; i < kp_send.size(); i++) hs[kp_send[i]] = (int32_t)i;
+        bool ok = !kp_send.empty();
+        for (int32_t d : rp.tdof) ok = ok && hs[d] < 0;
+        if (ok) pc->hslot.upload(hs);
     }
     clk.lap("rank plan + upload");
     if (devnum) {
@@ -386,16 +403,30 @@ double precond_refactor(Precond &p, const DMat &A11, const DMat &B, const DMat &
 }
 
 // y (=|+=) LDL * xin: forward sweep, [distributed: separator exchange + solve], backward sweep
-void Precond::ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run,
+bool Precond::ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run,
                         const int *act, const double *piggy_src) {
     Ctx &c = *ctx;
     FwdIn last;  // single GPU: the last round forward + backward in one launch (sptrsv_last_kernel)
-    launch_sptrsv_fwd(c, dF, xin, neg_from, w.p, run, act, false, nullptr, dist ? nullptr : &last);
-    if (dist) {
-        launch_sep_exchange(c, sep, w.p, xin, neg_from, piggy_src);
-        launch_sep_solve(c, sep, w.p + nsub, y, add, run, act);
+    if (!dist) {
+        launch_sptrsv_fwd(c, dF, xin, neg_from, w.p, run, act, false, nullptr, &last);
+        launch_sptrsv_bwd(c, dF, w.p, y, add, run, act, nullptr, &last);
+        return false;
     }
-    launch_sptrsv_bwd(c, dF, w.p, y, add, run, act, nullptr, &last);
+    // distributed: the sweeps' write-back packs the separator payload (forward) and the Kp halo
+    // of y (backward), so neither needs a gather launch
+    PackArgs fp;
+    if (sep.tslot.n) {
+        fp.slot = sep.tslot.p, fp.buf = sep.sbuf.p, fp.tdof = sep.tdof.p, fp.ntdof = (int)sep.ntdof;
+        fp.nsend = (int)sep.nsend, fp.kt_data = (int)sep.kt_data, fp.x = xin, fp.neg_from = neg_from;
+        fp.piggy = piggy_src;
+    }
+    const bool fpacked = launch_sptrsv_fwd(c, dF, xin, neg_from, w.p, run, act, false, nullptr, nullptr,
+                                           sep.tslot.n ? &fp : nullptr);
+    launch_sep_exchange(c, sep, w.p, xin, neg_from, piggy_src, fpacked);
+    launch_sep_solve(c, sep, w.p + nsub, y, add, run, act);
+    PackArgs bp;
+    if (hslot.n) bp.slot = hslot.p, bp.buf = dKp.sbuf.p;
+    return launch_sptrsv_bwd(c, dF, w.p, y, add, run, act, nullptr, nullptr, hslot.n ? &bp : nullptr);
 }
 
 void Precond::set_handle(bool on) {
@@ -411,6 +442,7 @@ void Precond::set_handle(bool on) {
 void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run, const double *piggy_src) {
     Ctx &c = *ctx;
     bool have_xs = false;  // the first forward sweep left the signed x in schedule order (xs)
+    bool hpacked = false;  // distributed: y's Kp halo packed by the last backward sweep
     if (residual_update != 0 && handle) {
         // y = op.LDL * [x(1:n) - op.Aty; x(n+1:N) - op.Cy]; then op.Aty = op.A(1:n, n+1:N) * y2,
         // op.Cy = op.A(n+1:N, n+1:N) * y2 = the columns n+1:N of Kp times y2  (opLDL2.m:164-172)
@@ -427,7 +459,7 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
     } else {
         // y = op.LDL * x   (opLDL2.m:165-167); the residual-update branch subtracts the zero
         // state of a value object and its SpMVs are dead: skipped
-        ldl_solve(x, neg_from, y, false, run, nullptr, piggy_src);
+        hpacked = ldl_solve(x, neg_from, y, false, run, nullptr, piggy_src);
     }
     if (nitref <= 0) return;
     const int64_t steps = (int64_t)nitref;
@@ -450,16 +482,18 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
     if (force_itref != 0) {
         // every step runs; rNorm/xNorm and the final residual are dead
         for (int64_t s = 0; s < steps; s++) {
-            launch_spmv_resid(c, dKp, x, neg_from, y, r.p, run, nullptr);  // r = x - op.A*y
-            ldl_solve(r.p, N, y, true, run, nullptr);                     // y = y + op.LDL*r
+            launch_spmv_resid(c, dKp, x, neg_from, y, r.p, run, nullptr, hpacked);  // r = x - op.A*y
+            hpacked = ldl_solve(r.p, N, y, true, run, nullptr);                    // y = y + op.LDL*r
         }
         return;
     }
     // data-dependent refinement: the predicate lives on the device, kernels test it
-    launch_spmv_resid_norm(c, dKp, x, neg_from, y, r.p, itref_tol, active.p, run, nullptr);
+    launch_spmv_resid_norm(c, dKp, x, neg_from, y, r.p, itref_tol, active.p, run, nullptr, hpacked);
     for (int64_t s = 0; s < steps; s++) {
-        ldl_solve(r.p, N, y, true, run, active.p);
-        if (s + 1 < steps) launch_spmv_resid_norm(c, dKp, x, neg_from, y, r.p, itref_tol, active.p, run, active.p);
+        // a skipped step (active == 0) leaves y and its packed halo as they were
+        hpacked = ldl_solve(r.p, N, y, true, run, active.p);
+        if (s + 1 < steps)
+            launch_spmv_resid_norm(c, dKp, x, neg_from, y, r.p, itref_tol, active.p, run, active.p, hpacked);
     }
 }
 
