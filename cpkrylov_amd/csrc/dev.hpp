@@ -291,7 +291,9 @@ void launch_sub_state(Ctx &c, const double *x, int64_t neg_from, const double *g
 void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x, int64_t neg_from,
                          const double *piggy_src = nullptr, bool packed = false);
 // redundant separator solve into wT (= w + nsub); rank 0 writes (add: accumulates) y at the T dofs
-void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active);
+// hslot / hbuf (optional): also pack y's Kp halo at the T dofs (PackArgs, backward)
+void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active,
+                      const int32_t *hslot = nullptr, double *hbuf = nullptr);
 
 // ---- device numeric LDL' (ldl.hip) --------------------------------------------------------
 struct DLdl {

@@ -2,9 +2,12 @@
 // [L,D,P] = ldl(op.A), ops/opLDL2.m:82) and the block/round schedule for the device
 // triangular sweeps that replace op.LDL = P*inv(L')*inv(D)*inv(L)*P' (ops/opLDL2.m:86).
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <atomic>
 #include <cstdlib>
 #include <numeric>
+#include <thread>
 
 #include "cpk.h"
 #include "host.hpp"
@@ -17,8 +20,164 @@ namespace cpk {
 // LDL: ldl_symbolic, ldl_numeric).  Here the reach of each row is visited in ascending column
 // order (a topological order of the row's triangular solve) instead of the stack order, so a
 // device thread walking the sorted row pattern performs the same operations in the same order.
+// Symbolic phase only (the device runs the numeric one), threaded.  The same outputs as the
+// serial loop below with numeric == false: the elimination tree by Liu's algorithm with path
+// compression (cs_etree), then every row's pattern -- the union of the tree paths from its Kp
+// entries up to the row, sorted ascending -- rows in parallel (each thread stamps its own
+// marker array), then the columns of L by a counting pass over the rows in ascending order.
+static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &perm, LdlSymbolic &sym) {
+    const int64_t N = Kp.nrows;
+    auto T0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *w) { if (getenv("CPK_SYMT")) { auto t = std::chrono::steady_clock::now(); fprintf(stderr, "%s %.3f\n", w, std::chrono::duration<double>(t - T0).count()); T0 = t; } };
+    Factor f;
+    f.N = N;
+    f.perm = perm;
+    std::vector<int32_t> pinv(N);
+    for (int64_t k = 0; k < N; k++) pinv[perm[k]] = (int32_t)k;
+    f.parent.assign(N, -1);
+    {
+        std::vector<int32_t> anc(N, -1);
+        for (int64_t k = 0; k < N; k++) {
+            const int32_t r = perm[k];
+            for (int64_t p = Kp.ptr[r]; p < Kp.ptr[r + 1]; p++) {
+                int32_t i = pinv[Kp.ind[p]];
+                while (i != -1 && i < k) {
+                    const int32_t nx = anc[i];
+                    anc[i] = (int32_t)k;
+                    if (nx == -1) f.parent[i] = (int32_t)k;
+                    i = nx;
+                }
+            }
+        }
+    }
+    lap("etree");
+    // row patterns and seeds, rows in parallel chunks
+    const int T = std::max(1, std::min<int>(host_threads(), (int)((N + 65535) / 65536)));
+    struct Chunk {
+        std::vector<int32_t> rc, tgt;
+        std::vector<uint32_t> src;
+        std::vector<int32_t> rcnt, scnt;  // per row: pattern length, seed count
+    };
+    std::vector<Chunk> ch(T);
+    const int64_t cs = (N + T - 1) / T;
+    std::vector<std::thread> th;
+    auto work = [&](int t) {
+        const int64_t lo = t * cs, hi = std::min<int64_t>(N, lo + cs);
+        Chunk &c = ch[t];
+        c.rcnt.resize(std::max<int64_t>(hi - lo, 0)), c.scnt.resize(std::max<int64_t>(hi - lo, 0));
+        std::vector<int32_t> flag(N, -1), slot(N), pat;
+        for (int64_t k = lo; k < hi; k++) {
+            flag[k] = (int32_t)k;
+            pat.clear();
+            const int32_t r = perm[k];
+            for (int64_t p = Kp.ptr[r]; p < Kp.ptr[r + 1]; p++)
+                for (int32_t i = pinv[Kp.ind[p]]; i < k && flag[i] != k; i = f.parent[i]) {
+                    pat.push_back(i);
+                    flag[i] = (int32_t)k;
+                }
+            std::sort(pat.begin(), pat.end());
+            for (size_t q = 0; q < pat.size(); q++) slot[pat[q]] = (int32_t)q;  // row-local, rebased later
+            c.rc.insert(c.rc.end(), pat.begin(), pat.end());
+            c.rcnt[k - lo] = (int32_t)pat.size();
+            int32_t ns = 0;
+            for (int64_t p = Kp.ptr[r]; p < Kp.ptr[r + 1]; p++) {
+                const int32_t i = pinv[Kp.ind[p]];
+                if (i > k) continue;
+                c.tgt.push_back(i == k ? -1 : slot[i]);
+                c.src.push_back((uint32_t)p);
+                ns++;
+            }
+            c.scnt[k - lo] = ns;
+        }
+    };
+    for (int t = 1; t < T; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto &x : th) x.join();
+    lap("rows");
+    sym.N = N;
+    sym.Rp.assign(N + 1, 0);
+    sym.kp_ptr.assign(N + 1, 0);
+    for (int t = 0; t < T; t++)
+        for (size_t q = 0; q < ch[t].rcnt.size(); q++) {
+            const int64_t k = t * cs + (int64_t)q;
+            sym.Rp[k + 1] = sym.Rp[k] + ch[t].rcnt[q];
+            sym.kp_ptr[k + 1] = sym.kp_ptr[k] + ch[t].scnt[q];
+        }
+    if ((int64_t)sym.Rp[N] > INT32_MAX || sym.kp_ptr[N] < 0)
+        throw Error(CPK_ERR_NOMEM, "factor too large for 32-bit entry offsets");
+    lap("prefix");
+    const int64_t nnz = sym.Rp[N];
+    sym.Rc.resize(nnz);
+    sym.kp_tgt.resize(sym.kp_ptr[N]);
+    sym.kp_src.resize(sym.kp_ptr[N]);
+    lap("alloc");
+    {
+        std::vector<std::thread> cp;
+        auto copy = [&](int t) {
+            const int64_t k0 = t * cs;
+            if (ch[t].rcnt.empty()) return;
+            std::copy(ch[t].rc.begin(), ch[t].rc.end(), sym.Rc.begin() + sym.Rp[k0]);
+            // seeds: row-local slots -> row-entry slots
+            int64_t o = sym.kp_ptr[k0];
+            for (size_t q = 0; q < ch[t].rcnt.size(); q++) {
+                const int32_t base = sym.Rp[k0 + (int64_t)q];
+                for (int32_t s = 0; s < ch[t].scnt[q]; s++, o++) {
+                    const int32_t tg = ch[t].tgt[o - sym.kp_ptr[k0]];
+                    sym.kp_tgt[o] = tg < 0 ? -1 : base + tg;
+                    sym.kp_src[o] = ch[t].src[o - sym.kp_ptr[k0]];
+                }
+            }
+            std::vector<int32_t>().swap(ch[t].rc);
+        };
+        for (int t = 1; t < T; t++) cp.emplace_back(copy, t);
+        copy(0);
+        for (auto &x : cp) x.join();
+    }
+    lap("concat");
+    // columns of L: rows in ascending order within each column (the serial loop's lnz[i]++ order)
+    f.Lp.assign(N + 1, 0);
+    for (int64_t q = 0; q < nnz; q++) f.Lp[sym.Rc[q] + 1]++;
+    for (int64_t i = 0; i < N; i++) f.Lp[i + 1] += f.Lp[i];
+    f.Li.resize(nnz);
+    sym.Rcsc.resize(nnz);
+    {
+        // threads own column ranges of equal entry counts; each scans the rows in ascending
+        // order and places the entries of its columns (so a column's rows stay ascending)
+        std::vector<int64_t> cut(T + 1, N);
+        cut[0] = 0;
+        for (int t = 1; t < T; t++)
+            cut[t] = std::upper_bound(f.Lp.begin(), f.Lp.end(), nnz * t / T) - f.Lp.begin() - 1;
+        std::vector<std::thread> cth;
+        auto place = [&](int t) {
+            const int32_t c0 = (int32_t)cut[t], c1 = (int32_t)cut[t + 1];
+            if (c0 >= c1) return;
+            std::vector<int64_t> nx(f.Lp.begin() + c0, f.Lp.begin() + c1);
+            for (int64_t k = 0; k < N; k++)
+                for (int32_t q = sym.Rp[k]; q < sym.Rp[k + 1]; q++) {
+                    const int32_t i = sym.Rc[q];
+                    if (i < c0 || i >= c1) continue;
+                    const int64_t p2 = nx[i - c0]++;
+                    f.Li[p2] = (int32_t)k;
+                    sym.Rcsc[q] = (int32_t)p2;
+                }
+        };
+        for (int t = 1; t < T; t++) cth.emplace_back(place, t);
+        place(0);
+        for (auto &x : cth) x.join();
+    }
+    lap("columns");
+    return f;
+}
+
+static void height_levels(const Factor &f, LdlSymbolic *sym);
+
 Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int /*nthreads*/, LdlSymbolic *sym,
                   bool numeric) {
+    if (!numeric && sym && Kp.nrows > 0) {
+        Factor f = ldl_symbolic_threaded(Kp, perm, *sym);
+        height_levels(f, sym);
+        return f;
+    }
     const int64_t N = Kp.nrows;
     Factor f;
     f.N = N;
@@ -113,9 +272,15 @@ Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int /*nthrea
                                             " (static 1x1 pivoting needs G > 0 on the nullspace and C > 0)");
         f.D[k] = d;
     }
-    if (sym) {
+    if (sym) height_levels(f, sym);
+    return f;
+}
+
+// rows by elimination-tree height: a row depends only on its descendants
+static void height_levels(const Factor &f, LdlSymbolic *sym) {
+    const int64_t N = f.N;
+    {
         if (sym->kp_tgt.size() > (size_t)INT32_MAX) throw Error(CPK_ERR_NOMEM, "too many Kp entries for the device factorization");
-        // rows by elimination-tree height: a row depends only on its descendants
         std::vector<int32_t> h(N, 0);
         int32_t hmax = 0;
         for (int64_t v = 0; v < N; v++) {
@@ -129,7 +294,6 @@ Factor ldl_factor(const HCsr &Kp, const std::vector<int32_t> &perm, int /*nthrea
         std::vector<int32_t> nx(sym->lev_ptr.begin(), sym->lev_ptr.end() - 1);
         for (int64_t v = 0; v < N; v++) sym->lev_rows[nx[h[v]]++] = (int32_t)v;
     }
-    return f;
 }
 
 Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1, int64_t SUB0,

@@ -395,7 +395,8 @@ __global__ __launch_bounds__(256) void tsolve_kernel(
     const int32_t *__restrict__ tf_ptr, const int32_t *__restrict__ tf_col, const double *__restrict__ tf_val,
     const int32_t *__restrict__ tf_src, const int32_t *__restrict__ tb_ptr, const int32_t *__restrict__ tb_col,
     const double *__restrict__ tb_val, const double *__restrict__ DT, const double *__restrict__ rbuf,
-    const int32_t *__restrict__ tdof, int ntdof, double *wT, double *y, int add, const int *run, const int *active) {
+    const int32_t *__restrict__ tdof, int ntdof, double *wT, double *y, int add, const int *run, const int *active,
+    const int32_t *__restrict__ hslot, double *hbuf) {
     extern __shared__ double wt[];
     if (skip(run, active)) return;
     const int tid = threadIdx.x;
@@ -425,7 +426,9 @@ __global__ __launch_bounds__(256) void tsolve_kernel(
         wT[t] = wt[t];
         if (t < ntdof) {
             const int32_t d = tdof[t];
-            y[d] = add ? y[d] + wt[t] : wt[t];
+            const double o = add ? y[d] + wt[t] : wt[t];
+            y[d] = o;
+            if (hslot && hslot[d] >= 0) hbuf[hslot[d]] = o;  // the Kp halo of y (PackArgs)
         }
     }
 }
@@ -528,7 +531,8 @@ template <bool GREC>
 __global__ __launch_bounds__(kTsolveThreads) void tsolve_steps_kernel(
     int nT, int nsf, int nsb, int nrec, const double *__restrict__ rec_v, const uint32_t *__restrict__ rec_m,
     const int32_t *__restrict__ steps, const double *__restrict__ pre, const double *__restrict__ DT,
-    const int32_t *__restrict__ tdof, int ntdof, double *wT, double *y, int add, const int *run, const int *active) {
+    const int32_t *__restrict__ tdof, int ntdof, double *wT, double *y, int add, const int *run, const int *active,
+    const int32_t *__restrict__ hslot, double *hbuf) {
     // LDS: wt[nT + 1, even] | rv[nrec] | rm[nrec] (the records: staged unless GREC)
     extern __shared__ __attribute__((aligned(16))) double tsw[];
     if (skip(run, active)) return;
@@ -576,7 +580,9 @@ __global__ __launch_bounds__(kTsolveThreads) void tsolve_steps_kernel(
         wT[t] = wt[t];
         if (t < ntdof) {
             const int32_t d = tdof[t];
-            y[d] = add ? y[d] + wt[t] : wt[t];
+            const double o = add ? y[d] + wt[t] : wt[t];
+            y[d] = o;
+            if (hslot && hslot[d] >= 0) hbuf[hslot[d]] = o;  // the Kp halo of y (PackArgs)
         }
     }
 }
@@ -776,7 +782,8 @@ void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x
     c.comm->allgather(S.sbuf.p, S.rbuf.p, (size_t)S.kt, c.stream);
 }
 
-void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active) {
+void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active,
+                      const int32_t *hslot, double *hbuf) {
     if (S.nT == 0) return;
     static const bool lds_attr = [] {
         return hipFuncSetAttribute((const void *)tsolve_steps_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -795,19 +802,19 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
             hipLaunchKernelGGL(tsolve_steps_kernel<true>, dim3(1), dim3(kTsolveThreads), lds, c.stream, (int)S.nT,
                                (int)S.nsf, (int)S.nsb, (int)S.nrec, (const double *)S.rec_v.p,
                                (const uint32_t *)S.rec_m.p, S.steps.p, (const double *)S.pre.p, (const double *)S.DT.p,
-                               S.tdof.p, (int)S.ntdof, wT, y, add ? 1 : 0, run, active);
+                               S.tdof.p, (int)S.ntdof, wT, y, add ? 1 : 0, run, active, hslot, hbuf);
         else
             hipLaunchKernelGGL(tsolve_steps_kernel<false>, dim3(1), dim3(kTsolveThreads), lds, c.stream, (int)S.nT,
                                (int)S.nsf, (int)S.nsb, (int)S.nrec, (const double *)S.rec_v.p,
                                (const uint32_t *)S.rec_m.p, S.steps.p, (const double *)S.pre.p, (const double *)S.DT.p,
-                               S.tdof.p, (int)S.ntdof, wT, y, add ? 1 : 0, run, active);
+                               S.tdof.p, (int)S.ntdof, wT, y, add ? 1 : 0, run, active, hslot, hbuf);
         CPK_HIP(hipGetLastError());
         return;
     }
     hipLaunchKernelGGL(tsolve_kernel, dim3(1), dim3(256), (size_t)S.nT * sizeof(double), c.stream, (int)S.nlev,
                        (int)S.nT, S.lev_ptr.p, S.lev_rows.p, S.tf_ptr.p, S.tf_col.p, S.tf_val.p, S.tf_src.p,
                        S.tb_ptr.p, S.tb_col.p, S.tb_val.p, S.DT.p, S.rbuf.p, S.tdof.p, (int)S.ntdof, wT, y,
-                       add ? 1 : 0, run, active);
+                       add ? 1 : 0, run, active, hslot, hbuf);
     CPK_HIP(hipGetLastError());
 }
 
@@ -1225,14 +1232,16 @@ __device__ __forceinline__ void pack_put(const PackArgs &pk, int64_t key, double
         if (s >= 0) pk.buf[s] = z;
     }
 }
-__device__ __forceinline__ void pack_inputs(const PackArgs &pk, int tid, int nthreads) {
+// one T input per thread of the launch (thread e of the grid), so no workgroup is delayed by
+// more than one dependent load pair; the piggyback values by the first threads of workgroup 0
+__device__ __forceinline__ void pack_inputs(const PackArgs &pk, int64_t e) {
     if (!pk.buf) return;
-    for (int t = tid; t < pk.ntdof; t += nthreads) {
-        const int32_t d = pk.tdof[t];
+    if (e < pk.ntdof) {
+        const int32_t d = pk.tdof[e];
         const double v = pk.x[d];
-        pk.buf[pk.nsend + t] = d >= pk.neg_from ? -v : v;
+        pk.buf[pk.nsend + e] = d >= pk.neg_from ? -v : v;
     }
-    if (pk.piggy && tid < (int)kSepPiggy) pk.buf[pk.kt_data + tid] = pk.piggy[tid];
+    if (pk.piggy && e < (int64_t)kSepPiggy) pk.buf[pk.kt_data + e] = pk.piggy[e];
 }
 
 // ---- upper rounds ------------------------------------------------------------------------------
@@ -1547,7 +1556,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     constexpr int R = RPT * TPB, CAP = EPT * TPB;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
-    if (!BWD && blockIdx.x == 0) pack_inputs(pk, threadIdx.x, TPB * SPLIT);  // rank 0's T inputs, piggyback
+    if (!BWD) pack_inputs(pk, (int64_t)blockIdx.x * (TPB * SPLIT) + threadIdx.x);  // rank 0's T inputs, piggyback
     const int sub = SPLIT > 1 ? (int)threadIdx.x / TPB : 0;
     SweepLds S(smem + (SPLIT > 1 ? sub * (int)sweep_lds_bytes_dev(R, CAP) : 0), R, CAP);
     const int tid = SPLIT > 1 ? (int)threadIdx.x % TPB : (int)threadIdx.x;
@@ -1802,7 +1811,8 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
 template <int TPB, int RPT, int EPT, int SPLIT = 1>
 static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
                        double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
-                       double *xs, const ResArgs *ra = nullptr, int64_t *plan_grid = nullptr, const PackArgs *pk = nullptr) {
+                       double *xs, const ResArgs *ra = nullptr, int64_t *plan_grid = nullptr, const PackArgs *pk = nullptr,
+                       bool *pk_used = nullptr) {
     if (F.sweep_threads[0] != TPB || F.sweep_rows[0] != RPT * TPB || F.sweep_cap[0] != EPT * TPB) return false;
     if (ra && (bwd || F.fcol16.n == 0 || SPLIT != 1)) return false;  // fused residual: one instantiation
     const int64_t nb = F.round_ptr[1] - F.round_ptr[0];
@@ -1820,6 +1830,9 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>((nb + SPLIT - 1) / SPLIT, (int64_t)occ * cus));
+    // the forward pack puts one T input per thread of the grid: only when the grid covers them
+    if (pk && !bwd && (int64_t)pk->ntdof > grid * TPB * SPLIT) pk = nullptr;
+    if (pk_used) *pk_used = pk != nullptr;
     if (plan_grid) {  // plan_round0: the grid this launch would use (no assignment for split blocks)
         *plan_grid = SPLIT == 1 ? grid : 0;
         return true;
@@ -1863,9 +1876,9 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
 // (plan_grid: nothing is launched, the grid of the matching instantiation is returned)
 static bool pipe_round0(Ctx &c, const DFactor &F, bool bwd, bool add, const double *xin, int64_t neg_from,
                         double *w, double *out, const int *run, const int *active, int sched_in, double *ys,
-                        double *xs, int64_t *plan_grid = nullptr, const PackArgs *pk = nullptr) {
+                        double *xs, int64_t *plan_grid = nullptr, const PackArgs *pk = nullptr, bool *pk_used = nullptr) {
     if (!F.pipelined || F.round_ptr.size() < 2) return false;
-#define CPK_PR(...) pipe_round<__VA_ARGS__>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs, nullptr, plan_grid, pk)
+#define CPK_PR(...) pipe_round<__VA_ARGS__>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs, nullptr, plan_grid, pk, pk_used)
     return CPK_PR(32, 6, 18, 2) || CPK_PR(32, 4, 12, 2) || CPK_PR(32, 8, 24, 2) || CPK_PR(128, 2, 6) ||
            CPK_PR(64, 3, 9) || CPK_PR(64, 4, 12) || CPK_PR(64, 6, 18) || CPK_PR(64, 8, 24) || CPK_PR(128, 1, 4) ||
            CPK_PR(256, 1, 3);
@@ -2048,9 +2061,13 @@ static bool fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
                            neg_from, sched_in, w, run, active);
     const PackArgs none{};
     for (int64_t r = rfirst; r < R; r++) {
+        bool used = true;
         if (r == 0 && MODE == 0 &&
-            pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr, xs, nullptr, pk))
+            pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr, xs, nullptr, pk,
+                        &used)) {
+            packed = packed && used;
             continue;
+        }
         if (r > 0 && MODE == 0 &&
             upper_round(c, F, r, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr, xs,
                         pk ? *pk : none))

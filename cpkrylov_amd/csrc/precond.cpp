@@ -265,13 +265,11 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
         kp_send = dk.send;
         make_dist_dmat(dk, c.nranks, pc->dKp);
     }
-    {   // the backward sweep's write-back packs the residual's Kp halo: output index -> slot;
-        // not where a halo value is a separator dof (rank 0: the separator solve writes those)
+    {   // the backward sweep's write-back (and, at the T dofs of rank 0, the separator solve's)
+        // packs the residual's Kp halo: output index -> slot
         std::vector<int32_t> hs((size_t)std::max<int64_t>(pc->N, 1), -1);
         for (size_t i = 0; i < kp_send.size(); i++) hs[kp_send[i]] = (int32_t)i;
-        bool ok = !kp_send.empty();
-        for (int32_t d : rp.tdof) ok = ok && hs[d] < 0;
-        if (ok) pc->hslot.upload(hs);
+        if (!kp_send.empty()) pc->hslot.upload(hs);
     }
     clk.lap("rank plan + upload");
     if (devnum) {
@@ -423,7 +421,7 @@ bool Precond::ldl_solve(const double *xin, int64_t neg_from, double *y, bool add
     const bool fpacked = launch_sptrsv_fwd(c, dF, xin, neg_from, w.p, run, act, false, nullptr, nullptr,
                                            sep.tslot.n ? &fp : nullptr);
     launch_sep_exchange(c, sep, w.p, xin, neg_from, piggy_src, fpacked);
-    launch_sep_solve(c, sep, w.p + nsub, y, add, run, act);
+    launch_sep_solve(c, sep, w.p + nsub, y, add, run, act, hslot.n ? hslot.p : nullptr, dKp.sbuf.p);
     PackArgs bp;
     if (hslot.n) bp.slot = hslot.p, bp.buf = dKp.sbuf.p;
     return launch_sptrsv_bwd(c, dF, w.p, y, add, run, act, nullptr, nullptr, hslot.n ? &bp : nullptr);
