@@ -252,8 +252,9 @@ def main():
             "config": {"workload": (f"S10 synthetic symmetric saddle-point system, cp{args.method} to convergence "
                                     "(cpk_exprog1 options), step = one method call" if args.config == "s10" else
                                     f"S50 synthetic nonsymmetric 3x3-block saddle-point system, cp{args.method}"
-                                    f"(mem 40), step = one method call of at most {args.opts['itmax']} iterations "
-                                    "(cpk_exprog1 tolerances)"),
+                                    f"(mem 40), step = one method call TRUNCATED at {args.opts['itmax']} iterations "
+                                    "(cpk_exprog1 tolerances; convergence takes 611-1039 iterations, rounding-"
+                                    "dependent, DESIGN.md sec. 6), parity checked on the same truncated run"),
                        "N": N, "n": n, "m": m, "nnz_kp": M.info["nnz_kp"], "nnz_l": M.info["nnz_l"],
                        "sweep_launches": M.info["nrounds"], "elim_tree_depth": M.info["depth"],
                        "parallelism": f"rowblock{world}" if distributed else "single",

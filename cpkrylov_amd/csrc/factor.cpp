@@ -450,13 +450,6 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     std::vector<int32_t> block(N, -1);  // -1: detached
     for (int64_t v = 0; v < N; v++)
         if (cl[v] >= 0) block[v] = cluster_block[cl[v]];
-    // intra-block levels (CSC columns ascend, so level[j] is final when column j is visited)
-    std::vector<int32_t> level(N, 0);
-    for (int64_t j = 0; j < N; j++)
-        for (int64_t p = f.Lp[j]; p < f.Lp[j + 1]; p++) {
-            const int32_t i = f.Li[p];
-            if (block[j] >= 0 && block[i] == block[j]) level[i] = std::max(level[i], level[j] + 1);
-        }
     // new order: detached rows (ascending), then blocks ascending (= rounds ascending), then
     // level, then old index
     std::vector<int64_t> bcount(nb + 2, 0);  // bcount[0]: detached
@@ -469,6 +462,20 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
         std::vector<int64_t> nx(bcount.begin(), bcount.end() - 1);
         for (int64_t v = 0; v < N; v++) s.order[nx[block[v] + 1]++] = (int32_t)v;
     }
+    // intra-block levels, blocks in parallel: a block's rows are disjoint from every other
+    // block's, and in ascending old index (a topological order: L's columns point to rows of
+    // larger index), so level[j] is final when column j is visited
+    std::vector<int32_t> level(N, 0);
+    parallel_for(nb, [&](int64_t lo, int64_t hi) {
+        for (int64_t b = lo; b < hi; b++)
+            for (int64_t q = s.blk_row[b]; q < s.blk_row[b + 1]; q++) {
+                const int32_t j = s.order[q];
+                for (int64_t p = f.Lp[j]; p < f.Lp[j + 1]; p++) {
+                    const int32_t i = f.Li[p];
+                    if (block[i] == block[j]) level[i] = std::max(level[i], level[j] + 1);
+                }
+            }
+    }, 64);
     s.blk_lvl.assign(1, 0);
     s.lvl_row.clear();
     parallel_for(nb, [&](int64_t lo, int64_t hi) {  // blocks sort independently

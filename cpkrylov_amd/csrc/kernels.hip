@@ -102,7 +102,9 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
                 }
             });
     }
-    std::vector<double> fval(nf, 0.0);
+    // structure only (the device numeric phase fills the values): no host value arrays, the
+    // device ones are zeroed in place
+    std::vector<double> fval(vals ? nf : 0, 0.0);
     if (vals)
         parallel_for(nf, [&](int64_t lo, int64_t hi) {
             for (int64_t q = lo; q < hi; q++) fval[q] = f.Lx[fidx[q]];
@@ -112,7 +114,8 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     for (int64_t j = 0; j < N; j++)
         bptr[j + 1] = bptr[j] + (uint32_t)(f.Lp[j + 1] - f.Lp[j]) + (uint32_t)(extra ? (*extra)[j].size() : 0);
     std::vector<int32_t> bcol(d.nnz), bidx(bsrc ? d.nnz : 0);
-    std::vector<double> bval(d.nnz, 0.0);
+    const bool bvals = vals || nextra > 0;
+    std::vector<double> bval(bvals ? d.nnz : 0, 0.0);
     parallel_for(N, [&](int64_t lo, int64_t hi) {  // rows (columns of L) sort independently
         std::vector<std::pair<int64_t, std::pair<int32_t, int64_t>>> row;  // (key, (col, CSC slot | ~extra))
         for (int64_t j = lo; j < hi; j++) {
@@ -142,14 +145,25 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
                 d.round_fits[r] = 0;
         }
     // padding entries: clamped, unconditional loads may touch one entry past a block's end
-    fcol.resize(fcol.size() + kFactorPadEntries, 0), fval.resize(fval.size() + kFactorPadEntries, 0.0);
-    bcol.resize(bcol.size() + kFactorPadEntries, 0), bval.resize(bval.size() + kFactorPadEntries, 0.0);
+    fcol.resize(fcol.size() + kFactorPadEntries, 0), bcol.resize(bcol.size() + kFactorPadEntries, 0);
     d.fptr.upload(fptr);
     d.fcol.upload(fcol);
-    d.fval.upload(fval);
+    if (vals) {
+        fval.resize(fval.size() + kFactorPadEntries, 0.0);
+        d.fval.upload(fval);
+    } else {
+        d.fval.alloc((size_t)nf + kFactorPadEntries);
+        CPK_HIP(hipMemset(d.fval.p, 0, d.fval.bytes()));
+    }
     d.bptr.upload(bptr);
     d.bcol.upload(bcol);
-    d.bval.upload(bval);
+    if (bvals) {
+        bval.resize(bval.size() + kFactorPadEntries, 0.0);
+        d.bval.upload(bval);
+    } else {
+        d.bval.alloc((size_t)d.nnz + kFactorPadEntries);
+        CPK_HIP(hipMemset(d.bval.p, 0, d.bval.bytes()));
+    }
     if (vals) d.D.upload(f.D);
     else d.D.alloc((size_t)N);
     d.perm.upload(f.perm);
@@ -1011,21 +1025,26 @@ __device__ __forceinline__ void levels_owned(SweepLds &S, int nl, int nr, bool s
 #ifndef CPK_LEVEL_GROUP
 #define CPK_LEVEL_GROUP 1
 #endif
+#ifndef CPK_UPPER_GROUP
+#define CPK_UPPER_GROUP 1  // the same in the upper-round and last-round kernels' one-wave levels
+#endif
 __device__ __forceinline__ double row_next_lane(double x) {  // lane i + 1 of its 16-lane row (15: 0)
     const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x101, 0xf, 0xf, true);
     const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x101, 0xf, 0xf, true);
     return __hiloint2double(hi, lo);
 }
 
-template <int CH>
-__device__ __forceinline__ void levels_grouped_fwd(SweepLds &S, int nl, bool skip_first, int lane) {
-    for (int l = skip_first ? 1 : 0; l < nl; l++) {
+// BWD: levels in reverse; PS: rows start at ps[k] (after fold_prefix) instead of p[k]
+template <int CH, bool BWD = false, bool PS = false>
+__device__ __forceinline__ void levels_grouped(SweepLds &S, int nl, bool skip_first, int lane) {
+    for (int li = (skip_first && !BWD) ? 1 : 0; li < nl; li++) {
+        const int l = BWD ? nl - 1 - li : li;
         const int a = S.lv[l], z = S.lv[l + 1], nr = z - a;
         if (nr > 16) {  // one lane per row, two terms per LDS round trip (sweep_levels)
             for (int k = a + lane; k < z; k += kWave) {
                 const int e1 = S.p[k + 1];
                 double acc = S.w[k];
-                for (int e = S.p[k]; e < e1; e += CH) {
+                for (int e = PS ? S.ps[k] : S.p[k]; e < e1; e += CH) {
                     int c[CH];
                     double v[CH], x[CH];
 #pragma unroll
@@ -1042,7 +1061,7 @@ __device__ __forceinline__ void levels_grouped_fwd(SweepLds &S, int nl, bool ski
             const int G = 1 << lg, g = lane >> lg, j = lane & (G - 1);
             const bool row = g < nr;
             const int k = a + (row ? g : 0);
-            const int e0 = S.p[k], e1 = row ? (int)S.p[k + 1] : e0;
+            const int e0 = PS ? S.ps[k] : S.p[k], e1 = row ? (int)S.p[k + 1] : e0;
             double acc = S.w[k];
             for (int c0 = 0;; c0 += G) {
                 const int e = e0 + c0 + j;
@@ -1060,6 +1079,10 @@ __device__ __forceinline__ void levels_grouped_fwd(SweepLds &S, int nl, bool ski
         }
         asm volatile("" ::: "memory");  // one wave: LDS in issue order (levels_owned)
     }
+}
+template <int CH>
+__device__ __forceinline__ void levels_grouped_fwd(SweepLds &S, int nl, bool skip_first, int lane) {
+    levels_grouped<CH, false, false>(S, nl, skip_first, lane);
 }
 
 // Backward write-back of row k (schedule order) with value z:
@@ -1312,8 +1335,12 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
     __syncthreads();
     fold_prefix<TPB, 1>(S, nr, -1, R);
     // levels on one wave: a level holds a few rows, and without a workgroup barrier per level
-    // (a single wave's LDS accesses complete in program order) the chain is LDS latency only
-    if (tid < kWave) sweep_levels<kWave, BWD, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
+    // (a single wave's LDS accesses complete in program order) the chain is LDS latency only;
+    // narrow levels give each row a lane group (levels_grouped)
+    if (tid < kWave) {
+        if (CPK_UPPER_GROUP) levels_grouped<CPK_UPPER_CH, BWD, true>(S, nl, false, tid);
+        else sweep_levels<kWave, BWD, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
+    }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < RPU; j++) {
@@ -1406,7 +1433,10 @@ __global__ __launch_bounds__(TPB) void sptrsv_last_kernel(
     }
     __syncthreads();
     fold_prefix<TPB, 1>(S, nr, -1, R);
-    if (tid < kWave) sweep_levels<kWave, false, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
+    if (tid < kWave) {
+        if (CPK_UPPER_GROUP) levels_grouped<CPK_UPPER_CH, false, true>(S, nl, false, tid);
+        else sweep_levels<kWave, false, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
+    }
     __syncthreads();
     // ---- backward (sptrsv_upper_kernel<..., true, ADD>): w / D, the entries, fold, levels; the
     // backward terms of a last-round block are its own rows (the 1.0 slot path is kept for any other)
@@ -1433,7 +1463,10 @@ __global__ __launch_bounds__(TPB) void sptrsv_last_kernel(
     }
     __syncthreads();
     fold_prefix<TPB, 1>(S, nr, -1, R);
-    if (tid < kWave) sweep_levels<kWave, true, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
+    if (tid < kWave) {
+        if (CPK_UPPER_GROUP) levels_grouped<CPK_UPPER_CH, true, true>(S, nl, false, tid);
+        else sweep_levels<kWave, true, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
+    }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < RPU; j++) {
