@@ -65,7 +65,7 @@ static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &
         const int64_t lo = t * cs, hi = std::min<int64_t>(N, lo + cs);
         Chunk &c = ch[t];
         c.rcnt.resize(std::max<int64_t>(hi - lo, 0)), c.scnt.resize(std::max<int64_t>(hi - lo, 0));
-        std::vector<int32_t> flag(N, -1), slot(N), pat;
+        std::vector<int32_t> flag(N, -1), pat;  // one marker array per thread (N int32)
         for (int64_t k = lo; k < hi; k++) {
             flag[k] = (int32_t)k;
             pat.clear();
@@ -76,14 +76,14 @@ static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &
                     flag[i] = (int32_t)k;
                 }
             std::sort(pat.begin(), pat.end());
-            for (size_t q = 0; q < pat.size(); q++) slot[pat[q]] = (int32_t)q;  // row-local, rebased later
             c.rc.insert(c.rc.end(), pat.begin(), pat.end());
             c.rcnt[k - lo] = (int32_t)pat.size();
             int32_t ns = 0;
             for (int64_t p = Kp.ptr[r]; p < Kp.ptr[r + 1]; p++) {
                 const int32_t i = pinv[Kp.ind[p]];
                 if (i > k) continue;
-                c.tgt.push_back(i == k ? -1 : slot[i]);
+                // row-local slot of i in the sorted pattern (rebased later)
+                c.tgt.push_back(i == k ? -1 : (int32_t)(std::lower_bound(pat.begin(), pat.end(), i) - pat.begin()));
                 c.src.push_back((uint32_t)p);
                 ns++;
             }

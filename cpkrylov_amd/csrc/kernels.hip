@@ -1026,7 +1026,10 @@ __device__ __forceinline__ void levels_owned(SweepLds &S, int nl, int nr, bool s
 #define CPK_LEVEL_GROUP 1
 #endif
 #ifndef CPK_UPPER_GROUP
-#define CPK_UPPER_GROUP 1  // the same in the upper-round and last-round kernels' one-wave levels
+// The same grouping in the upper-round and last-round kernels' one-wave levels: bit-identical,
+// but measured slower there (S10 backward 0.1835 vs 0.1778 ms, profiles/r03_upper_group_ab_v9.txt),
+// so off by default.
+#define CPK_UPPER_GROUP 0
 #endif
 __device__ __forceinline__ double row_next_lane(double x) {  // lane i + 1 of its 16-lane row (15: 0)
     const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x101, 0xf, 0xf, true);
