@@ -93,6 +93,7 @@ struct EngineOpts {
     bool no_fused_resid = false;  // no_fused_resid:     refinement residual as its own SpMV
     bool fused_tail_launch = false;  // fused_tail_launch: rows above round 0 by a residual launch
     bool r0_stride = false;       // r0_stride:          round-0 blocks by stride, not by cost
+    int r0_xcd_chunk = 16;        // r0_xcd_chunk:       K > 0: runs of K consecutive round-0 blocks share an XCD
     bool tsolve_global = false;   // tsolve_global:      separator records read from HBM
     bool tsolve_onepass = false;  // tsolve_onepass:     one-pass separator solve
     bool no_piggy = false;        // no_piggy:           cpminres alpha by its own allreduce

@@ -108,20 +108,23 @@ HCsr assemble_kp(const HCsr &A, const HCsr &B, const HCsr &C) {
     HCsr K;
     K.nrows = K.ncols = N;
     K.ptr.assign(N + 1, 0);
-    K.ind.reserve(A.nnz() + 2 * B.nnz() + C.nnz());
-    K.val.reserve(K.ind.capacity());
-    for (int64_t i = 0; i < n; i++) {
-        for (int64_t p = A.ptr[i]; p < A.ptr[i + 1]; p++) K.ind.push_back(A.ind[p]), K.val.push_back(A.val[p]);
-        for (int64_t p = Bt.ptr[i]; p < Bt.ptr[i + 1]; p++)
-            K.ind.push_back((int32_t)(n + Bt.ind[p])), K.val.push_back(Bt.val[p]);
-        K.ptr[i + 1] = (int64_t)K.ind.size();
-    }
-    for (int64_t i = 0; i < m; i++) {
-        for (int64_t p = B.ptr[i]; p < B.ptr[i + 1]; p++) K.ind.push_back(B.ind[p]), K.val.push_back(B.val[p]);
-        for (int64_t p = C.ptr[i]; p < C.ptr[i + 1]; p++)
-            K.ind.push_back((int32_t)(n + C.ind[p])), K.val.push_back(C.val[p]);
-        K.ptr[n + i + 1] = (int64_t)K.ind.size();
-    }
+    for (int64_t i = 0; i < n; i++) K.ptr[i + 1] = K.ptr[i] + (A.ptr[i + 1] - A.ptr[i]) + (Bt.ptr[i + 1] - Bt.ptr[i]);
+    for (int64_t i = 0; i < m; i++)
+        K.ptr[n + i + 1] = K.ptr[n + i] + (B.ptr[i + 1] - B.ptr[i]) + (C.ptr[i + 1] - C.ptr[i]);
+    K.ind.resize(K.ptr[N]);
+    K.val.resize(K.ptr[N]);
+    // row i: [A row; B' row shifted by n] (i < n), [B row; C row shifted by n] (i >= n)
+    auto put = [&](int64_t row, const HCsr &L, int64_t li, int32_t lshift, const HCsr &R, int64_t ri, int32_t rshift) {
+        int64_t q = K.ptr[row];
+        for (int64_t p = L.ptr[li]; p < L.ptr[li + 1]; p++, q++) K.ind[q] = L.ind[p] + lshift, K.val[q] = L.val[p];
+        for (int64_t p = R.ptr[ri]; p < R.ptr[ri + 1]; p++, q++) K.ind[q] = R.ind[p] + rshift, K.val[q] = R.val[p];
+    };
+    parallel_for(N, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; i++) {
+            if (i < n) put(i, A, i, 0, Bt, i, (int32_t)n);
+            else put(i, B, i - n, 0, C, i - n, (int32_t)n);
+        }
+    });
     return K;
 }
 

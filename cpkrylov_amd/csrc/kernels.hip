@@ -1991,18 +1991,26 @@ void plan_round0(Ctx &c, DFactor &d, const int64_t *kps_ptr) {
         // min over slots of (load + cost) / speed, the least loaded workgroup of each slot a heap top
         const int64_t per_slot = std::max<int64_t>(1, (int64_t)cus * 4);
         const int nslot = (int)std::min<int64_t>(kR0Slots, (G + per_slot - 1) / per_slot);
+        // XCD affinity (option r0_xcd_chunk = K): runs of K consecutive blocks go to the
+        // workgroups of one XCD (workgroup g on XCD g mod 8, the dispatcher's round robin -- a
+        // speed assumption only), so the 128-byte lines two neighbouring blocks share in every
+        // stream, and the input lines their perm gathers share, are fetched into one L2
+        const int64_t K = c.opts.r0_xcd_chunk;
+        const int nxcd = (K > 0 && G % 8 == 0) ? 8 : 1;
         using HE = std::pair<double, int32_t>;  // (load, workgroup)
         auto gt = [](const HE &a, const HE &b) { return a.first > b.first || (a.first == b.first && a.second > b.second); };
-        std::vector<std::vector<HE>> heaps(nslot);
-        for (int64_t g = 0; g < G; g++) heaps[(size_t)std::min<int64_t>(g / per_slot, nslot - 1)].push_back({0.0, (int32_t)g});
+        std::vector<std::vector<HE>> heaps((size_t)nxcd * nslot);
+        for (int64_t g = 0; g < G; g++)
+            heaps[(size_t)(g % nxcd) * nslot + std::min<int64_t>(g / per_slot, nslot - 1)].push_back({0.0, (int32_t)g});
         for (auto &h : heaps) std::make_heap(h.begin(), h.end(), gt);
         std::vector<int32_t> owner(nb);
         for (int64_t i : ord) {
+            const int x0 = nxcd > 1 ? (int)((i / K) % nxcd) * nslot : 0;
             int best = -1;
             double bt = 0.0;
-            for (int s = 0; s < nslot; s++) {
+            for (int s = x0; s < x0 + nslot; s++) {
                 if (heaps[s].empty()) continue;
-                const double t = (heaps[s].front().first + cost[i]) / kR0SlotSpeed[v == 2 ? 1 : 0][s];
+                const double t = (heaps[s].front().first + cost[i]) / kR0SlotSpeed[v == 2 ? 1 : 0][s - x0];
                 if (best < 0 || t < bt) best = s, bt = t;
             }
             auto &h = heaps[best];

@@ -87,12 +87,12 @@ void set_engine_option(EngineOpts &o, const std::string &name, const std::string
         if (end == value.c_str() || *end != '\0' || !std::isfinite(v) || !(v > 0 && v < 1))
             throw Error(CPK_ERR_ARGS, "engine option split_tol must be a number in (0, 1), got '" + value + "'");
         o.split_tol = v;
-    } else if (name == "batch") {
+    } else if (name == "batch" || name == "r0_xcd_chunk") {
         char *end = nullptr;
         const long v = strtol(value.c_str(), &end, 10);
         if (end == value.c_str() || *end != '\0' || v < 0 || v > 4096)
-            throw Error(CPK_ERR_ARGS, "engine option batch must be an integer in [0, 4096], got '" + value + "'");
-        o.batch = (int)v;
+            throw Error(CPK_ERR_ARGS, "engine option " + name + " must be an integer in [0, 4096], got '" + value + "'");
+        (name == "batch" ? o.batch : o.r0_xcd_chunk) = (int)v;
     } else {
         throw Error(CPK_ERR_ARGS, "unknown engine option '" + name + "'");
     }
@@ -108,6 +108,7 @@ std::string get_engine_option(const EngineOpts &o, const std::string &name) {
         return b;
     }
     if (name == "batch") return std::to_string(o.batch);
+    if (name == "r0_xcd_chunk") return std::to_string(o.r0_xcd_chunk);
     throw Error(CPK_ERR_ARGS, "unknown engine option '" + name + "'");
 }
 
@@ -122,6 +123,7 @@ EngineOpts engine_opts_from_env() {
     from("sweep");
     from("split_tol");
     from("batch");
+    from("r0_xcd_chunk");
     return o;
 }
 
@@ -135,6 +137,7 @@ uint64_t engine_opts_hash(const EngineOpts &o) {
     mix(sweep_str(o.sweep));
     mix(get_engine_option(o, "split_tol"));
     mix(std::to_string(o.batch));
+    mix(std::to_string(o.r0_xcd_chunk));
     return h;
 }
 

@@ -8,6 +8,8 @@
 //     are independent leaves), then order the Schur-complement graph S = pattern(C + B G^-1 B')
 //     by nested dissection (large) or minimum degree (small);
 //   - otherwise nested dissection / minimum degree on the whole graph of Kp.
+#include <chrono>
+#include <cstdio>
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
@@ -107,14 +109,17 @@ namespace {
 struct Nd {
     const HCsr &g;
     std::unique_ptr<std::atomic<int32_t>[]> label;  // subset id of each node
-    std::vector<int32_t> dist;                       // BFS distance (valid when stamp matches)
-    std::vector<int32_t> stamp;
+    // BFS distance and visit stamp of each node, twice: the pseudo-peripheral search keeps the
+    // best start's BFS in one copy while it tries a candidate in the other
+    std::vector<int32_t> dist_[2], stamp_[2];
+    std::vector<int32_t> &dist = dist_[0], &stamp = stamp_[0];
     std::vector<int32_t> out;
     std::atomic<int32_t> next_label{1}, next_stamp{0};
     std::atomic<int> spare_threads;
     int leaf;
     Nd(const HCsr &gg, int lf, int threads)
-        : g(gg), label(new std::atomic<int32_t>[gg.nrows]), dist(gg.nrows, 0), stamp(gg.nrows, -1), out(gg.nrows),
+        : g(gg), label(new std::atomic<int32_t>[gg.nrows]), dist_{std::vector<int32_t>(gg.nrows, 0), std::vector<int32_t>(gg.nrows, 0)},
+          stamp_{std::vector<int32_t>(gg.nrows, -1), std::vector<int32_t>(gg.nrows, -1)}, out(gg.nrows),
           spare_threads(threads - 1), leaf(lf) {
         for (int64_t i = 0; i < gg.nrows; i++) label[i].store(0, std::memory_order_relaxed);
     }
@@ -124,23 +129,24 @@ struct Nd {
     // BFS within nodes of `lab` from `src`; fills `bfs` in visit order, returns eccentricity.
     // Nodes of other subsets (possibly relabelled concurrently by another thread) never carry
     // `lab`, so reading their labels is harmless.
-    int32_t bfs(int32_t src, int32_t lab, std::vector<int32_t> &bfs_order, int32_t &st) {
+    int32_t bfs(int32_t src, int32_t lab, std::vector<int32_t> &bfs_order, int32_t &st, int buf = 0) {
+        std::vector<int32_t> &dst = dist_[buf], &stm = stamp_[buf];
         st = next_stamp.fetch_add(1, std::memory_order_relaxed) + 1;
         bfs_order.clear();
         bfs_order.push_back(src);
-        stamp[src] = st;
-        dist[src] = 0;
+        stm[src] = st;
+        dst[src] = 0;
         for (size_t h = 0; h < bfs_order.size(); h++) {
             int32_t v = bfs_order[h];
             for (int64_t p = g.ptr[v]; p < g.ptr[v + 1]; p++) {
                 int32_t w = g.ind[p];
-                if (lab_of(w) != lab || stamp[w] == st) continue;
-                stamp[w] = st;
-                dist[w] = dist[v] + 1;
+                if (lab_of(w) != lab || stm[w] == st) continue;
+                stm[w] = st;
+                dst[w] = dst[v] + 1;
                 bfs_order.push_back(w);
             }
         }
-        return dist[bfs_order.back()];
+        return dst[bfs_order.back()];
     }
 
     void emit(std::vector<int32_t> &nodes, int64_t pos) {
@@ -191,18 +197,19 @@ struct Nd {
             run_comps(comps, 0, pos);
             return;
         }
-        // pseudo-peripheral node
+        // pseudo-peripheral node; the best start's BFS stays in buffer `cur`, so it is not redone
         int32_t start = order.back();
-        int32_t ecc = bfs(start, lab, order, st);
+        int cur = 0;
+        int32_t ecc = bfs(start, lab, order, st, cur);
         for (int it = 0; it < 4; it++) {
             int32_t cand = order.back();
             std::vector<int32_t> o2;
             int32_t st2;
-            int32_t e2 = bfs(cand, lab, o2, st2);
+            int32_t e2 = bfs(cand, lab, o2, st2, 1 - cur);
             if (e2 <= ecc) break;
-            ecc = e2, start = cand, order.swap(o2);
+            ecc = e2, start = cand, order.swap(o2), st = st2, cur = 1 - cur;
         }
-        bfs(start, lab, order, st);
+        const std::vector<int32_t> &dist = dist_[cur], &stamp = stamp_[cur];
         if (ecc < 2) {  // too shallow to dissect
             emit(nodes, pos);
             return;
@@ -281,6 +288,15 @@ std::vector<int32_t> nested_dissection(const HCsr &g, int leaf_size) {
 }
 
 std::vector<int32_t> order_kp(const HCsr &Kp, int64_t n, int *kind_out) {
+    // CPK_TIMING=1: sub-phase wall times on stderr (diagnostic)
+    const bool timing = getenv("CPK_TIMING") != nullptr;
+    auto t = std::chrono::steady_clock::now();
+    auto sub_lap = [&](const char *what) {
+        if (!timing) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[cpk]   %-40s %8.3f s\n", what, std::chrono::duration<double>(now - t).count());
+        t = now;
+    };
     const int64_t N = Kp.nrows, m = N - n;
     bool g_diag = true;
     for (int64_t i = 0; i < n && g_diag; i++)
@@ -306,7 +322,9 @@ std::vector<int32_t> order_kp(const HCsr &Kp, int64_t n, int *kind_out) {
                 int32_t c = Kp.ind[p];
                 if (c >= n && c - n != i) edges.emplace_back((int32_t)i, c - (int32_t)n);
             }
+        sub_lap("order: Schur-graph edges");
         HCsr S = graph_from_edges(m, edges);
+        sub_lap("order: Schur graph");
         std::vector<int32_t> os;
         if (m <= kMdLimit) {
             os = min_degree(S);
@@ -315,6 +333,7 @@ std::vector<int32_t> order_kp(const HCsr &Kp, int64_t n, int *kind_out) {
             os = nested_dissection(S, kNdLeaf);
             *kind_out = ORD_GFIRST_ND;
         }
+        sub_lap("order: dissection");
         for (int64_t i = 0; i < n; i++) perm[i] = (int32_t)i;
         for (int64_t i = 0; i < m; i++) perm[n + i] = (int32_t)(n + os[i]);
     } else {

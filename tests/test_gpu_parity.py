@@ -314,18 +314,19 @@ def test_precond_apply_fused_residual(gpu_ctx, name, sweep):
 
 def test_precond_apply_round0_assignment(gpu_ctx):
     """Round 0's blocks run in the host's cost-balanced assignment to the persistent launch's
-    workgroups (default) or every G-th block per workgroup (engine option r0_stride): which
-    workgroup runs a block changes nothing in it -- the same bits either way, and as the oracle
-    (forward, fused-residual forward and backward variants: one refinement step).  1M dofs:
-    more round-0 blocks than the launch has workgroups, so the assignment exists."""
+    workgroups (default), the same with runs of consecutive blocks on one XCD (engine option
+    r0_xcd_chunk) or every G-th block per workgroup (engine option r0_stride): which workgroup
+    runs a block changes nothing in it -- the same bits every way, and as the oracle (forward,
+    fused-residual forward and backward variants: one refinement step).  1M dofs: more round-0
+    blocks than the launch has workgroups, so the assignment exists."""
     import cpkrylov_amd as cpk
     from cpkrylov_amd.synthetic import saddle_system
     S = saddle_system(N=1_000_000, seed=7)
     G, B, C = S["G"], S["B"], S["C"]
     z = np.random.default_rng(29).standard_normal(G.shape[0] + B.shape[0])
     ys = []
-    for stride in (False, True):
-        with cpk.engine_options(r0_stride=stride):
+    for stride, chunk in ((False, 0), (False, 16), (False, 3), (True, 0)):
+        with cpk.engine_options(r0_stride=stride, r0_xcd_chunk=chunk):
             M = cpk.opLDL2(G, B, -C)
         M.nitref, M.force_itref = 1, True
         ys.append(M * z)
@@ -336,7 +337,9 @@ def test_precond_apply_round0_assignment(gpu_ctx):
     L, D, perm = M.export_factors()
     Mo = O.LDL2(G, B, -C, factors=(L, D, perm))
     Mo.set(nitref=1.0, force_itref=1.0)
-    assert np.array_equal(ys[0], ys[1]) and np.array_equal(ys[0], Mo @ z)
+    yo = Mo @ z
+    for y in ys:
+        assert np.array_equal(y, yo)
 
 
 @pytest.mark.parametrize("name", ["cvxqp1_m", "cvxqp2_s", "synthetic"])

@@ -2,8 +2,9 @@
 
 CPK_COMM=null gives the context a communicator without peers: collectives are no-ops, so the
 numbers are meaningless but the kernels are exactly one rank's share of the P-way solve.
-Prints, per (P, rank): the local rows, kernel timings (cpk_profile_kernels) and the wall time
-per iteration of a 20-iteration cpminres call (collective latency NOT included).
+Prints, per (P, rank): the local rows, the construction time of the rank's preconditioner
+(ptime, and a refactorization with the same values), kernel timings (cpk_profile_kernels) and
+the wall time per iteration of a 20-iteration cpminres call (collective latency NOT included).
 """
 import ctypes as C
 import json
@@ -31,7 +32,10 @@ for P, r, sw in runs:
         os.environ["CPK_SWEEP"] = sw
     ctx = cpk.Context(device=0, rank=r, nranks=P) if P > 1 else cpk.Context(device=0)
     A, B, Cm, G = (cpk.Matrix(S[k], ctx) for k in ("Q", "B", "C", "G"))
+    t0 = time.perf_counter()
     M = cpk.opLDL2(G, B, -S["C"], ctx=ctx)
+    construct_s, ptime_s = time.perf_counter() - t0, M.ptime
+    refactor_s = M.refactor(S["G"], S["B"], -S["C"])
     M.nitref, M.force_itref = 1, True
     dofs, n_loc = M.local_dofs()
     p = _lib.Profile()
@@ -59,6 +63,7 @@ for P, r, sw in runs:
     except cpk.CpkError as e:
         err = str(e)[:120]
     print(json.dumps({"P": P, "rank": r, "sweep": sw, "N_loc": len(dofs), "nrounds": M.info["nrounds"],
+                      "construct_s": round(construct_s, 3), "ptime_s": round(ptime_s, 3), "refactor_s": round(refactor_s, 4),
                       "spmv_us": round(p.spmv_ms * 1e3, 1), "resid_us": round(p.resid_ms * 1e3, 1),
                       "fwd_us": round(p.fwd_ms * 1e3, 1), "bwd_us": round(p.bwd_ms * 1e3, 1),
                       "apply_us": round(p.apply_ms * 1e3, 1), "niters": int(st.niters),
