@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <atomic>
 #include <cstdlib>
+#include <memory>
 #include <numeric>
 #include <thread>
 
@@ -300,42 +301,39 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
                         const std::vector<int64_t> *extra_bwd, bool detach) {
     if (SUB0 <= 0 || SUB0 > CAP0) SUB0 = CAP0;
     const int64_t N = f.N;
+    SubClock clk;
     Schedule s;
     s.N = N;
     // Node weights: a block is staged in LDS when it holds at most R rows, at most CAP forward
     // entries (rows of L) and at most CAP backward entries (columns of L).  With
     // wt(v) = max(CAP/R, fwd(v), bwd(v)), a cluster of total weight <= CAP meets all three.
-    std::vector<int64_t> ent(N), wt0(N), wt1(N), ent_fwd;
-    {
-        const int64_t u0 = std::max<int64_t>(1, CAP0 / std::max<int64_t>(R0, 1));
-        const int64_t u1 = std::max<int64_t>(1, CAP1 / std::max<int64_t>(R1, 1));
-        std::vector<int64_t> &fl = ent_fwd;
-        fl.assign(N, 0);
-        for (int32_t i : f.Li) fl[i]++;
-        for (int64_t v = 0; v < N; v++) {
-            ent[v] = std::max(fl[v], f.Lp[v + 1] - f.Lp[v] + (extra_bwd ? (*extra_bwd)[v] : 0));
-            wt0[v] = std::max(u0, ent[v]);
-            wt1[v] = std::max(u1, ent[v]);
-        }
-    }
+    std::vector<int32_t> ent(N), nfwd(N, 0);  // nfwd: forward entries (row counts of L)
+    for (int32_t i : f.Li) nfwd[i]++;
+    parallel_for(N, [&](int64_t lo, int64_t hi) {
+        for (int64_t v = lo; v < hi; v++)
+            ent[v] = (int32_t)std::max<int64_t>(nfwd[v], f.Lp[v + 1] - f.Lp[v] + (extra_bwd ? (*extra_bwd)[v] : 0));
+    });
+    const int64_t u0 = std::max<int64_t>(1, CAP0 / std::max<int64_t>(R0, 1));
+    const int64_t u1 = std::max<int64_t>(1, CAP1 / std::max<int64_t>(R1, 1));
+    auto wt0 = [&](int64_t v) { return std::max<int64_t>(u0, ent[v]); };
+    auto wt1 = [&](int64_t v) { return std::max<int64_t>(u1, ent[v]); };
     auto capof = [&](int32_t r) { return r == 0 ? CAP0 : CAP1; };
-    // children lists
-    std::vector<int64_t> cptr(N + 2, 0);
-    for (int64_t v = 0; v < N; v++)
-        if (f.parent[v] >= 0) cptr[f.parent[v] + 1]++;
+    // children lists and the tree height (for reporting), one ascending pass each
+    std::vector<int32_t> cptr(N + 2, 0), height(N, 0);
+    for (int64_t v = 0; v < N; v++) {
+        const int32_t p = f.parent[v];
+        if (p >= 0) cptr[p + 1]++, height[p] = std::max(height[p], height[v] + 1);
+        s.depth = std::max<int64_t>(s.depth, height[v] + 1);
+    }
     for (int64_t v = 0; v < N; v++) cptr[v + 1] += cptr[v];
     std::vector<int32_t> kids(cptr[N]);
     {
-        std::vector<int64_t> nx(cptr.begin(), cptr.begin() + N);
+        std::vector<int32_t> nx(cptr.begin(), cptr.begin() + N);
         for (int64_t v = 0; v < N; v++)
             if (f.parent[v] >= 0) kids[nx[f.parent[v]]++] = (int32_t)v;
     }
-    // tree height (for reporting)
-    std::vector<int32_t> height(N, 0);
-    for (int64_t v = 0; v < N; v++) {
-        if (f.parent[v] >= 0) height[f.parent[v]] = std::max(height[f.parent[v]], height[v] + 1);
-        s.depth = std::max<int64_t>(s.depth, height[v] + 1);
-    }
+    std::vector<int32_t>().swap(height);
+    clk.lap("schedule: weights, children, heights");
     std::vector<int32_t> closed_round(N, -1);  // >= 0 iff v roots a cluster
     // (1) Layer peeling: round r takes the maximal subtrees of at most R rows of the tree that
     //     remains after rounds 0..r-1.  On bushy (nested-dissection) trees the remainder
@@ -349,23 +347,24 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     // did inside the blocks, so the default keeps them in.
     std::vector<char> detached(N, 0);
     if (detach)
-        for (int64_t v = 0; v < N; v++) detached[v] = ent_fwd[v] == 0;
+        for (int64_t v = 0; v < N; v++) detached[v] = nfwd[v] == 0;
     std::vector<int32_t> alive;
     alive.reserve(N);
     for (int64_t v = 0; v < N; v++)
         if (!detached[v]) alive.push_back((int32_t)v);
     std::vector<char> is_alive(N, 0);
     for (int32_t v : alive) is_alive[v] = 1;
-    std::vector<int64_t> sz(N, 0);
-    std::vector<int32_t> root_of(N, -1);
+    // per round, written for every alive row before any read (the parent of an alive row is alive)
+    std::unique_ptr<int64_t[]> sz(new int64_t[N]);
+    std::unique_ptr<int32_t[]> root_of(new int32_t[N]);
     int32_t round = 0;
     while (!alive.empty()) {
         for (int32_t v : alive) sz[v] = 0;
-        const std::vector<int64_t> &wt = round == 0 ? wt0 : wt1;
+        const int64_t u = round == 0 ? u0 : u1;
         // round 0 peels subtrees of weight <= SUB0 and packs several of them per block
         const int64_t CAP = round == 0 ? SUB0 : capof(round);
         for (int32_t v : alive) {  // ascending: children before parents
-            sz[v] += wt[v];
+            sz[v] += std::max<int64_t>(u, ent[v]);
             if (f.parent[v] >= 0 && is_alive[f.parent[v]]) sz[f.parent[v]] += sz[v];
         }
         const size_t before = alive.size();
@@ -385,16 +384,21 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
         round++;
         if (!alive.empty() && round >= 8 && alive.size() * 2 > before) break;  // chain-like tree
     }
+    clk.lap("schedule: layer peeling");
     // (2) Greedy bottom-up clustering of what peeling left (chain-like upper trees): a node's
     //     open cluster absorbs its children's open clusters, closing the largest ones until it
     //     fits in R rows.  Peeled children are already-closed clusters.
-    std::vector<int64_t> open_size(N, 0);
-    std::vector<int32_t> open_dep(N, -1);
+    // read only for alive nodes (a peeled row's parent is peeled too), each written before its
+    // parent reads it: no initialisation, except for detached rows (leaves outside the peeling)
+    std::unique_ptr<int64_t[]> open_size(new int64_t[N]);
+    std::unique_ptr<int32_t[]> open_dep(new int32_t[N]);
+    if (detach)
+        for (int64_t v = 0; v < N; v++)
+            if (detached[v]) open_size[v] = 0, open_dep[v] = -1;
     std::vector<int32_t> tmp;
     const int64_t CAP = CAP1;
-    const std::vector<int64_t> &wt = wt1;
     for (int32_t v : alive) {
-        int64_t total = wt[v];
+        int64_t total = wt1(v);
         tmp.clear();
         for (int64_t q = cptr[v]; q < cptr[v + 1]; q++)
             if (closed_round[kids[q]] < 0) tmp.push_back(kids[q]), total += open_size[kids[q]];
@@ -418,20 +422,25 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
         if (f.parent[v] < 0) closed_round[v] = dep + 1;
     }
     // cluster membership (top-down): a non-root joins its parent's cluster
+    // and the cluster sizes (a root comes before its members, so it starts its sum)
     std::vector<int32_t> cl(N, -1);
-    for (int64_t v = N - 1; v >= 0; v--)
-        if (!detached[v]) cl[v] = closed_round[v] >= 0 ? (int32_t)v : cl[f.parent[v]];
-    std::vector<int64_t> csize(N, 0);
-    for (int64_t v = 0; v < N; v++)
-        if (cl[v] >= 0) csize[cl[v]] += (closed_round[cl[v]] == 0 ? wt0[v] : wt1[v]);
+    std::unique_ptr<int64_t[]> csize(new int64_t[N]);
     int32_t nrounds = 0;
-    for (int64_t v = 0; v < N; v++)
+    for (int64_t v = N - 1; v >= 0; v--) {
         if (closed_round[v] >= 0) nrounds = std::max(nrounds, closed_round[v] + 1);
+        if (detached[v]) continue;
+        const bool root = closed_round[v] >= 0;
+        const int32_t c = root ? (int32_t)v : cl[f.parent[v]];
+        cl[v] = c;
+        const int64_t w = closed_round[c] == 0 ? wt0(v) : wt1(v);
+        csize[c] = root ? w : csize[c] + w;
+    }
+    clk.lap("schedule: clustering");
     // pack the clusters of one round into blocks of <= R rows (clusters taken in root order)
     std::vector<std::vector<int32_t>> roots_by_round(nrounds);
     for (int64_t v = 0; v < N; v++)
         if (closed_round[v] >= 0) roots_by_round[closed_round[v]].push_back((int32_t)v);
-    std::vector<int32_t> cluster_block(N, -1);
+    int32_t *cluster_block = root_of.get();  // free after the peeling; read for cluster roots only
     int32_t nb = 0;
     s.round_ptr.assign(1, 0);
     for (int32_t r = 0; r < nrounds; r++) {
@@ -447,13 +456,14 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
         }
         s.round_ptr.push_back(nb);
     }
-    std::vector<int32_t> block(N, -1);  // -1: detached
-    for (int64_t v = 0; v < N; v++)
-        if (cl[v] >= 0) block[v] = cluster_block[cl[v]];
     // new order: detached rows (ascending), then blocks ascending (= rounds ascending), then
     // level, then old index
+    std::vector<int32_t> block(N);  // -1: detached
     std::vector<int64_t> bcount(nb + 2, 0);  // bcount[0]: detached
-    for (int64_t v = 0; v < N; v++) bcount[block[v] + 2]++;
+    for (int64_t v = 0; v < N; v++) {
+        block[v] = cl[v] >= 0 ? cluster_block[cl[v]] : -1;
+        bcount[block[v] + 2]++;
+    }
     for (int32_t b = 0; b <= nb; b++) bcount[b + 1] += bcount[b];
     s.ndet = bcount[1];
     s.blk_row.assign(bcount.begin() + 1, bcount.end());
@@ -462,6 +472,7 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
         std::vector<int64_t> nx(bcount.begin(), bcount.end() - 1);
         for (int64_t v = 0; v < N; v++) s.order[nx[block[v] + 1]++] = (int32_t)v;
     }
+    clk.lap("schedule: blocks and order");
     // intra-block levels, blocks in parallel: a block's rows are disjoint from every other
     // block's, and in ascending old index (a topological order: L's columns point to rows of
     // larger index), so level[j] is final when column j is visited
@@ -493,6 +504,7 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
         s.max_levels = std::max<int64_t>(s.max_levels, s.blk_lvl[b + 1] - s.blk_lvl[b]);
     }
     s.lvl_row.push_back(N);
+    clk.lap("schedule: intra-block levels");
     return s;
 }
 

@@ -2,7 +2,10 @@
 // that replaces MATLAB's ldl() inside opLDL2 (ops/opLDL2.m:81-86).
 #pragma once
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -61,6 +64,17 @@ void parallel_for(int64_t n, F f, int64_t grain = 4096) {
     f(int64_t(0), std::min(n, chunk));
     for (auto &x : th) x.join();
 }
+// CPK_TIMING=1: wall times of the sub-phases of a host phase on stderr (diagnostic)
+struct SubClock {
+    bool on = getenv("CPK_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(const char *what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[cpk]   %-40s %8.3f s\n", what, std::chrono::duration<double>(now - t).count());
+        t = now;
+    }
+};
 // building blocks (exposed for tests)
 std::vector<int32_t> min_degree(const HCsr &graph);
 std::vector<int32_t> nested_dissection(const HCsr &graph, int leaf_size);

@@ -64,6 +64,7 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
                   const std::vector<std::vector<BwdExtra>> *extra, std::vector<int32_t> *fsrc,
                   std::vector<int32_t> *bsrc) {
     const int64_t N = f.N;
+    SubClock clk;
     auto K = [&](int64_t q) { return key ? (*key)[q] : q; };
     int64_t nextra = 0;
     if (extra)
@@ -102,6 +103,7 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
                 }
             });
     }
+    clk.lap("layout: forward rows");
     // structure only (the device numeric phase fills the values): no host value arrays, the
     // device ones are zeroed in place
     std::vector<double> fval(vals ? nf : 0, 0.0);
@@ -133,6 +135,7 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
             }
         }
     });
+    clk.lap("layout: backward rows");
     if (fsrc) *fsrc = std::move(fidx);
     if (bsrc) *bsrc = std::move(bidx);
     // rounds whose blocks all fit the upper-round staging image (sptrsv_upper_kernel)
@@ -146,6 +149,7 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
         }
     // padding entries: clamped, unconditional loads may touch one entry past a block's end
     fcol.resize(fcol.size() + kFactorPadEntries, 0), bcol.resize(bcol.size() + kFactorPadEntries, 0);
+    clk.lap("layout: round fits, padding");
     d.fptr.upload(fptr);
     d.fcol.upload(fcol);
     if (vals) {
@@ -185,6 +189,7 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     }
     d.meta.upload(meta);
     d.hmeta = meta;
+    clk.lap("layout: uploads, block records");
     d.round0_rows = -1;
     if (s.ndet == 0 && s.round_ptr.size() >= 2) {  // round 0 a leading, contiguous row range?
         int64_t r = 0;
@@ -216,6 +221,7 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
             d.fcol16.upload(c16);
         }
     }
+    clk.lap("layout: int16 round-0 columns");
 }
 
 // ---- SpMV launchers --------------------------------------------------------------------------

@@ -178,6 +178,7 @@ void dldl_setup(DLdl &d, const LdlSymbolic &sym, const Factor &f, const std::vec
         d.lev_long[l] = (int32_t)(mid - rows.begin());
         for (auto it = mid; it != e; ++it) d.max_long = std::max<int64_t>(d.max_long, sym.Rp[*it + 1] - sym.Rp[*it]);
     }
+    SubClock clk;
     d.lev_rows.upload(rows);
     d.Rp.upload(sym.Rp);
     d.Rc.upload(sym.Rc);
@@ -196,6 +197,7 @@ void dldl_setup(DLdl &d, const LdlSymbolic &sym, const Factor &f, const std::vec
     d.Y.alloc((size_t)std::max<int64_t>(d.nnz, 1));
     d.bad.alloc(2);
     d.ready = true;
+    clk.lap("ldl setup: uploads");
 }
 
 void dldl_assemble_kp(Ctx &c, const DLdl &d, const double *a, const double *b, const double *cc, double *kpv) {

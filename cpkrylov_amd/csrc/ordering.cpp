@@ -8,8 +8,6 @@
 //     are independent leaves), then order the Schur-complement graph S = pattern(C + B G^-1 B')
 //     by nested dissection (large) or minimum degree (small);
 //   - otherwise nested dissection / minimum degree on the whole graph of Kp.
-#include <chrono>
-#include <cstdio>
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
@@ -288,15 +286,8 @@ std::vector<int32_t> nested_dissection(const HCsr &g, int leaf_size) {
 }
 
 std::vector<int32_t> order_kp(const HCsr &Kp, int64_t n, int *kind_out) {
-    // CPK_TIMING=1: sub-phase wall times on stderr (diagnostic)
-    const bool timing = getenv("CPK_TIMING") != nullptr;
-    auto t = std::chrono::steady_clock::now();
-    auto sub_lap = [&](const char *what) {
-        if (!timing) return;
-        const auto now = std::chrono::steady_clock::now();
-        fprintf(stderr, "[cpk]   %-40s %8.3f s\n", what, std::chrono::duration<double>(now - t).count());
-        t = now;
-    };
+    SubClock clk;
+    auto sub_lap = [&](const char *what) { clk.lap(what); };
     const int64_t N = Kp.nrows, m = N - n;
     bool g_diag = true;
     for (int64_t i = 0; i < n && g_diag; i++)

@@ -13,7 +13,9 @@
 #include <cstdlib>
 #include <algorithm>
 #include <cmath>
+#include <exception>
 #include <memory>
+#include <thread>
 
 #include "dev.hpp"
 #include "dist.hpp"
@@ -67,14 +69,50 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
     pc->ordering = an.ordering;
     pc->Kp = std::move(an.Kp);
     pc->S = std::move(an.S);
-    make_dmat(pc->Kp, pc->dKp);
     for (int i = 0; i < 2; i++)  // before make_dfactor: the device layout follows the configuration
         pc->dF.sweep_rows[i] = an.sweep.rows[i], pc->dF.sweep_cap[i] = an.sweep.cap[i],
         pc->dF.sweep_threads[i] = an.sweep.threads[i];
     pc->dF.pipelined = !c.opts.no_pipe, pc->dF.no_upper = c.opts.no_upper, pc->dF.no_col16 = c.opts.no_col16;
     pc->dF.no_fused_resid = c.opts.no_fused_resid, pc->dF.fused_tail_launch = c.opts.fused_tail_launch;
     pc->dF.fuse_last = !c.opts.no_fuse_last;  // single GPU: no entries outside the factor
-    {
+    pc->no_sched = c.opts.no_sched_resid;
+    // Kp and Kp in schedule order depend only on Kp and the pivot order: they are built and
+    // uploaded on a second host thread while this one lays out and uploads the factor
+    std::vector<int64_t> kps_ptr;
+    std::exception_ptr kp_err;
+    std::thread kp_thread([&] {
+        try {
+            CPK_HIP(hipSetDevice(c.device));
+            make_dmat(pc->Kp, pc->dKp);
+            if (pc->Kp.nnz() > (int64_t)INT32_MAX) return;
+            // Kp in schedule order: row q = Kp row perm_s[q] with its entries in Kp's order, columns
+            // renumbered to schedule positions (perm_s = the relabelled factor's pivot order)
+            const std::vector<int32_t> &ps = an.F.perm;
+            const int64_t N = pc->N;
+            std::vector<int32_t> pos(N);
+            for (int64_t q = 0; q < N; q++) pos[ps[q]] = (int32_t)q;
+            HCsr ks;
+            ks.nrows = ks.ncols = N;
+            ks.ptr.assign(N + 1, 0);
+            for (int64_t q = 0; q < N; q++) ks.ptr[q + 1] = ks.ptr[q] + (pc->Kp.ptr[ps[q] + 1] - pc->Kp.ptr[ps[q]]);
+            ks.ind.resize(pc->Kp.nnz());
+            ks.val.resize(pc->Kp.nnz());
+            std::vector<int32_t> from(pc->Kp.nnz());
+            parallel_for(N, [&](int64_t lo, int64_t hi) {
+                for (int64_t q = lo; q < hi; q++) {
+                    int64_t t = ks.ptr[q];
+                    for (int64_t p = pc->Kp.ptr[ps[q]]; p < pc->Kp.ptr[ps[q] + 1]; p++, t++)
+                        ks.ind[t] = pos[pc->Kp.ind[p]], ks.val[t] = pc->Kp.val[p], from[t] = (int32_t)p;
+                }
+            });
+            make_dmat(ks, pc->dKps);
+            pc->kps_from.upload(from);
+            kps_ptr = std::move(ks.ptr);
+        } catch (...) {
+            kp_err = std::current_exception();
+        }
+    });
+    try {
         const std::vector<int64_t> key(pc->S.order.begin(), pc->S.order.end());
         if (an.device_numeric) {
             std::vector<int32_t> fsrc, bsrc;
@@ -85,45 +123,24 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
         } else {
             make_dfactor(an.F, pc->S, pc->dF, &key);
         }
+    } catch (...) {
+        kp_thread.join();
+        throw;
     }
     clk.lap("device factor layout + upload");
+    kp_thread.join();
+    if (kp_err) std::rethrow_exception(kp_err);
+    clk.lap("Kp, Kp in schedule order (overlapped)");
     if (an.device_numeric) {
         dldl_factor(c, pc->dl, pc->dKp.val.p, pc->dF);
         CPK_HIP(hipStreamSynchronize(c.stream));
         clk.lap("numeric factorization (device)");
     }
-    pc->no_sched = c.opts.no_sched_resid;
-    if (pc->Kp.nnz() <= (int64_t)INT32_MAX) {
-        // Kp in schedule order: row q = Kp row perm_s[q] with its entries in Kp's order, columns
-        // renumbered to schedule positions (perm_s = the relabelled factor's pivot order)
-        const std::vector<int32_t> &ps = an.F.perm;
-        const int64_t N = pc->N;
-        std::vector<int32_t> pos(N);
-        for (int64_t q = 0; q < N; q++) pos[ps[q]] = (int32_t)q;
-        HCsr ks;
-        ks.nrows = ks.ncols = N;
-        ks.ptr.assign(N + 1, 0);
-        for (int64_t q = 0; q < N; q++) ks.ptr[q + 1] = ks.ptr[q] + (pc->Kp.ptr[ps[q] + 1] - pc->Kp.ptr[ps[q]]);
-        ks.ind.resize(pc->Kp.nnz());
-        ks.val.resize(pc->Kp.nnz());
-        std::vector<int32_t> from(pc->Kp.nnz());
-        parallel_for(N, [&](int64_t lo, int64_t hi) {
-            for (int64_t q = lo; q < hi; q++) {
-                int64_t t = ks.ptr[q];
-                for (int64_t p = pc->Kp.ptr[ps[q]]; p < pc->Kp.ptr[ps[q] + 1]; p++, t++)
-                    ks.ind[t] = pos[pc->Kp.ind[p]], ks.val[t] = pc->Kp.val[p], from[t] = (int32_t)p;
-            }
-        });
-        make_dmat(ks, pc->dKps);
-        pc->kps_from.upload(from);
-        plan_round0(c, pc->dF, ks.ptr.data());
-    } else {
-        plan_round0(c, pc->dF, nullptr);
-    }
+    plan_round0(c, pc->dF, kps_ptr.empty() ? nullptr : kps_ptr.data());
     if (pc->dKps.nnz && pc->dF.ndet == 0) pc->xs.alloc(pc->N);
     if (pc->dKps.nnz && pc->dF.round0_rows >= 0 && pc->dF.fcol16.n > 0)
         make_tail_blk(pc->dKps, pc->dF.round0_rows, pc->kps_tail_blk, pc->kps_tail_nblk);
-    clk.lap("schedule-order Kp");
+    clk.lap("round-0 assignment");
     an.F = Factor();
     pc->F = std::move(an.F0);
     pc->w.alloc(pc->N);
@@ -333,11 +350,24 @@ uint64_t pattern_hash(const HCsr &A11, const HCsr &B, const HCsr &C22) {
 // (engine option host_factor: host numeric, the reference path of the device one's parity tests).
 Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22) {
     const bool dev = !c.opts.host_factor;
-    Analysis an = analyze(A11, B, C22, c.opts, dev);
+    // the refactorization's inputs (Kp's value sources, the sparsity hash) depend only on the
+    // matrices: computed on a second host thread during the analysis
     std::vector<int64_t> src;
-    if (dev) src = kp_value_sources(A11, B, C22);
+    uint64_t hash = 0;
+    std::thread side([&] {
+        if (dev) src = kp_value_sources(A11, B, C22);
+        hash = pattern_hash(A11, B, C22);
+    });
+    Analysis an;
+    try {
+        an = analyze(A11, B, C22, c.opts, dev);
+    } catch (...) {
+        side.join();
+        throw;
+    }
+    side.join();
     Precond *pc = precond_create(c, std::move(an));
-    pc->pattern_hash = pattern_hash(A11, B, C22);
+    pc->pattern_hash = hash;
     if (dev) pc->dl.kp_from.upload(src);
     return pc;
 }
