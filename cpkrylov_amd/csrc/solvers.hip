@@ -2021,7 +2021,10 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
     out->apply_ms = timeit([&]() { M.apply(x.p, M.n, z.p, nullptr); });
     out->apply_bytes = M.apply_bytes();
     out->fwd_launches = out->bwd_launches = (int64_t)M.dF.round_ptr.size() - 1;
-    if (last.valid) out->fwd_launches -= 1;  // the last round: one launch inside the backward count
+    if (last.valid) {  // the deferred rounds: one launch (last round or chain) inside the backward count
+        out->fwd_launches = last.from;
+        out->bwd_launches = last.from + 1;
+    }
     out->fwd_resid_ms = out->fwd_resid_bytes = 0;
     if (M.sched_path() && M.xs.n &&
         launch_sptrsv_fwd_resid(c, M.dF, M.dKps, M.kps_tail_blk.p, M.kps_tail_nblk, x.p, y.p, z.p, nullptr)) {

@@ -367,19 +367,29 @@ def test_precond_apply_fused_residual_tail_launch(gpu_ctx, name):
                                    dict(nitref=2, force_itref=False, itref_tol=1e-30)])
 def test_precond_apply_fused_last_round(gpu_ctx, name, props):
     """The last sweep round forward and backward in one launch (sptrsv_last_kernel) against two
-    launches (engine option no_fuse_last) and the oracle, in every apply path: plain, forced
-    refinement in schedule order with the fused residual, data-dependent refinement."""
+    launches (engine option no_fuse_last), and every upper round in one cooperative launch
+    (engine option upper_chain, sptrsv_chain_kernel; with small blocks, so the schedule has
+    several upper rounds), against the oracle, in every apply path: plain, forced refinement in
+    schedule order with the fused residual, data-dependent refinement."""
     import cpkrylov_amd as cpk
     G, B, C = _system_gbc(name)
     z = np.random.default_rng(31).standard_normal(G.shape[0] + B.shape[0])
-    ys = []
-    for off in (False, True):
-        with cpk.engine_options(no_fuse_last=off):
-            M = cpk.opLDL2(G, B, -C)
-        for k, v in props.items():
-            setattr(M, k, v)
-        ys.append(M * z)
-    L, D, perm = M.export_factors()
-    Mo = O.LDL2(G, B, -C, factors=(L, D, perm))
-    Mo.set(**{k: float(v) for k, v in props.items()})
-    assert np.array_equal(ys[0], ys[1]) and np.array_equal(ys[0], Mo @ z)
+    for sweep in ("", "64,192,64,128,512,512"):
+        ys = []
+        for opts in (dict(), dict(no_fuse_last=True), dict(upper_chain=True)):
+            if sweep:
+                opts["sweep"] = sweep
+            with cpk.engine_options(**opts):
+                M = cpk.opLDL2(G, B, -C)
+            for k, v in props.items():
+                setattr(M, k, v)
+            ys.append(M * z)
+            info = M.sweep_info()
+            if opts.get("upper_chain") and sweep:
+                assert info["rounds"] >= 3 and info["chain_grid"] > 0, info
+        L, D, perm = M.export_factors()
+        Mo = O.LDL2(G, B, -C, factors=(L, D, perm))
+        Mo.set(**{k: float(v) for k, v in props.items()})
+        yo = Mo @ z
+        for y in ys:
+            assert np.array_equal(y, yo)
