@@ -83,7 +83,9 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     for (int32_t i : f.Li) fptr[i + 1]++;
     for (int64_t i = 0; i < N; i++) fptr[i + 1] += fptr[i];
     const int64_t nf = (int64_t)f.Li.size();
-    std::vector<int32_t> fcol(nf), fidx(nf);
+    std::vector<int32_t> fcol, fidx(nf);
+    fcol.reserve((size_t)nf + kFactorPadEntries);  // the padding below appends without a reallocation
+    fcol.resize(nf);
     {
         std::vector<uint32_t> nx(fptr.begin(), fptr.end() - 1);
         for (int64_t j = 0; j < N; j++)
@@ -116,7 +118,9 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     std::vector<uint32_t> bptr(N + 1, 0);
     for (int64_t j = 0; j < N; j++)
         bptr[j + 1] = bptr[j] + (uint32_t)(f.Lp[j + 1] - f.Lp[j]) + (uint32_t)(extra ? (*extra)[j].size() : 0);
-    std::vector<int32_t> bcol(d.nnz), bidx(bsrc ? d.nnz : 0);
+    std::vector<int32_t> bcol, bidx(bsrc ? d.nnz : 0);
+    bcol.reserve((size_t)d.nnz + kFactorPadEntries);
+    bcol.resize(d.nnz);
     const bool bvals = vals || nextra > 0;
     std::vector<double> bval(bvals ? d.nnz : 0, 0.0);
     parallel_for(N, [&](int64_t lo, int64_t hi) {  // rows (columns of L) sort independently

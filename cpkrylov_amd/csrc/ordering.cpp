@@ -167,8 +167,11 @@ struct Nd {
         fb();
     }
 
-    // order the nodes of subset `nodes` (all carry label `lab`) into out[pos, pos + |nodes|)
-    void run(std::vector<int32_t> nodes, int32_t lab, int64_t pos) {
+    // order the nodes of subset `nodes` (all carry label `lab`) into out[pos, pos + |nodes|).
+    // bfs_ordered: the subset is connected and `nodes` is already its BFS order from nodes[0]
+    // (the near half of a dissection: the parent's BFS restricted to it), so the component
+    // search is skipped -- it would visit the same nodes in the same order
+    void run(std::vector<int32_t> nodes, int32_t lab, int64_t pos, bool bfs_ordered = false) {
         std::vector<int32_t> order;
         int32_t st = 0;
         if ((int64_t)nodes.size() <= leaf) {
@@ -176,7 +179,8 @@ struct Nd {
             return;
         }
         // split into connected components first (one linear pass over the subset)
-        bfs(nodes[0], lab, order, st);
+        if (bfs_ordered) order = nodes;
+        else bfs(nodes[0], lab, order, st);
         if (order.size() < nodes.size()) {
             std::vector<std::pair<int32_t, std::vector<int32_t>>> comps;
             const int32_t stamp0 = st;  // this subset's later BFS get newer stamps
@@ -249,7 +253,9 @@ struct Nd {
         const int64_t pa = pos, pb = pos + (int64_t)a.size(), ps = pb + (int64_t)b.size();
         emit(sep, ps);
         const size_t na = std::min(a.size(), b.size());
-        both(na, [&] { run(std::move(a), la, pa); }, [&] { run(std::move(b), lb, pb); });
+        // part A (levels < s, and level-s nodes without a neighbour at s + 1) is connected through
+        // the BFS tree and listed in BFS order from `start`; part B may fall apart
+        both(na, [&] { run(std::move(a), la, pa, true); }, [&] { run(std::move(b), lb, pb); });
     }
 
     // components [i, end) into consecutive output ranges starting at pos

