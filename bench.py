@@ -201,12 +201,11 @@ def main():
     gbs = lambda byts, ms: byts / (ms * 1e-3) / 1e9  # noqa: E731
     # the dominant kernel: the triangular sweeps of one LDL' solve (forward + backward, every
     # round: sptrsv_pipe_kernel for round 0, sptrsv_upper_kernel above and sptrsv_last_kernel for
-    # the last round's forward + backward, or all upper rounds in one sptrsv_chain_kernel), 2 per M*z
+    # the last round's forward + backward), 2 per M*z
     sweep_ms, sweep_bytes = prof.fwd_ms + prof.bwd_ms, prof.fwd_bytes + prof.bwd_bytes
     achieved = gbs(sweep_bytes, sweep_ms)
     roofline = {"bound": "hbm", "kernel": "sptrsv_pipe_kernel (round 0) + sptrsv_upper_kernel / sptrsv_last_kernel "
-                                          "or sptrsv_chain_kernel (upper rounds): one LDL' solve (forward + backward "
-                                          "sweep, all rounds)",
+                                          "(upper rounds): one LDL' solve (forward + backward sweep, all rounds)",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "bytes_per_launch": sweep_bytes,
                 "avg_ms": round(sweep_ms, 5), "launches": int(prof.fwd_launches) + int(prof.bwd_launches)}

@@ -602,7 +602,7 @@ int cpk_pc_sweep_info(cpk_pc M, int64_t *info) {
     const DFactor &F = M->p->dF;
     const int64_t nr = (int64_t)F.round_ptr.size() - 1;
     const int64_t r0 = nr >= 1 ? F.round_ptr[1] - F.round_ptr[0] : 0;
-    const int64_t v[8] = {nr, r0, F.nblk - r0, F.agrid[0], F.agrid[1], F.agrid[2], F.pipelined ? 1 : 0, chain_grid(F)};
+    const int64_t v[8] = {nr, r0, F.nblk - r0, F.agrid[0], F.agrid[1], F.agrid[2], F.pipelined ? 1 : 0, 0};
     std::memcpy(info, v, sizeof v);
     API_END
 }

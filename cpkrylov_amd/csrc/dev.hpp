@@ -100,7 +100,6 @@ struct EngineOpts {
     bool no_halo_merge = false;   // no_halo_merge:      cpminres beta by its own allreduce
     bool no_graph = false;        // no_graph:           no hipGraph capture of iterations
     bool no_fuse_last = false;    // no_fuse_last:       the last sweep round as two launches
-    bool upper_chain = false;     // upper_chain:        the upper rounds in one cooperative launch
     bool dist_graph = true;       // dist_graph:         capture collectives in the graphs
     int batch = 0;                // batch:              fixed iterations per graph (0: adaptive)
     bool profile_fwd_nolevels = false;  // profile_fwd_nolevels: diagnostic (cpk_profile_kernels)
@@ -172,7 +171,6 @@ struct DFactor {
     // engine options of the preconditioner's context when it was built (launch-time paths)
     bool no_fused_resid = false, fused_tail_launch = false;
     bool fuse_last = false;  // single GPU, no entries outside the factor: the last round fwd + bwd in one launch
-    bool chain = false;      // and the upper rounds in one cooperative launch (sptrsv_chain_kernel)
     int64_t round0_rows = -1;  // round 0 is the rows [0, round0_rows) (-1: not a leading row range)
     std::vector<int32_t> hmeta;  // host copy of meta
     // round-0 blocks assigned to the persistent launch's workgroups by modelled cost (plan_round0),
@@ -238,11 +236,9 @@ struct FwdIn {
     int sched_in = 0;
     double *xs = nullptr;
     bool valid = false;
-    int64_t from = 0;  // the first deferred round (the last round alone, or 1: the chain launch)
+    int64_t from = 0;  // the deferred round (the last one)
 };
 bool fuse_last_ok(const DFactor &F);
-// workgroups of the cooperative upper-round launch (sptrsv_chain_kernel), 0 when it does not apply
-int chain_grid(const DFactor &F);
 // defer (optional): the last round is left to the backward sweep (sptrsv_last_kernel solves it
 // forward and backward in one launch); *defer then says how, for launch_sptrsv_bwd's last
 // pk (optional, distributed): the separator payload packed by the write-back; returns whether

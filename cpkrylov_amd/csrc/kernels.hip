@@ -3,7 +3,6 @@
 // (-ffp-contract=off), and every row sum runs in increasing column order from 0, the
 // accumulation order of MATLAB's sparse mtimes and column-oriented sparse mldivide, so the
 // per-row results equal the CPU oracle bit for bit given equal inputs.
-#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1287,8 +1286,7 @@ __device__ __forceinline__ void pack_inputs(const PackArgs &pk, int64_t e) {
 // issues all of its row and entry loads at once, then all of its gathers (input through perm,
 // w of outside-block columns) with clamped, unconditional addresses, so staging costs about two
 // dependent round trips instead of one per predicated slot.  Fold and levels as before.
-// one block of an upper round (the body of sptrsv_upper_kernel and of sptrsv_chain_kernel's
-// round phases); ends with the block's write-back, so LDS is free after a workgroup barrier
+// one block of an upper round (the body of sptrsv_upper_kernel); ends with the block's write-back
 template <int TPB, int RPU, int EPU, bool BWD, bool ADD>
 __device__ __forceinline__ void upper_block(
     char *smem, const BlkMeta m, const int32_t *__restrict__ lvl_row,
@@ -1513,108 +1511,6 @@ __global__ __launch_bounds__(TPB) void sptrsv_last_kernel(
     if (skip(run, active)) return;
     last_block<TPB, RPU, EPU, ADD>(smem, meta[blk0 + blockIdx.x], lvl_row, fptr, fcol, fval, bptr, bcol, bval, D, perm,
                                    xin, neg_from, sched_in, xs, w, out, ys);
-}
-
-// ---- the upper rounds in one cooperative launch (single GPU) ---------------------------------
-// Forward rounds 1 .. R-2, the fused last round, backward rounds R-2 .. 1: the blocks of each
-// phase spread over the grid (workgroup g takes blocks g, g + G, ...), a grid barrier between
-// phases (cooperative groups; the runtime admits the launch only when every workgroup is
-// resident, so the barrier cannot wait on a workgroup that never starts).  The barrier orders
-// and publishes the phase's writes at device scope as a kernel boundary does; the blocks run
-// upper_block / last_block, the bodies of the per-round kernels: bit-identical, and 2(R-2)
-// launches fewer per solve.
-constexpr int kChainMaxRounds = 16;
-struct ChainArgs {
-    int nrounds = 0;                        // R: rounds 1 .. R-1 run here
-    int64_t rp[kChainMaxRounds + 1] = {};   // round_ptr[0 .. R]
-    const BlkMeta *meta = nullptr;
-    const int32_t *lvl_row = nullptr;
-    const uint32_t *fptr = nullptr, *bptr = nullptr;
-    const int32_t *fcol = nullptr, *bcol = nullptr, *perm = nullptr;
-    const double *fval = nullptr, *bval = nullptr, *D = nullptr, *xin = nullptr;
-    int64_t neg_from = 0;
-    int sched_in = 0;
-    double *xs = nullptr, *w = nullptr, *out = nullptr, *ys = nullptr;
-    const int *run = nullptr, *active = nullptr;
-};
-
-template <int TPB, int RPU, int EPU, bool ADD>
-__global__ __launch_bounds__(TPB) void sptrsv_chain_kernel(ChainArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    if (skip(a.run, a.active)) return;  // the same flags for every workgroup: all or none
-    cooperative_groups::grid_group grid = cooperative_groups::this_grid();
-    const PackArgs none{};
-    const int R = a.nrounds;
-    for (int r = 1; r < R - 1; r++) {
-        for (int64_t b = a.rp[r] + blockIdx.x; b < a.rp[r + 1]; b += gridDim.x) {
-            upper_block<TPB, RPU, EPU, false, false>(smem, a.meta[b], a.lvl_row, a.fptr, a.fcol, a.fval, a.D, a.perm,
-                                                     a.xin, a.neg_from, a.w, nullptr, a.sched_in, nullptr, a.xs, none);
-            __syncthreads();
-        }
-        grid.sync();
-    }
-    for (int64_t b = a.rp[R - 1] + blockIdx.x; b < a.rp[R]; b += gridDim.x) {
-        last_block<TPB, RPU, EPU, ADD>(smem, a.meta[b], a.lvl_row, a.fptr, a.fcol, a.fval, a.bptr, a.bcol, a.bval, a.D,
-                                       a.perm, a.xin, a.neg_from, a.sched_in, a.xs, a.w, a.out, a.ys);
-        __syncthreads();
-    }
-    for (int r = R - 2; r >= 1; r--) {
-        grid.sync();
-        for (int64_t b = a.rp[r] + blockIdx.x; b < a.rp[r + 1]; b += gridDim.x) {
-            upper_block<TPB, RPU, EPU, true, ADD>(smem, a.meta[b], a.lvl_row, a.bptr, a.bcol, a.bval, a.D, a.perm,
-                                                  nullptr, 0, a.w, a.out, 0, a.ys, nullptr, none);
-            __syncthreads();
-        }
-    }
-}
-
-// the grid of the chain launch (0: no chain): as many workgroups as the widest upper round, at
-// most what the device keeps resident at once
-int chain_grid(const DFactor &F) {
-    constexpr int TPB = 512, RPU = 2, EPU = 8;
-    const int64_t R = (int64_t)F.round_ptr.size() - 1;
-    if (!F.chain || !fuse_last_ok(F) || R < 3 || R > kChainMaxRounds) return 0;
-    for (int64_t r = 1; r < R; r++)
-        if (r >= (int64_t)F.round_fits.size() || !F.round_fits[r]) return 0;
-    static int resident = -1;  // co-resident workgroups of the instantiation (same for both ADD)
-    if (resident < 0) {
-        int dev = 0, coop = 0, cus = 0, per_cu = 0;
-        const size_t lds = sweep_lds_bytes(RPU * TPB, EPU * TPB);
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const bool lds_ok = lds <= 64 * 1024 ||
-            (hipFuncSetAttribute((const void *)sptrsv_chain_kernel<TPB, RPU, EPU, false>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
-             hipFuncSetAttribute((const void *)sptrsv_chain_kernel<TPB, RPU, EPU, true>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess);
-        if (!coop || !lds_ok ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)sptrsv_chain_kernel<TPB, RPU, EPU, true>,
-                                                         TPB, lds) != hipSuccess)
-            per_cu = 0;
-        resident = per_cu * cus;
-    }
-    int64_t widest = 0;
-    for (int64_t r = 1; r < R; r++) widest = std::max(widest, F.round_ptr[r + 1] - F.round_ptr[r]);
-    return (int)std::min<int64_t>(widest, resident);
-}
-
-static void launch_chain(Ctx &c, const DFactor &F, const FwdIn &in, double *w, double *out, bool add, const int *run,
-                         const int *active, double *ys, int grid) {
-    constexpr int TPB = 512, RPU = 2, EPU = 8;
-    ChainArgs a;
-    a.nrounds = (int)F.round_ptr.size() - 1;
-    for (int r = 0; r <= a.nrounds; r++) a.rp[r] = F.round_ptr[r];
-    a.meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
-    a.lvl_row = F.lvl_row.p, a.fptr = F.fptr.p, a.bptr = F.bptr.p, a.fcol = F.fcol.p, a.bcol = F.bcol.p;
-    a.perm = F.perm.p, a.fval = F.fval.p, a.bval = F.bval.p, a.D = F.D.p;
-    a.xin = in.xin, a.neg_from = in.neg_from, a.sched_in = in.sched_in, a.xs = in.xs;
-    a.w = w, a.out = out, a.ys = ys, a.run = run, a.active = active;
-    void *args[] = {&a};
-    const size_t lds = sweep_lds_bytes(RPU * TPB, EPU * TPB);
-    const void *f = add ? (const void *)sptrsv_chain_kernel<TPB, RPU, EPU, true>
-                        : (const void *)sptrsv_chain_kernel<TPB, RPU, EPU, false>;
-    CPK_HIP(hipLaunchCooperativeKernel(f, dim3((unsigned)grid), dim3(TPB), args, (unsigned)lds, c.stream));
 }
 
 // the last round fused (fwd + bwd) when it is an upper round whose blocks fit sptrsv_last_kernel
@@ -2230,10 +2126,7 @@ static bool fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
                     const PackArgs *pk = nullptr) {
     int64_t R = (int64_t)F.round_ptr.size() - 1;
     bool packed = pk != nullptr && F.ndet == 0 && rfirst == 0;  // every round through a packing kernel
-    if (defer && MODE == 0 && rfirst <= 1 && chain_grid(F) > 0) {  // rounds 1 .. R-1 run in the chain launch
-        *defer = FwdIn{xin, neg_from, sched_in, xs, true, 1};
-        R = 1;
-    } else if (defer && MODE == 0 && fuse_last_ok(F)) {  // the last round runs with the backward sweep
+    if (defer && MODE == 0 && fuse_last_ok(F)) {  // the last round runs with the backward sweep
         *defer = FwdIn{xin, neg_from, sched_in, xs, true, R - 1};
         R -= 1;
     }
@@ -2345,9 +2238,8 @@ bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
     int64_t R = (int64_t)F.round_ptr.size() - 1;
     bool packed = pk != nullptr && out != nullptr && F.ndet == 0 && !(last && last->valid);
     const PackArgs none{};
-    if (last && last->valid) {  // the deferred rounds: the chain launch, or the last round alone
-        if (last->from < R - 1) launch_chain(c, F, *last, w, out, add, run, active, ys, chain_grid(F));
-        else launch_last(c, F, *last, w, out, add, run, active, ys);
+    if (last && last->valid) {  // the deferred last round, forward and backward (sptrsv_last_kernel)
+        launch_last(c, F, *last, w, out, add, run, active, ys);
         R = last->from;
     }
     for (int64_t r = R - 1; r >= 0; r--) {

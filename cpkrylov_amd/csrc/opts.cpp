@@ -67,7 +67,6 @@ const BoolOpt kBool[] = {
     {"no_halo_merge", &EngineOpts::no_halo_merge},
     {"no_graph", &EngineOpts::no_graph},
     {"no_fuse_last", &EngineOpts::no_fuse_last},
-    {"upper_chain", &EngineOpts::upper_chain},
     {"dist_graph", &EngineOpts::dist_graph},
     {"profile_fwd_nolevels", &EngineOpts::profile_fwd_nolevels},
 };

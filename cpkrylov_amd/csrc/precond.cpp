@@ -75,7 +75,6 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
     pc->dF.pipelined = !c.opts.no_pipe, pc->dF.no_upper = c.opts.no_upper, pc->dF.no_col16 = c.opts.no_col16;
     pc->dF.no_fused_resid = c.opts.no_fused_resid, pc->dF.fused_tail_launch = c.opts.fused_tail_launch;
     pc->dF.fuse_last = !c.opts.no_fuse_last;  // single GPU: no entries outside the factor
-    pc->dF.chain = c.opts.upper_chain;
     pc->no_sched = c.opts.no_sched_resid;
     // Kp and Kp in schedule order depend only on Kp and the pivot order: they are built and
     // uploaded on a second host thread while this one lays out and uploads the factor

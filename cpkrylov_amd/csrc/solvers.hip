@@ -2021,7 +2021,7 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
     out->apply_ms = timeit([&]() { M.apply(x.p, M.n, z.p, nullptr); });
     out->apply_bytes = M.apply_bytes();
     out->fwd_launches = out->bwd_launches = (int64_t)M.dF.round_ptr.size() - 1;
-    if (last.valid) {  // the deferred rounds: one launch (last round or chain) inside the backward count
+    if (last.valid) {  // the deferred last round: one launch inside the backward count
         out->fwd_launches = last.from;
         out->bwd_launches = last.from + 1;
     }

@@ -122,7 +122,7 @@ int cpk_ctx_create_sim(int device, cpk_simgroup group, int rank, int nranks, cpk
  * Names: sweep ("rows,cap,threads[,rows,cap,threads[,sub0]]"), detach, split_tol, host_factor,
  * no_pipe, no_upper, no_col16, no_sched_resid, no_fused_resid, fused_tail_launch, r0_stride,
  * r0_xcd_chunk, tsolve_global, tsolve_onepass, no_piggy, no_halo_merge, no_graph, no_fuse_last,
- * upper_chain, dist_graph, batch, profile_fwd_nolevels.  Booleans as "0"/"1".  A distributed preconditioner allgathers a hash
+ * dist_graph, batch, profile_fwd_nolevels.  Booleans as "0"/"1".  A distributed preconditioner allgathers a hash
  * of its plan and of every option at creation and fails (CPK_ERR_ARGS) on every rank unless
  * all ranks agree. */
 int cpk_ctx_set_option(cpk_ctx ctx, const char *name, const char *value);
@@ -189,8 +189,7 @@ int cpk_pc_get_info(cpk_pc M, cpk_pc_info *info);
 int cpk_pc_sep_info(cpk_pc M, int64_t *info);
 /* Diagnostic (not in the reference): the sweep schedule as launched, info[8] = {rounds, round-0
  * blocks, blocks above round 0, grid of the cost-balanced round-0 assignment of the forward /
- * fused-residual forward / backward kernel (0: the launch strides), round 0 persistent, grid of
- * the cooperative upper-round launch (0: the upper rounds launch one by one)}. */
+ * fused-residual forward / backward kernel (0: the launch strides), round 0 persistent, 0}. */
 int cpk_pc_sweep_info(cpk_pc M, int64_t *info);
 int cpk_pc_local_dofs(cpk_pc M, int64_t *n_loc, int64_t *m_loc, int32_t *dofs);
 /* Export the factors P'*Kp*P = L*D*L': strict-lower L in CSC (Lcolptr[N+1], Lrowind[nnz_l],
