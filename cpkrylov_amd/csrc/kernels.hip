@@ -1286,14 +1286,35 @@ __device__ __forceinline__ void pack_inputs(const PackArgs &pk, int64_t e) {
 // issues all of its row and entry loads at once, then all of its gathers (input through perm,
 // w of outside-block columns) with clamped, unconditional addresses, so staging costs about two
 // dependent round trips instead of one per predicated slot.  Fold and levels as before.
+#ifdef CPK_PIPE_STAMPS
+// per-block cycles (s_memtime) of the last launch of each unsplit round-0 variant: [fwd, fwd +
+// fused residual, bwd, bwd accumulating][block] (tools/blk_cycles.py: the round-0 cost model),
+// then the upper rounds' phases [fwd, bwd][staging, fold, levels, write-back][block]
+// (tools/upper_cycles.py)
+constexpr int kBlkCycMax = 1 << 17;
+__device__ uint64_t g_blk_cyc[12 * kBlkCycMax];
+#define CPK_UP_STAMP(k)                                                                          \
+    do {                                                                                       \
+        const uint64_t t_ = (uint64_t)clock64();                                               \
+        if (threadIdx.x == 0 && b < kBlkCycMax) g_blk_cyc[(4 + (BWD ? 4 : 0) + (k)) * kBlkCycMax + b] = t_ - tp; \
+        tp = t_;                                                                               \
+    } while (0)
+#else
+#define CPK_UP_STAMP(k) (void)0
+#endif
 // one block of an upper round (the body of sptrsv_upper_kernel); ends with the block's write-back
 template <int TPB, int RPU, int EPU, bool BWD, bool ADD>
 __device__ __forceinline__ void upper_block(
     char *smem, const BlkMeta m, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
-    double *w, double *out, int sched_in, double *ys, double *xs, const PackArgs &pk) {
+    double *w, double *out, int sched_in, double *ys, double *xs, const PackArgs &pk, int64_t b) {
     constexpr int R = RPU * TPB, CAP = EPU * TPB;
+#ifdef CPK_PIPE_STAMPS
+    uint64_t tp = (uint64_t)clock64();
+#else
+    (void)b;
+#endif
     const int r0 = m.r0, r1 = m.r1, nr = r1 - r0, nl = m.l1 - m.l0;
     const uint32_t e0 = BWD ? (uint32_t)m.be0 : (uint32_t)m.fe0;
     const int ne = BWD ? m.be1 - m.be0 : m.fe1 - m.fe0;
@@ -1344,7 +1365,9 @@ __device__ __forceinline__ void upper_block(
         }
     }
     __syncthreads();
+    CPK_UP_STAMP(0);
     fold_prefix<TPB, 1>(S, nr, -1, R);
+    CPK_UP_STAMP(1);
     // levels on one wave: a level holds a few rows, and without a workgroup barrier per level
     // (a single wave's LDS accesses complete in program order) the chain is LDS latency only;
     // narrow levels give each row a lane group (levels_grouped)
@@ -1353,6 +1376,7 @@ __device__ __forceinline__ void upper_block(
         else sweep_levels<kWave, BWD, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
     }
     __syncthreads();
+    CPK_UP_STAMP(2);
 #pragma unroll
     for (int j = 0; j < RPU; j++) {
         const int i = tid + j * TPB;
@@ -1372,6 +1396,7 @@ __device__ __forceinline__ void upper_block(
             }
         }
     }
+    CPK_UP_STAMP(3);
 }
 
 template <int TPB, int RPU, int EPU, bool BWD, bool ADD>
@@ -1383,7 +1408,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
     upper_block<TPB, RPU, EPU, BWD, ADD>(smem, meta[blk0 + blockIdx.x], lvl_row, ptr, col, val, D, perm, xin, neg_from,
-                                         w, out, sched_in, ys, xs, pk);
+                                         w, out, sched_in, ys, xs, pk, blk0 + blockIdx.x);
 }
 
 // The last round's forward and backward sweeps in one launch (single GPU).  The sweeps meet at
@@ -1597,10 +1622,6 @@ static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add,
 // diagnostic build only (make HIPEXTRA=-DCPK_PIPE_STAMPS): per-workgroup start / end of the last
 // round-0 launch (s_memrealtime, 100 MHz), read by cpk_debug_pipe_stamps (tools/pipe_stamps.py)
 __device__ uint64_t g_pipe_stamps[2 * 16384];
-// per-block cycles (s_memtime) of the last launch of each unsplit variant: [fwd, fwd + fused
-// residual, bwd, bwd accumulating][block] (tools/blk_cycles.py: the round-0 cost model)
-constexpr int kBlkCycMax = 1 << 17;
-__device__ uint64_t g_blk_cyc[4 * kBlkCycMax];
 #endif
 template <int TPB, int RPT, int EPT, bool BWD, bool ADD, int SPLIT = 1, bool LOC = false, bool RES = false>
 #ifndef CPK_PIPE_WAVES
@@ -2176,7 +2197,7 @@ bool launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_
 // CPK_PIPE_STAMPS); returns the number of pairs copied
 int64_t debug_blk_cycles(uint64_t *out, int64_t n) {
 #ifdef CPK_PIPE_STAMPS
-    n = std::min<int64_t>(n, 4 * (int64_t)kBlkCycMax);
+    n = std::min<int64_t>(n, 12 * (int64_t)kBlkCycMax);
     CPK_HIP(hipDeviceSynchronize());
     CPK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blk_cyc), (size_t)n * sizeof(uint64_t)));
     return n;
