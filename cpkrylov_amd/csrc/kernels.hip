@@ -1035,12 +1035,16 @@ __device__ __forceinline__ void levels_owned(SweepLds &S, int nl, int nr, bool s
 #ifndef CPK_LEVEL_GROUP
 #define CPK_LEVEL_GROUP 1
 #endif
-#ifndef CPK_UPPER_GROUP
-// The same grouping in the upper-round and last-round kernels' one-wave levels: bit-identical,
-// but measured slower there (S10 backward 0.1835 vs 0.1778 ms, profiles/r03_upper_group_ab_v9.txt),
-// so off by default.
-#define CPK_UPPER_GROUP 0
+// The same grouping in the upper-round and last-round kernels' one-wave levels, per direction:
+// bit-identical either way.  Both on measured slower (S10 backward 0.1835 vs 0.1778 ms,
+// profiles/r03_upper_group_ab_v9.txt); CPK_UPPER_GROUP_FWD / _BWD select each (A/B builds).
+#ifndef CPK_UPPER_GROUP_FWD
+#define CPK_UPPER_GROUP_FWD 0
 #endif
+#ifndef CPK_UPPER_GROUP_BWD
+#define CPK_UPPER_GROUP_BWD 0
+#endif
+#define CPK_UPPER_GROUP(bwd) ((bwd) ? CPK_UPPER_GROUP_BWD : CPK_UPPER_GROUP_FWD)
 __device__ __forceinline__ double row_next_lane(double x) {  // lane i + 1 of its 16-lane row (15: 0)
     const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x101, 0xf, 0xf, true);
     const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x101, 0xf, 0xf, true);
@@ -1372,7 +1376,7 @@ __device__ __forceinline__ void upper_block(
     // (a single wave's LDS accesses complete in program order) the chain is LDS latency only;
     // narrow levels give each row a lane group (levels_grouped)
     if (tid < kWave) {
-        if (CPK_UPPER_GROUP) levels_grouped<CPK_UPPER_CH, BWD, true>(S, nl, false, tid);
+        if (CPK_UPPER_GROUP(BWD)) levels_grouped<CPK_UPPER_CH, BWD, true>(S, nl, false, tid);
         else sweep_levels<kWave, BWD, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
     }
     __syncthreads();
@@ -1479,7 +1483,7 @@ __device__ __forceinline__ void last_block(
     __syncthreads();
     fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (CPK_UPPER_GROUP) levels_grouped<CPK_UPPER_CH, false, true>(S, nl, false, tid);
+        if (CPK_UPPER_GROUP(false)) levels_grouped<CPK_UPPER_CH, false, true>(S, nl, false, tid);
         else sweep_levels<kWave, false, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
     }
     __syncthreads();
@@ -1509,7 +1513,7 @@ __device__ __forceinline__ void last_block(
     __syncthreads();
     fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (CPK_UPPER_GROUP) levels_grouped<CPK_UPPER_CH, true, true>(S, nl, false, tid);
+        if (CPK_UPPER_GROUP(true)) levels_grouped<CPK_UPPER_CH, true, true>(S, nl, false, tid);
         else sweep_levels<kWave, true, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
     }
     __syncthreads();

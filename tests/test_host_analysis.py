@@ -162,6 +162,22 @@ def test_engine_option_from_env_validated(monkeypatch):
     assert small["nblocks"] > default["nblocks"]
 
 
+@pytest.mark.parametrize("name", ["r0_xcd_chunk", "batch"])
+def test_integer_engine_options_validated(monkeypatch, name):
+    """Integer engine options (round-0 XCD run length, fixed graph batch) accept 0..4096 and
+    reject anything else, whether from CPK_<NAME> or not an integer at all."""
+    S = saddle_system(N=20000, seed=3)
+    env = "CPK_" + name.upper()
+    for bad in ("abc", "-1", "4097", "16x", "1.5"):
+        monkeypatch.setenv(env, bad)
+        with pytest.raises(cpk.CpkError):
+            cpk.analyze(S["G"], S["B"], -S["C"])
+    for good in ("0", "3", "4096"):
+        monkeypatch.setenv(env, good)
+        cpk.analyze(S["G"], S["B"], -S["C"])
+    monkeypatch.delenv(env)
+
+
 def test_split_tol_option_validated(monkeypatch):
     """CPK_SPLIT_TOL (a diagnostic of the distributed plan) must be a finite number in (0, 1):
     every rank builds the same plan from it, so a malformed value is an error, not a default."""
