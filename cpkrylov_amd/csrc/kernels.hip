@@ -860,9 +860,6 @@ constexpr int kSweepPad = 8;
 #ifndef CPK_UPPER_CH
 #define CPK_UPPER_CH 4  // entries per LDS round trip in the upper-round level loop
 #endif
-#ifndef CPK_UPPER_PF
-#define CPK_UPPER_PF 0  // A/B builds: the level loop's next chunk read during this chunk's gathers
-#endif
 #ifndef CPK_PIPE_CH
 #define CPK_PIPE_CH 2  // entries per LDS round trip in the round-0 level loop
 #endif  // entry arrays padded for the branchless 8-entry chunks
@@ -943,32 +940,6 @@ __device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_firs
         for (int k = a + tid; k < z; k += TPB) {
             const int e1 = S.p[k + 1];
             double acc = S.w[k];
-            if (ONE && WAVE && CPK_UPPER_PF) {
-                // the next chunk's (col, val) are read while this chunk's gathers are in flight:
-                // the columns and values are static, only the gathers depend on earlier levels.
-                // Reads stop at e1 (< the block's entries + kSweepPad): valid LDS, never used
-                int e = PS ? S.ps[k] : S.p[k];
-                int c[CH];
-                double v[CH];
-#pragma unroll
-                for (int j = 0; j < CH; j++) c[j] = S.c[e + j], v[j] = S.v[e + j];
-                for (; e < e1; e += CH) {
-                    double x[CH];
-#pragma unroll
-                    for (int j = 0; j < CH; j++) x[j] = S.w[c[j]];
-                    const int en = e + CH < e1 ? e + CH : e1;
-                    int cn[CH];
-                    double vn[CH];
-#pragma unroll
-                    for (int j = 0; j < CH; j++) cn[j] = S.c[en + j], vn[j] = S.v[en + j];
-#pragma unroll
-                    for (int j = 0; j < CH; j++) acc -= (e + j < e1) ? v[j] * x[j] : 0.0;
-#pragma unroll
-                    for (int j = 0; j < CH; j++) c[j] = cn[j], v[j] = vn[j];
-                }
-                S.w[k] = acc;
-                continue;
-            }
             for (int e = PS ? S.ps[k] : S.p[k]; e < e1; e += CH) {
                 int c[CH];
                 double v[CH], x[CH];
