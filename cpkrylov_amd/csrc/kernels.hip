@@ -857,9 +857,16 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
 // LDS image of a staged block (dynamic shared memory, sized per launch):
 //   double w[R + 1] | double v[CAP + 8] | int16 c[CAP + 8] | int16 p[R + 1] | int16 lv[R + 1] | int16 ps[R + 1]
 constexpr int kSweepPad = 8;
-#ifndef CPK_UPPER_CH
-#define CPK_UPPER_CH 4  // entries per LDS round trip in the upper-round level loop
+// entries per LDS round trip in the upper-round level loop, per direction: the forward rows
+// carry tens of in-block terms, the backward ones few (stamps build, profiles/r03_upper_ch_v17.txt:
+// 8 vs 4 per chunk, forward levels -7 % / -11 % in rounds 1 / 2, backward +14 % / +17 %)
+#ifndef CPK_UPPER_CH_FWD
+#define CPK_UPPER_CH_FWD 8
 #endif
+#ifndef CPK_UPPER_CH_BWD
+#define CPK_UPPER_CH_BWD 4
+#endif
+#define CPK_UPPER_CH(bwd) ((bwd) ? CPK_UPPER_CH_BWD : CPK_UPPER_CH_FWD)
 #ifndef CPK_PIPE_CH
 #define CPK_PIPE_CH 2  // entries per LDS round trip in the round-0 level loop
 #endif  // entry arrays padded for the branchless 8-entry chunks
@@ -1376,8 +1383,8 @@ __device__ __forceinline__ void upper_block(
     // (a single wave's LDS accesses complete in program order) the chain is LDS latency only;
     // narrow levels give each row a lane group (levels_grouped)
     if (tid < kWave) {
-        if (CPK_UPPER_GROUP(BWD)) levels_grouped<CPK_UPPER_CH, BWD, true>(S, nl, false, tid);
-        else sweep_levels<kWave, BWD, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
+        if (CPK_UPPER_GROUP(BWD)) levels_grouped<CPK_UPPER_CH(BWD), BWD, true>(S, nl, false, tid);
+        else sweep_levels<kWave, BWD, true, CPK_UPPER_CH(BWD), true, true>(S, nl, false, tid);
     }
     __syncthreads();
     CPK_UP_STAMP(2);
@@ -1483,8 +1490,8 @@ __device__ __forceinline__ void last_block(
     __syncthreads();
     fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (CPK_UPPER_GROUP(false)) levels_grouped<CPK_UPPER_CH, false, true>(S, nl, false, tid);
-        else sweep_levels<kWave, false, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
+        if (CPK_UPPER_GROUP(false)) levels_grouped<CPK_UPPER_CH(false), false, true>(S, nl, false, tid);
+        else sweep_levels<kWave, false, true, CPK_UPPER_CH(false), true, true>(S, nl, false, tid);
     }
     __syncthreads();
     // ---- backward (sptrsv_upper_kernel<..., true, ADD>): w / D, the entries, fold, levels; the
@@ -1513,8 +1520,8 @@ __device__ __forceinline__ void last_block(
     __syncthreads();
     fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (CPK_UPPER_GROUP(true)) levels_grouped<CPK_UPPER_CH, true, true>(S, nl, false, tid);
-        else sweep_levels<kWave, true, true, CPK_UPPER_CH, true, true>(S, nl, false, tid);
+        if (CPK_UPPER_GROUP(true)) levels_grouped<CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
+        else sweep_levels<kWave, true, true, CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
     }
     __syncthreads();
 #pragma unroll
