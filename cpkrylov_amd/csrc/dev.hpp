@@ -100,6 +100,7 @@ struct EngineOpts {
     bool no_halo_merge = false;   // no_halo_merge:      cpminres beta by its own allreduce
     bool no_graph = false;        // no_graph:           no hipGraph capture of iterations
     bool no_fuse_last = false;    // no_fuse_last:       the last sweep round as two launches
+    bool no_tkr = false;          // no_tkr:             distributed refinement residual through the Kp halo
     bool dist_graph = true;       // dist_graph:         capture collectives in the graphs
     int batch = 0;                // batch:              fixed iterations per graph (0: adaptive)
     bool profile_fwd_nolevels = false;  // profile_fwd_nolevels: diagnostic (cpk_profile_kernels)
@@ -147,6 +148,9 @@ struct DistCsr;
 void make_dist_dmat(const DistCsr &a, int nranks, DMat &d);
 // allgather the halo of x (local vector) into A.rbuf
 void launch_halo(Ctx &c, const DMat &A, const double *x, bool packed = false);
+// r = xin - A*y with A's columns >= A.nloc read from halo[c - nloc] (no exchange)
+void launch_spmv_resid_loc(Ctx &c, const DMat &A, const double *xin, int64_t neg_from, const double *y, double *r,
+                           const int *run, const double *halo);
 
 // HBM-resident factor + sweep schedule (rows in schedule order).
 struct DFactor {
@@ -294,8 +298,16 @@ void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x
                          const double *piggy_src = nullptr, bool packed = false);
 // redundant separator solve into wT (= w + nsub); rank 0 writes (add: accumulates) y at the T dofs
 // hslot / hbuf (optional): also pack y's Kp halo at the T dofs (PackArgs, backward)
+// tkr_* (optional, Precond::tkr): first form the T rows' refinement residual (launch_tkr_resid's
+// arithmetic, inside the prefix kernel when that path runs)
 void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active,
-                      const int32_t *hslot = nullptr, double *hbuf = nullptr);
+                      const int32_t *hslot = nullptr, double *hbuf = nullptr, const int32_t *tkr_ptr = nullptr,
+                      const int32_t *tkr_col = nullptr, const double *tkr_val = nullptr);
+// the T rows' refinement residual after the refinement's separator exchange, on every rank:
+// S.rbuf[tf_src[t]] (the T input +-x sent by rank 0) -= Kp row t * y, y from wT (T columns) and
+// the exchange's extra slots (subtree columns); each row summed in Kp's column order from 0.0
+void launch_tkr_resid(Ctx &c, const DSep &S, const int32_t *ptr, const int32_t *col, const double *val,
+                      const double *wT, const int *run, const int *active);
 
 // ---- device numeric LDL' (ldl.hip) --------------------------------------------------------
 struct DLdl {
@@ -439,9 +451,24 @@ struct Precond {
     bool no_sched = false;
     void set_handle(bool on);  // enabling or disabling clears the state
     // returns whether the backward sweep packed y's Kp halo (distributed: the residual's gather)
+    // stage (tkr): 1 the apply's first solve (the backward sweep packs hslot2 into the separator
+    // payload), 2 the refinement solve (its forward packs the T inputs from xT, the T rows'
+    // residual is formed after the exchange); 0 neither
     bool ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run, const int *act,
-                   const double *piggy_src = nullptr);
+                   const double *piggy_src = nullptr, int stage = 0, const double *xT = nullptr, int64_t xT_neg = 0);
     DBuf<int32_t> hslot;  // distributed: local output index -> Kp halo slot (-1: none); empty: no packing
+    // distributed, one forced refinement step: the residual without the Kp halo exchange
+    // (DESIGN.md section 7).  Kp couples a subtree row only with its own subtree and with T, and
+    // every rank holds T's solution (wT), so the local rows need no halo (dKpl: T-dof columns
+    // read wT at nloc + t; rank 0's T rows left empty); the T rows' residual is formed by every
+    // rank after the refinement's separator exchange, whose payload also carries the y values of
+    // the subtree rows those rows read (hslot2: local index -> extra payload slot; tkr_*: the T
+    // dofs' Kp rows, col >= 0 payload position, < 0 -(t + 1)), into the exchange's T-input slots
+    DMat dKpl;
+    DBuf<int32_t> hslot2, tkr_ptr, tkr_col;
+    DBuf<double> tkr_val;
+    bool tkr = false;
+    bool steps1_forced() const { return nitref == 1 && force_itref != 0 && !(residual_update != 0 && handle); }
     // algorithmic HBM bytes of one apply
     double apply_bytes() const;
 };

@@ -377,6 +377,16 @@ void launch_spmv_resid(Ctx &c, const DMat &A, const double *xin, int64_t neg_fro
     spmv_launch(c, A, y, 0, EpiResid{xin, neg_from, r, run, active});
 }
 
+void launch_spmv_resid_loc(Ctx &c, const DMat &A, const double *xin, int64_t neg_from, const double *y, double *r,
+                           const int *run, const double *halo) {
+    if (!A.nblk) return;
+    const EpiResid e{xin, neg_from, r, run, nullptr};
+    const unsigned grid = spmv_grid<EpiResid, true>(A.nblk);
+    hipLaunchKernelGGL((spmv_stream<EpiResid, true>), dim3(grid), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
+                       A.val.p, A.blk.p, A.nblk, y, (int64_t)0, e, halo, A.nloc);
+    CPK_HIP(hipGetLastError());
+}
+
 void launch_spmv_resid_sched(Ctx &c, const DMat &A, const int32_t *perm, const double *xin, int64_t neg_from,
                              const double *y, double *r, const int *run) {
     if (!A.nblk) return;
@@ -482,6 +492,12 @@ constexpr int64_t kTsMaxRows = 1 << 16;
 constexpr uint32_t kTsLead = 1u << 31, kTsFirst = 1u << 30, kTsLast = 1u << 29;
 constexpr uint32_t kTsBarrier = 1u << 16;  // step table: waves | barrier after the step
 
+// the T rows' Kp rows for the refinement residual (Precond::tkr); ptr null: none
+struct TkrArgs {
+    const int32_t *ptr = nullptr, *col = nullptr;
+    const double *val = nullptr, *wT = nullptr;
+};
+
 // x of lane i + 1 (wave shift; the last lane gets 0)
 __device__ __forceinline__ double ts_next_lane(double x) {
     const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x130, 0xf, 0xf, true);  // wave_shl:1
@@ -489,16 +505,38 @@ __device__ __forceinline__ double ts_next_lane(double x) {
     return __hiloint2double(hi, lo);
 }
 
+// TKR (Precond::tkr, the refinement solve): the row's input is the T row's refinement residual
+// xs_t - Kp row t * y, formed here first (the wave's products, added in Kp's column order from
+// 0.0 by lane 0 through the same lane shifts): tkr_resid_kernel's arithmetic without its launch
 __global__ __launch_bounds__(256) void tprefix_kernel(
     int nT, const int32_t *__restrict__ tk_ptr, const int32_t *__restrict__ tk_col, const double *__restrict__ tk_val,
     const int32_t *__restrict__ tr_ptr, const int32_t *__restrict__ tr_col, const double *__restrict__ tr_val,
     const int32_t *__restrict__ tr_slot, const int32_t *__restrict__ tf_src, const double *__restrict__ rbuf,
-    double *__restrict__ pre, double *__restrict__ rec_v, const int *run, const int *active) {
+    double *__restrict__ pre, double *__restrict__ rec_v, const int *run, const int *active, TkrArgs tkr) {
     if (skip(run, active)) return;
     const int wv = threadIdx.x / kWave, lane = threadIdx.x % kWave;
     const int t = blockIdx.x * 4 + wv;
     if (t >= nT) return;  // whole waves: the shifts below need every lane
     double acc = rbuf[tf_src[t]];
+    if (tkr.ptr) {
+        double sum = 0.0;
+        const int q1 = tkr.ptr[t + 1];
+        for (int e = tkr.ptr[t]; e < q1; e += kWave) {
+            const int q = e + lane;
+            double x = 0.0;
+            if (q < q1) {
+                const int32_t cq = tkr.col[q];
+                x = tkr.val[q] * (cq < 0 ? tkr.wT[-cq - 1] : rbuf[cq]);
+            }
+            const int n = min(kWave, q1 - e);
+            sum += x;
+            for (int u = 1; u < n; u++) {
+                x = ts_next_lane(x);
+                sum += x;
+            }
+        }
+        acc = acc - sum;
+    }
     const int k1 = tk_ptr[t + 1];
     for (int e = tk_ptr[t]; e < k1; e += kWave) {
         const int q = e + lane;
@@ -806,8 +844,32 @@ void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x
     c.comm->allgather(S.sbuf.p, S.rbuf.p, (size_t)S.kt, c.stream);
 }
 
+__global__ void tkr_resid_kernel(int nT, const int32_t *__restrict__ ptr, const int32_t *__restrict__ col,
+                                 const double *__restrict__ val, const int32_t *__restrict__ tf_src,
+                                 const double *__restrict__ wT, double *rbuf, const int *run, const int *active) {
+    if (skip(run, active)) return;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nT) return;
+    double acc = 0.0;  // the residual SpMV's row: products in Kp's column order, summed from 0.0
+    for (int e = ptr[t]; e < ptr[t + 1]; e++) {
+        const int32_t c = col[e];
+        const double p = val[e] * (c < 0 ? wT[-c - 1] : rbuf[c]);
+        acc += p;
+    }
+    rbuf[tf_src[t]] = rbuf[tf_src[t]] - acc;
+}
+
+void launch_tkr_resid(Ctx &c, const DSep &S, const int32_t *ptr, const int32_t *col, const double *val,
+                      const double *wT, const int *run, const int *active) {
+    if (S.nT == 0) return;
+    hipLaunchKernelGGL(tkr_resid_kernel, dim3((unsigned)((S.nT + 255) / 256)), dim3(256), 0, c.stream, (int)S.nT, ptr,
+                       col, val, S.tf_src.p, wT, S.rbuf.p, run, active);
+    CPK_HIP(hipGetLastError());
+}
+
 void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active,
-                      const int32_t *hslot, double *hbuf) {
+                      const int32_t *hslot, double *hbuf, const int32_t *tkr_ptr, const int32_t *tkr_col,
+                      const double *tkr_val) {
     if (S.nT == 0) return;
     static const bool lds_attr = [] {
         return hipFuncSetAttribute((const void *)tsolve_steps_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -818,10 +880,11 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
     auto fits = [&](size_t b) { return b && (b <= 64 * 1024 || lds_attr); };
     const bool grec = S.tsolve_global || !fits(S.lds);  // engine option: records in HBM
     const size_t lds = grec ? S.lds_g : S.lds;
+    const TkrArgs tkr{tkr_ptr, tkr_col, tkr_val, wT};  // wT: still y's T values (this solve writes it last)
     if (S.nrec > 0 && fits(lds) && !S.tsolve_onepass) {
         hipLaunchKernelGGL(tprefix_kernel, dim3((unsigned)((S.nT + 3) / 4)), dim3(256), 0, c.stream, (int)S.nT,
                            S.tk_ptr.p, S.tk_col.p, S.tk_val.p, S.tr_ptr.p, S.tr_col.p, S.tr_val.p, S.tr_slot.p,
-                           S.tf_src.p, S.rbuf.p, S.pre.p, S.rec_v.p, run, active);
+                           S.tf_src.p, S.rbuf.p, S.pre.p, S.rec_v.p, run, active, tkr);
         if (grec)
             hipLaunchKernelGGL(tsolve_steps_kernel<true>, dim3(1), dim3(kTsolveThreads), lds, c.stream, (int)S.nT,
                                (int)S.nsf, (int)S.nsb, (int)S.nrec, (const double *)S.rec_v.p,
@@ -835,6 +898,7 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
         CPK_HIP(hipGetLastError());
         return;
     }
+    if (tkr_ptr) launch_tkr_resid(c, S, tkr_ptr, tkr_col, tkr_val, wT, run, active);  // the one-pass kernel reads rbuf
     hipLaunchKernelGGL(tsolve_kernel, dim3(1), dim3(256), (size_t)S.nT * sizeof(double), c.stream, (int)S.nlev,
                        (int)S.nT, S.lev_ptr.p, S.lev_rows.p, S.tf_ptr.p, S.tf_col.p, S.tf_val.p, S.tf_src.p,
                        S.tb_ptr.p, S.tb_col.p, S.tb_val.p, S.DT.p, S.rbuf.p, S.tdof.p, (int)S.ntdof, wT, y,

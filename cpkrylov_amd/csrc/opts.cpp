@@ -67,6 +67,7 @@ const BoolOpt kBool[] = {
     {"no_halo_merge", &EngineOpts::no_halo_merge},
     {"no_graph", &EngineOpts::no_graph},
     {"no_fuse_last", &EngineOpts::no_fuse_last},
+    {"no_tkr", &EngineOpts::no_tkr},
     {"dist_graph", &EngineOpts::dist_graph},
     {"profile_fwd_nolevels", &EngineOpts::profile_fwd_nolevels},
 };

@@ -261,9 +261,87 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
         for (auto &q : rp.tf_src) q = remap(q);
         rp.kt = kt1;
     }
+    // the refinement residual without the Kp halo exchange (Precond::tkr): the subtree rows the
+    // T dofs' Kp rows read, per owner (ascending dof), ride in extra payload slots after the
+    // plan's payload and the piggyback: positions r * kt1 + j become r * kt2 + j.  Every rank
+    // decides from global data only, so all take the same path.
+    std::vector<int32_t> tkr_ptr{0}, tkr_col, hslot2;
+    std::vector<double> tkr_val;
+    const int64_t kt1 = rp.kt;
+    {
+        const HCsr &K = an.Kp;
+        std::vector<int32_t> tof((size_t)an.N, -1);  // dof -> T index
+        for (int64_t t = 0; t < rp.nT; t++) tof[an.F0.perm[ts.T[t]]] = (int32_t)t;
+        // Kp(i, j) != 0 joins an ancestor and a descendant, so outside T a row couples only with
+        // its own rank's rows: checked over the whole matrix (the same verdict on every rank)
+        bool ok = !c.opts.no_tkr && rp.kt > 0 && rp.nT > 0;
+        for (int64_t d = 0; d < K.nrows && ok; d++)
+            if (tof[d] < 0)
+                for (int64_t p = K.ptr[d]; p < K.ptr[d + 1] && ok; p++) {
+                    const int32_t g = K.ind[p];
+                    ok = tof[g] >= 0 || dm->owner[g] == dm->owner[d];
+                }
+        std::vector<std::vector<int32_t>> need((size_t)c.nranks);
+        for (int64_t t = 0; t < rp.nT && ok; t++) {
+            const int32_t d = an.F0.perm[ts.T[t]];
+            for (int64_t p = K.ptr[d]; p < K.ptr[d + 1]; p++) {
+                const int32_t g = K.ind[p];
+                if (tof[g] < 0) need[(size_t)dm->owner[g]].push_back(g);
+            }
+        }
+        size_t kext = 0;
+        std::vector<int32_t> epos((size_t)an.N, -1);
+        for (auto &v : need) {
+            std::sort(v.begin(), v.end());
+            v.erase(std::unique(v.begin(), v.end()), v.end());
+            for (size_t e = 0; e < v.size(); e++) epos[(size_t)v[e]] = (int32_t)e;
+            kext = std::max(kext, v.size());
+        }
+        if (ok && kext > 0) {
+            const int64_t kt2 = kt1 + (int64_t)kext;
+            auto remap = [&](int32_t q) { return (int32_t)((q / kt1) * kt2 + q % kt1); };
+            for (auto &q : rp.tf_col)
+                if (q >= 0) q = remap(q);
+            for (auto &q : rp.tf_src) q = remap(q);
+            rp.kt = kt2;
+            for (int64_t t = 0; t < rp.nT; t++) {
+                const int32_t d = an.F0.perm[ts.T[t]];
+                for (int64_t p = K.ptr[d]; p < K.ptr[d + 1]; p++) {
+                    const int32_t g = K.ind[p];
+                    tkr_col.push_back(tof[g] >= 0 ? -(tof[g] + 1)
+                                                  : (int32_t)((int64_t)dm->owner[g] * kt2 + kt1 + epos[(size_t)g]));
+                    tkr_val.push_back(devnum ? (double)(p + 1) : K.val[p]);
+                }
+                tkr_ptr.push_back((int32_t)tkr_col.size());
+            }
+            hslot2.assign((size_t)std::max<int64_t>(pc->N, 1), -1);
+            for (size_t e = 0; e < need[(size_t)c.rank].size(); e++)
+                hslot2[(size_t)dm->lidx[need[(size_t)c.rank][e]]] = (int32_t)(kt1 + (int64_t)e);
+            // this rank's Kp rows: T-dof columns read wT (column nloc + t); rank 0's T rows empty
+            const std::vector<int32_t> mine = dm->dofs(c.rank);
+            const int64_t nloc = (int64_t)mine.size();
+            HCsr kl;
+            kl.nrows = nloc, kl.ncols = nloc + rp.nT;
+            kl.ptr.assign(1, 0);
+            for (int64_t i = 0; i < nloc; i++) {
+                const int32_t d = mine[(size_t)i];
+                if (tof[d] < 0)
+                    for (int64_t p = K.ptr[d]; p < K.ptr[d + 1]; p++) {
+                        const int32_t g = K.ind[p];
+                        kl.ind.push_back(tof[g] >= 0 ? (int32_t)(nloc + tof[g]) : dm->lidx[g]);
+                        kl.val.push_back(devnum ? (double)(p + 1) : K.val[p]);
+                    }
+                kl.ptr.push_back((int64_t)kl.ind.size());
+            }
+            make_dmat(kl, pc->dKpl);
+            pc->dKpl.nloc = nloc;  // columns >= nloc: wT
+            pc->tkr = true;
+        }
+    }
     T.nT = rp.nT, T.kt = rp.kt, T.nlev = (int64_t)rp.tlev_ptr.size() - 1, T.ntdof = (int64_t)rp.tdof.size();
     T.tsolve_global = c.opts.tsolve_global, T.tsolve_onepass = c.opts.tsolve_onepass;
-    T.kt_data = rp.kt > 0 ? rp.kt - kSepPiggy : 0;
+    T.kt_data = kt1 > 0 ? kt1 - kSepPiggy : 0;
+    if (pc->tkr) pc->hslot2.upload(hslot2), pc->tkr_ptr.upload(tkr_ptr), pc->tkr_col.upload(tkr_col), pc->tkr_val.upload(tkr_val);
     auto i32 = [](const std::vector<int64_t> &v) { return std::vector<int32_t>(v.begin(), v.end()); };
     T.tf_ptr.upload(i32(rp.tf_ptr)), T.tf_col.upload(rp.tf_col), T.tf_val.upload(rp.tf_val);
     T.tf_src.upload(rp.tf_src), T.tb_ptr.upload(i32(rp.tb_ptr)), T.tb_col.upload(rp.tb_col);
@@ -304,6 +382,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
         add(pc->dF.fval, 0), add(pc->dF.bval, 0), add(pc->dF.D, 1);
         add(T.tf_val, 0), add(T.tb_val, 0), add(T.DT, 1), add(T.tk_val, 0), add(T.tr_val, 0), add(T.rec_v, 0);
         add(pc->dKp.val, 2);
+        add(pc->dKpl.val, 2), add(pc->tkr_val, 2);
         dldl_setup(pc->dl, an.sym, an.F0, {}, {}, {});
         pc->kpg.upload(an.Kp.val);
         dldl_numeric(c, pc->dl, pc->kpg.p, pc->dl.Lx.p, pc->dl.D.p);
@@ -436,7 +515,7 @@ double precond_refactor(Precond &p, const DMat &A11, const DMat &B, const DMat &
 
 // y (=|+=) LDL * xin: forward sweep, [distributed: separator exchange + solve], backward sweep
 bool Precond::ldl_solve(const double *xin, int64_t neg_from, double *y, bool add, const int *run,
-                        const int *act, const double *piggy_src) {
+                        const int *act, const double *piggy_src, int stage, const double *xT, int64_t xT_neg) {
     Ctx &c = *ctx;
     FwdIn last;  // single GPU: the last round forward + backward in one launch (sptrsv_last_kernel)
     if (!dist) {
@@ -446,19 +525,26 @@ bool Precond::ldl_solve(const double *xin, int64_t neg_from, double *y, bool add
     }
     // distributed: the sweeps' write-back packs the separator payload (forward) and the Kp halo
     // of y (backward), so neither needs a gather launch
+    // stage 2 (tkr): rank 0 sends the apply's own T inputs +-x (the T rows' residual is formed
+    // from them after the exchange), not the refinement input's
+    const double *xt = stage == 2 ? xT : xin;
+    const int64_t xt_neg = stage == 2 ? xT_neg : neg_from;
     PackArgs fp;
     if (sep.tslot.n) {
         fp.slot = sep.tslot.p, fp.buf = sep.sbuf.p, fp.tdof = sep.tdof.p, fp.ntdof = (int)sep.ntdof;
-        fp.nsend = (int)sep.nsend, fp.kt_data = (int)sep.kt_data, fp.x = xin, fp.neg_from = neg_from;
+        fp.nsend = (int)sep.nsend, fp.kt_data = (int)sep.kt_data, fp.x = xt, fp.neg_from = xt_neg;
         fp.piggy = piggy_src;
     }
     const bool fpacked = launch_sptrsv_fwd(c, dF, xin, neg_from, w.p, run, act, false, nullptr, nullptr,
                                            sep.tslot.n ? &fp : nullptr);
-    launch_sep_exchange(c, sep, w.p, xin, neg_from, piggy_src, fpacked);
-    launch_sep_solve(c, sep, w.p + nsub, y, add, run, act, hslot.n ? hslot.p : nullptr, dKp.sbuf.p);
+    launch_sep_exchange(c, sep, w.p, xt, xt_neg, piggy_src, fpacked);
+    const bool hpack = stage == 0 && hslot.n;
+    launch_sep_solve(c, sep, w.p + nsub, y, add, run, act, hpack ? hslot.p : nullptr, dKp.sbuf.p,
+                     stage == 2 ? tkr_ptr.p : nullptr, tkr_col.p, tkr_val.p);
     PackArgs bp;
-    if (hslot.n) bp.slot = hslot.p, bp.buf = dKp.sbuf.p;
-    return launch_sptrsv_bwd(c, dF, w.p, y, add, run, act, nullptr, nullptr, hslot.n ? &bp : nullptr);
+    if (hpack) bp.slot = hslot.p, bp.buf = dKp.sbuf.p;
+    if (stage == 1) bp.slot = hslot2.p, bp.buf = sep.sbuf.p;  // y of the rows T's Kp rows read
+    return launch_sptrsv_bwd(c, dF, w.p, y, add, run, act, nullptr, nullptr, (hpack || stage == 1) ? &bp : nullptr);
 }
 
 void Precond::set_handle(bool on) {
@@ -488,6 +574,14 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
         launch_sptrsv_fwd(c, dF, x, neg_from, w.p, run, nullptr, false, xs.n ? xs.p : nullptr, &last);
         have_xs = xs.n > 0;
         launch_sptrsv_bwd(c, dF, w.p, nullptr, false, run, nullptr, nullptr, &last);
+    } else if (dist && tkr && steps1_forced()) {
+        // distributed, one forced refinement step, no Kp halo exchange (Precond::tkr): y = LDL*x
+        // packs the y values the T rows' residual needs into the separator payload; the local
+        // rows' residual reads T's values from wT; the refinement solve forms the T rows' own
+        ldl_solve(x, neg_from, y, false, run, nullptr, piggy_src, 1);
+        launch_spmv_resid_loc(c, dKpl, x, neg_from, y, r.p, run, w.p + nsub);  // r = x - op.A*y
+        ldl_solve(r.p, N, y, true, run, nullptr, nullptr, 2, x, neg_from);    // y = y + op.LDL*r
+        return;
     } else {
         // y = op.LDL * x   (opLDL2.m:165-167); the residual-update branch subtracts the zero
         // state of a value object and its SpMVs are dead: skipped

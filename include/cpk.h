@@ -121,7 +121,7 @@ int cpk_ctx_create_sim(int device, cpk_simgroup group, int rank, int nranks, cpk
  * once at creation; a change applies to preconditioners and solves created afterwards.
  * Names: sweep ("rows,cap,threads[,rows,cap,threads[,sub0]]"), detach, split_tol, host_factor,
  * no_pipe, no_upper, no_col16, no_sched_resid, no_fused_resid, fused_tail_launch, r0_stride,
- * r0_xcd_chunk, tsolve_global, tsolve_onepass, no_piggy, no_halo_merge, no_graph, no_fuse_last,
+ * r0_xcd_chunk, tsolve_global, tsolve_onepass, no_piggy, no_halo_merge, no_graph, no_fuse_last, no_tkr,
  * dist_graph, batch, profile_fwd_nolevels.  Booleans as "0"/"1".  A distributed preconditioner allgathers a hash
  * of its plan and of every option at creation and fails (CPK_ERR_ARGS) on every rank unless
  * all ranks agree. */
@@ -184,8 +184,9 @@ int cpk_pc_get_info(cpk_pc M, cpk_pc_info *info);
 /* Local slice of a (distributed) preconditioner: n_loc x-part and m_loc y-part dofs; dofs[i] =
  * global index of local entry i (n_loc + m_loc entries).  One GPU: the identity. */
 /* Diagnostic (not in the reference): the separator solve of a distributed preconditioner,
- * info[7] = {distributed, separator rows, levels, step records, LDS bytes with the records
- * staged (0: they do not fit), LDS bytes with the records left in HBM, payload per rank}. */
+ * info[8] = {distributed, separator rows, levels, step records, LDS bytes with the records
+ * staged (0: they do not fit), LDS bytes with the records left in HBM, payload per rank,
+ * refinement residual without the Kp halo exchange}. */
 int cpk_pc_sep_info(cpk_pc M, int64_t *info);
 /* Diagnostic (not in the reference): the sweep schedule as launched, info[8] = {rounds, round-0
  * blocks, blocks above round 0, grid of the cost-balanced round-0 assignment of the forward /

@@ -81,6 +81,35 @@ def test_dist_apply_bitexact(name, P, props):
         assert np.all(d[:nl] < S["n"]) and np.all(d[nl:] >= S["n"])
 
 
+@pytest.mark.parametrize("P", [2, 3, 4])
+@pytest.mark.parametrize("name", ["cvxqp1_m", "synthetic20k"])
+def test_dist_refinement_without_kp_halo(name, P):
+    """One forced refinement step (the example options) without the Kp halo exchange: every
+    rank's local rows read T's solution from its own separator solve, the T rows' residual is
+    formed after the refinement's separator exchange (engine option no_tkr restores the halo
+    exchange).  A sequence of applies, each bit for bit the oracle's and the halo path's."""
+    import cpkrylov_amd as cpk
+    S = _system(name)
+    rng = np.random.default_rng(41)
+    zs = [rng.standard_normal(S["n"] + S["m"]) for _ in range(3)]
+
+    def work(ctx, r):
+        M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+        M.nitref, M.force_itref = 1, True
+        return [M * z for z in zs], M.export_factors() if r == 0 else None, M.sep_info()["tkr"]
+
+    for opts in (None, dict(no_tkr=True)):
+        res = _run_ranks(P, work, opts)
+        assert all(t == (0 if opts else 1) for _, _, t in res), opts
+        L, D, perm = res[0][1]
+        Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=(L, D, perm))
+        Mo.set(nitref=1.0, force_itref=1.0)
+        for k, z in enumerate(zs):
+            yo = Mo @ z
+            for ys, _, _ in res:
+                assert np.array_equal(ys[k], yo), (opts, k, np.max(np.abs(ys[k] - yo)))
+
+
 DIST_CASES = [("cvxqp1_m", "minres", {}), ("cvxqp1_m", "cg", {}), ("cvxqp1_m", "cglanczos", {}),
               ("cvxqp1_m", "symmlq", {}), ("cvxqp1_m", "dqgmres", {"mem": 2}),
               ("cvxqp2_s", "gmres", {"restart": 20}), ("cvxqp2_s", "gmres", {"restart": 100}),
