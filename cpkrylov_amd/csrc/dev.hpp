@@ -101,6 +101,7 @@ struct EngineOpts {
     bool no_graph = false;        // no_graph:           no hipGraph capture of iterations
     bool no_fuse_last = false;    // no_fuse_last:       the last sweep round as two launches
     bool no_tkr = false;          // no_tkr:             distributed refinement residual through the Kp halo
+    bool no_minres_fuse = false;  // no_minres_fuse:     cpminres update as its own pass (normalise + w, x)
     bool dist_graph = true;       // dist_graph:         capture collectives in the graphs
     int batch = 0;                // batch:              fixed iterations per graph (0: adaptive)
     bool profile_fwd_nolevels = false;  // profile_fwd_nolevels: diagnostic (cpk_profile_kernels)
@@ -128,6 +129,10 @@ struct Ctx {
 // HBM-resident CSR with a row-block partition for the LDS-staged streaming SpMV.
 constexpr int kSpmvCap = 2048;      // entries staged in LDS per workgroup
 constexpr int kSpmvMaxRows = 1024;  // rows per workgroup
+// 6 waves per SIMD (<= 80 VGPRs): the reducing epilogues otherwise take 82 and run 5
+#ifndef CPK_SPMV_WAVES
+#define CPK_SPMV_WAVES 6
+#endif
 struct DMat {
     int64_t nrows = 0, ncols = 0, nnz = 0, nblk = 0;
     DBuf<uint32_t> ptr;

@@ -68,6 +68,7 @@ const BoolOpt kBool[] = {
     {"no_graph", &EngineOpts::no_graph},
     {"no_fuse_last", &EngineOpts::no_fuse_last},
     {"no_tkr", &EngineOpts::no_tkr},
+    {"no_minres_fuse", &EngineOpts::no_minres_fuse},
     {"dist_graph", &EngineOpts::dist_graph},
     {"profile_fwd_nolevels", &EngineOpts::profile_fwd_nolevels},
 };

@@ -184,6 +184,13 @@ inline void launch_scalar(Ctx &c, const F &f) {
 // with the two inner products <y(1:n), x(1:n)> and <y(n+1:N), x(n+1:N)> of the result against
 // the input (alpha = dot(u,vk) + dot(t,qk), pAp and qCq).  F::select(st) picks the input
 // vector and the finalize runs F::fin(st, tot).
+// F::kNorm (cpminres, fused update): the input is the previous step's unnormalised vector;
+// every value read is divided by F::norm(st) (when > 0: the division MinresUpdate would have
+// stored, so the same bits), and each row's normalised value is stored to F::out(st) -- the
+// normalisation pass folded into the product that reads the vector next.
+#ifndef CPK_SPMV_NORM_WAVES
+#define CPK_SPMV_NORM_WAVES 5
+#endif
 template <class F>
 struct EpiKrylov {
     DState *st;
@@ -193,14 +200,24 @@ struct EpiKrylov {
     RedBuf rb;
     F f;
     double dn = 0.0, dm = 0.0;
+    static constexpr int kWaves = F::kNorm ? CPK_SPMV_NORM_WAVES : CPK_SPMV_WAVES;
+    double nb = 0.0;          // F::kNorm: the divisor (0: none)
+    double *xo = nullptr;     // F::kNorm: where the normalised input goes
     __device__ bool skip() { return f.skip(st); }
     __device__ const double *xvec(const double *base) {
         xsel = f.select(st, base);
+        if constexpr (F::kNorm) nb = f.norm(st), xo = f.out(st);
         return xsel;
     }
-    __device__ double pre(int64_t r) const { return xsel[r]; }
+    __device__ double xl(double v) const {
+        if constexpr (F::kNorm) return nb > 0 ? v / nb : v;
+        return v;
+    }
+    __device__ double pre(int64_t r) const { return xl(xsel[r]); }
     __device__ void row(int64_t r, double acc, double xr) {
         y[r] = acc;
+        if constexpr (F::kNorm)
+            if (xo) xo[r] = xr;
         if (r < n) dn += acc * xr;
         else dm += acc * xr;
     }

@@ -41,16 +41,28 @@ struct PolStart {  // starts an iteration: decides `running` from `stop`
 };
 
 // cpminres.m:187-189 / cpcglanczos.m:232-234 / cpsymmlq.m:231-268 : u = A*vk; t = C*qk; alpha
-template <int KIND>
+// cpminres with the fused update (raw set): the input is the previous Lanczos step's
+// unnormalised vector; the product divides what it reads by beta and stores vk normalised
+// into its ring slot (EpiKrylov::kNorm), the pass MinresUpdate made on its own before
+template <int KIND, bool NORM = false>
 struct PolLanczosSpmv {
+    static_assert(!NORM || KIND == 0, "the fused update is cpminres's");
+    static constexpr bool kNorm = NORM;
     const double *VQ;
     int64_t N;
     int slot_shift;  // vk = VQ[(kk + slot_shift) % 3]
+    const double *raw = nullptr;  // NORM: the unnormalised input
     __device__ bool skip(DState *st) { return PolStart::start(st); }
     __device__ bool ran(DState *st) const { return st->running != 0; }
     __device__ const double *select(DState *st, const double *) {
+        if (NORM) return raw;
         const int64_t kk = st->k + 1;
         return VQ + ((kk + slot_shift) % 3) * N;
+    }
+    __device__ double norm(DState *st) const { return st->beta; }
+    __device__ double *out(DState *st) const {
+        const int64_t kk = st->k + 1;
+        return const_cast<double *>(VQ) + ((kk + slot_shift) % 3) * N;
     }
     __device__ void fin(DState *st, const double *tot) {
         const int64_t kk = st->k + 1;
@@ -81,6 +93,7 @@ struct PolLanczosSpmv {
 
 // cpcg.m:151-154 : Ap = A*p; pAp; Cq = C*q; qCq; alpha = residNorm2/(pAp+qCq)
 struct PolCgSpmv {
+    static constexpr bool kNorm = false;
     const double *PQ;
     __device__ bool skip(DState *st) { return PolStart::start(st); }
     __device__ bool ran(DState *st) const { return st->running != 0; }
@@ -101,6 +114,7 @@ struct PolCgSpmv {
 
 // GMRES family: u = A*V_k; t = C*Q_k (no inner products needed)
 struct PolArnoldiSpmv {
+    static constexpr bool kNorm = false;
     const double *V;
     int64_t N;
     int64_t ring;  // 0: GMRES (column k-1), >0: DQGMRES ring size mem+1
@@ -116,6 +130,7 @@ struct PolArnoldiSpmv {
 
 // Pre-step spmv (cpsymmlq.m:198-200): no running/stop logic.
 struct PolPlainSpmv {
+    static constexpr bool kNorm = false;
     const double *X;
     __device__ bool skip(DState *) { return false; }
     __device__ bool ran(DState *) const { return true; }
@@ -128,8 +143,12 @@ struct PolPlainSpmv {
 template <class P>
 __global__ void krylov_pack_kernel(P pol, DState *st, const int32_t *__restrict__ idx, int64_t n, double *out) {
     const double *x = pol.select(st, nullptr);
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = x[idx[i]];
+    double nb = 0.0;
+    if constexpr (P::kNorm) nb = pol.norm(st);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double v = x[idx[i]];
+        out[i] = nb > 0 ? v / nb : v;
+    }
 }
 template <class P>
 __global__ void krylov_fin_kernel(P pol, DState *st, const double *tot) {
@@ -260,6 +279,15 @@ struct LanczosStep {
     const double *sep = nullptr;
     int sep_ranks = 0;
     int64_t sep_kt = 0, sep_data = 0, kk = 0;
+    // cpminres, fused update (raw set): the new vector goes to raw unnormalised (the next
+    // Krylov product normalises it), and from the second iteration on this pass also makes the
+    // previous iteration's MinresUpdate w/x update (cpminres.m:221-232): its vk is this step's
+    // vkm1, and its scalars are still in the state (this step's epilogue replaces them)
+    double *raw = nullptr;
+    bool upd = false;
+    double u_oldeps = 0, u_delta = 0, u_gamma = 1, u_tau = 0;
+    const double *u_w1 = nullptr, *u_w2 = nullptr;
+    double *u_wn = nullptr;
     __device__ bool setup() {
         if (!st->running) return false;
         kk = st->k;
@@ -276,7 +304,24 @@ struct LanczosStep {
         vk = VQ + ((kk + sk) % 3) * N;
         vkm1 = VQ + ((kk + skm1) % 3) * N;
         vkp1 = VQ + ((kk + skp1) % 3) * N;
+        if (KIND == 0 && raw) {
+            vkp1 = raw;
+            upd = kk >= 2;
+            if (upd) {  // MinresUpdate's slots at its iteration kp = kk - 1
+                const int64_t kp = kk - 1;
+                u_oldeps = st->oldeps, u_delta = st->delta, u_gamma = st->gamma, u_tau = st->tau;
+                u_wn = W + (kp % 3) * N;
+                u_w2 = W + ((kp + 2) % 3) * N;
+                u_w1 = W + ((kp + 1) % 3) * N;
+            }
+        }
         return true;
+    }
+    // the previous iteration's w/x update of entry i; vprev = its vk (this step's vkm1)
+    __device__ void minres_wx(int64_t i, double vprev, double w1, double w2, double x) {
+        const double w = (vprev - u_oldeps * w1 - u_delta * w2) / u_gamma;
+        u_wn[i] = w;
+        xy[i] = (i < n) ? x + u_tau * w : x - u_tau * w;
     }
     // the new (not yet normalised) Lanczos vector's entry i
     __device__ double value(int64_t i) const {
@@ -294,6 +339,7 @@ struct LanczosStep {
             if (KIND == 1) xy[i] = xy[i] - zeta * W[i];  // y = y - zeta*wq
         }
         vkp1[i] = v;
+        if (KIND == 0 && upd) minres_wx(i, vkm1[i], u_w1[i], u_w2[i], xy[i]);
     }
     // kTile elements kBlock apart (ewtred_kernel): every load of the tile in flight at once; the
     // per-element arithmetic and the thread's accumulation order over its elements are unchanged
@@ -301,6 +347,10 @@ struct LanczosStep {
         if (i0 + (kTile - 1) * kBlock >= Nn) {
             for (int e = 0; e < kTile; e++)
                 if (i0 + e * kBlock < Nn) (*this)(i0 + e * kBlock, acc);
+            return;
+        }
+        if (KIND == 0 && upd) {
+            tile_upd(i0, acc);
             return;
         }
         double p[kTile], a[kTile], b[kTile], u[kTile];
@@ -324,6 +374,32 @@ struct LanczosStep {
                 if (KIND == 1) xy[i] = xy[i] - zeta * W[i];
             }
             vkp1[i] = v;
+        }
+    }
+    // tile() with the fused MINRES update: all seven loads of the tile in flight at once; the
+    // step's arithmetic and accumulation order as in tile(), the update's as in MinresUpdate
+    __device__ void tile_upd(int64_t i0, double *acc) {
+        double p[kTile], a[kTile], b[kTile], u[kTile], w1[kTile], w2[kTile], x[kTile];
+#pragma unroll
+        for (int e = 0; e < kTile; e++) {
+            const int64_t i = i0 + e * kBlock;
+            p[e] = vprec[i], a[e] = vk[i], b[e] = vkm1[i], u[e] = ut[i];
+            w1[e] = u_w1[i], w2[e] = u_w2[i], x[e] = xy[i];
+        }
+#pragma unroll
+        for (int e = 0; e < kTile; e++) {
+            const int64_t i = i0 + e * kBlock;
+            double v;
+            if (i < n) {
+                v = p[e] - alpha * a[e] - beta * b[e];
+                acc[0] += u[e] * v;
+            } else {
+                const double t = a[e] - p[e];
+                v = t - alpha * a[e] - beta * b[e];
+                acc[1] += u[e] * v;
+            }
+            vkp1[i] = v;
+            minres_wx(i, b[e], w1[e], w2[e], x[e]);
         }
     }
     __device__ void fin(const double *tot);
@@ -512,18 +588,21 @@ struct NormalizeCopy {
     }
 };
 
-// cpminres.m:202-232 (normalisation of vkp1 and the w/x/y updates)
+// cpminres.m:202-232 (normalisation of vkp1 and the w/x/y updates).  tail (fused update):
+// after the loop, the last iteration's w/x update, which no next Lanczos step made
 struct MinresUpdate {
     DState *st;
     double *VQ, *W, *xy;
     int64_t n, N;
+    bool tail = false;
     double beta, oldeps, delta, gamma, tau;
     const double *vk, *w1, *w2;
     double *vkp1, *wn;
     __device__ bool setup() {
-        if (!st->running) return false;
+        if (tail ? st->k < 1 : !st->running) return false;
         const int64_t kk = st->k;
-        beta = st->beta, oldeps = st->oldeps, delta = st->delta, gamma = st->gamma, tau = st->tau;
+        beta = tail ? 0.0 : st->beta;  // tail: vkp1 is not normalised (beta > 0 fails)
+        oldeps = st->oldeps, delta = st->delta, gamma = st->gamma, tau = st->tau;
         vk = VQ + (kk % 3) * N;
         vkp1 = VQ + ((kk + 1) % 3) * N;
         wn = W + (kk % 3) * N;
@@ -1582,12 +1661,15 @@ void SolveCore::minres_like(int kind, const double *b, double *xy, cpk_stats *st
     // vprec = M * [u; t] with u = b, t = 0
     launch_set_concat(c, UT, b, n, m);
     M.apply(UT, N, VPREC, nullptr);
+    // cpminres, fused update (below): v1 unnormalised in RAW as well, for the first product
+    double *RAW = kind == 0 && !c.opts.no_minres_fuse ? vec(2) : nullptr;
     if (kind == 0)
         launch_ewred<1>(c, N, InitLanczos<0>{st, VPREC, b, VQ + N, VQ, W + 2 * N, xy, n});
     else if (kind == 1)
         launch_ewred<1>(c, N, InitLanczos<1>{st, VPREC, b, VQ + N, VQ, nullptr, xy, n});
     else
         launch_ewred<1>(c, N, InitLanczos<2>{st, VPREC, b, VQ + N, VQ, W, xy, n});
+    if (RAW) CPK_HIP(hipMemcpyAsync(RAW, VQ + N, sizeof(double) * N, hipMemcpyDeviceToDevice, c.stream));
     launch_ew(c, N, NormalizeCopy{st, VQ + N, kind == 2 ? nullptr : W, 0, 0.0});
     CPK_HIP(hipGetLastError());
     pull();
@@ -1603,28 +1685,37 @@ void SolveCore::minres_like(int kind, const double *b, double *xy, cpk_stats *st
         const bool piggy = c.dist() && M.piggyback_ok() && !c.opts.no_piggy;
         // and beta's partials ride in the next Lanczos vector's halo exchange (spare slots)
         const bool hmerge = piggy && AC.halo() && AC.kstride >= AC.kmax + 2 && !c.opts.no_halo_merge;
-        const PolLanczosSpmv<0> pol{VQ, N, 0};
-        if (hmerge) launch_krylov_halo(c, AC, st, pol);  // v1's halo, before the first iteration
-        auto body = [&]() {
-            if (piggy) {
-                launch_krylov_spmv(c, AC, st, UT, n, pol, true, hmerge);
-                M.apply(UT, n, VPREC, &st->running, c.red.p);
-                if (!hmerge) launch_krylov_fin_sep(c, M.sep, st, pol);  // else in the Lanczos step
-            } else {
-                launch_krylov_spmv(c, AC, st, UT, n, pol);
-                M.apply(UT, n, VPREC, &st->running);
-            }
-            LanczosStep<0> ls{st, VQ, VPREC, UT, xy, W, n, N, 0, 2, 1};
-            if (hmerge) {
-                ls.sep = M.sep.rbuf.p, ls.sep_ranks = c.nranks, ls.sep_kt = M.sep.kt, ls.sep_data = M.sep.kt_data;
-                launch_lanczos_step_halo(c, AC, st, N, ls);
-            } else {
-                launch_ewtred<2>(c, N, ls);
-            }
-            launch_ewt(c, N, MinresUpdate{st, VQ, W, xy, n, N});
+        // fused update: the Lanczos step leaves the new vector unnormalised in RAW and makes the
+        // previous iteration's w/x update; the Krylov product normalises (no MinresUpdate pass)
+        auto iterate = [&](const auto &pol) {
+            if (hmerge) launch_krylov_halo(c, AC, st, pol);  // v1's halo, before the first iteration
+            auto body = [&]() {
+                if (piggy) {
+                    launch_krylov_spmv(c, AC, st, UT, n, pol, true, hmerge);
+                    M.apply(UT, n, VPREC, &st->running, c.red.p);
+                    if (!hmerge) launch_krylov_fin_sep(c, M.sep, st, pol);  // else in the Lanczos step
+                } else {
+                    launch_krylov_spmv(c, AC, st, UT, n, pol);
+                    M.apply(UT, n, VPREC, &st->running);
+                }
+                LanczosStep<0> ls{st, VQ, VPREC, UT, xy, W, n, N, 0, 2, 1};
+                ls.raw = RAW;
+                if (hmerge) {
+                    ls.sep = M.sep.rbuf.p, ls.sep_ranks = c.nranks, ls.sep_kt = M.sep.kt, ls.sep_data = M.sep.kt_data;
+                    launch_lanczos_step_halo(c, AC, st, N, ls);
+                } else {
+                    launch_ewtred<2>(c, N, ls);
+                }
+                if (!RAW) launch_ewt(c, N, MinresUpdate{st, VQ, W, xy, n, N});
+            };
+            if (print) print_hist_lines("%5lld  %9.2e\n");
+            loop(body, [&]() { print_hist_lines("%5lld  %9.2e\n"); });
         };
-        if (print) print_hist_lines("%5lld  %9.2e\n");
-        loop(body, [&]() { print_hist_lines("%5lld  %9.2e\n"); });
+        if (RAW)
+            iterate(PolLanczosSpmv<0, true>{VQ, N, 0, RAW});
+        else
+            iterate(PolLanczosSpmv<0>{VQ, N, 0});
+        if (RAW) launch_ewt(c, N, MinresUpdate{st, VQ, W, xy, n, N, true});
         if (h.err) raise_error();
         if (print) printf("\n");
         if (stats) stats->solved = h.residNorm <= h.stopTol;
@@ -2046,7 +2137,10 @@ double method_bytes(int method, const DMat &AC, const Precond &M, int64_t iters,
     const double mapply = M.apply_bytes();
     double vec = 0;
     switch (method) {
-    case CPK_MINRES: vec = 8 * N * (5 + 8); break;      // lanczos step (5 streams) + update (8 streams)
+    case CPK_MINRES:  // lanczos step (5 streams) + update (8 streams); fused: the step with the update
+        // (10 streams) and the normalised vector the Krylov product stores (1)
+        vec = 8 * N * (M.ctx && !M.ctx->opts.no_minres_fuse ? 10 + 1 : 5 + 8);
+        break;
     case CPK_CGLANCZOS: vec = 8 * N * (7 + 4); break;
     case CPK_SYMMLQ: vec = 8 * N * (5 + 7); break;
     case CPK_CG: vec = 8 * N * (6 + 5 + 4); break;

@@ -9,6 +9,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "dev.hpp"
 #include "devutil.hpp"
 
@@ -16,12 +18,26 @@ namespace cpk {
 
 // HALO: distributed rows (DistCsr); column c >= nloc reads the allgathered halo xg[c - nloc].
 // A workgroup handles row blocks blockIdx.x, blockIdx.x + gridDim.x, ... (grid: spmv_grid).
-// 6 waves per SIMD (<= 80 VGPRs): the reducing epilogues otherwise take 82 and run 5
-#ifndef CPK_SPMV_WAVES
-#define CPK_SPMV_WAVES 6
-#endif
+// a gathered input value as the epilogue wants it: Epi::xl where it has one (EpiKrylov's
+// normalise-on-read), else as stored.  Halo values arrive already transformed.
+template <class E, class = void>
+struct HasXl : std::false_type {};
+template <class E>
+struct HasXl<E, std::void_t<decltype(&E::xl)>> : std::true_type {};
+template <class Epi>
+__device__ __forceinline__ double gathered(const Epi &e, double v) {
+    if constexpr (HasXl<Epi>::value) return e.xl(v);
+    return v;
+}
+
+// Epi::kWaves where the epilogue sets one (EpiKrylov's normalise-on-read needs more registers)
+template <class E, class = void>
+struct SpmvWaves : std::integral_constant<int, CPK_SPMV_WAVES> {};
+template <class E>
+struct SpmvWaves<E, std::void_t<decltype(E::kWaves)>> : std::integral_constant<int, E::kWaves> {};
+
 template <class Epi, bool HALO = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CPK_SPMV_WAVES))) void spmv_stream(const uint32_t *__restrict__ ptr,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SpmvWaves<Epi>::value))) void spmv_stream(const uint32_t *__restrict__ ptr,
                                                       const int32_t *__restrict__ col,
                                                       const double *__restrict__ val,
                                                       const int32_t *__restrict__ blk, int64_t nblk,
@@ -59,7 +75,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CPK_SPMV
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
             const int32_t c = cc[j];
-            xv[j] = (!HALO || c < nloc) ? x[c] : xg[c - nloc];
+            xv[j] = (!HALO || c < nloc) ? gathered(epi, x[c]) : xg[c - nloc];
         }
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
@@ -83,7 +99,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CPK_SPMV
             const uint32_t c1 = min(e1, c0 + (uint32_t)kSpmvCap);
             for (uint32_t e = c0 + tid; e < c1; e += kBlock) {
                 const int32_t c = col[e];
-                const double xv = (!HALO || c < nloc) ? x[c] : xg[c - nloc];
+                const double xv = (!HALO || c < nloc) ? gathered(epi, x[c]) : xg[c - nloc];
                 prod[e - c0] = (c >= col_min) ? val[e] * xv : 0.0;
             }
             __syncthreads();

@@ -266,6 +266,27 @@ def test_dist_minres_merged_exchanges(P):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("P", [2, 3])
+def test_dist_minres_fused_update_bitexact(P):
+    """Distributed cpminres with the update folded into the Lanczos step and the Krylov product
+    (the halo the product reads is normalised by the owners' formula) equals the separate
+    MinresUpdate pass bit for bit, with each exchange variant."""
+    import cpkrylov_amd as cpk
+    Pd = F.load("cvxqp1_m")
+    opts = dict(F.EXPROG_OPTS)
+
+    def work(ctx, r):
+        x, stats, flag = cpk.reg_cpkrylov(cpk.cpminres, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts, ctx=ctx)
+        return x, stats["residHistory"], stats["niters"]
+
+    for variant in ({}, {"no_halo_merge": 1}, {"no_piggy": 1}):
+        a = _run_ranks(P, work, dict(variant))[0]
+        b = _run_ranks(P, work, dict(variant, no_minres_fuse=1))[0]
+        assert a[2] == b[2] and np.array_equal(a[1], b[1]), variant
+        assert np.array_equal(a[0], b[0]), (variant, np.max(np.abs(a[0] - b[0])))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("path", ["tsolve_global", "tsolve_onepass"])
 @pytest.mark.parametrize("P", [2, 4])
 def test_dist_apply_separator_fallbacks_bitexact(P, path):

@@ -390,3 +390,27 @@ def test_precond_apply_fused_last_round(gpu_ctx, name, props):
         yo = Mo @ z
         for y in ys:
             assert np.array_equal(y, yo)
+
+@pytest.mark.parametrize("name", ["cvxqp1_m", "syn_symm20k"])
+@pytest.mark.parametrize("extra", [{}, {"itmax": 1}, {"itmax": 2}, {"itmax": 7}])
+@pytest.mark.parametrize("batch", [0, 3])
+def test_minres_fused_update_bitexact(gpu_ctx, name, extra, batch):
+    """cpminres with the update folded into the Lanczos step and the Krylov product (default)
+    against the separate MinresUpdate pass (engine option no_minres_fuse): x, the history and
+    the iteration count bit for bit -- including solves that stop at itmax inside a graph batch,
+    where the last iteration's update runs after the loop."""
+    import cpkrylov_amd as cpk
+    P = F.load(name)
+    opts = dict(F.EXPROG_OPTS, **extra)
+    out = []
+    for fuse_off in (0, 1):
+        ctx = cpk.Context(device=0, options={"no_minres_fuse": fuse_off, "batch": batch})
+        try:
+            x, stats, flag = cpk.reg_cpkrylov(cpk.cpminres, P["rhs"], P["Q"], P["B"], P["C"], P["G"], opts, ctx=ctx)
+            out.append((x, stats["residHistory"], stats["niters"]))
+            del stats  # its preconditioner, before the context
+        finally:
+            ctx.close()
+    (x0, h0, n0), (x1, h1, n1) = out
+    assert n0 == n1 and np.array_equal(h0, h1)
+    assert np.array_equal(x0, x1), np.max(np.abs(x0 - x1))
