@@ -391,9 +391,9 @@ def test_precond_apply_fused_last_round(gpu_ctx, name, props):
         for y in ys:
             assert np.array_equal(y, yo)
 
-@pytest.mark.parametrize("name", ["cvxqp1_m", "syn_symm20k"])
-@pytest.mark.parametrize("extra", [{}, {"itmax": 1}, {"itmax": 2}, {"itmax": 7}])
-@pytest.mark.parametrize("batch", [0, 3])
+@pytest.mark.parametrize("name,extra,batch", [("cvxqp1_m", {}, 0), ("cvxqp1_m", {}, 3), ("cvxqp1_m", {"itmax": 1}, 0),
+                                              ("cvxqp1_m", {"itmax": 2}, 3), ("cvxqp1_m", {"itmax": 7}, 3),
+                                              ("syn_symm20k", {}, 0)])
 def test_minres_fused_update_bitexact(gpu_ctx, name, extra, batch):
     """cpminres with the update folded into the Lanczos step and the Krylov product (default)
     against the separate MinresUpdate pass (engine option no_minres_fuse): x, the history and
