@@ -108,9 +108,18 @@ static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &
         throw Error(CPK_ERR_NOMEM, "factor too large for 32-bit entry offsets");
     lap("prefix");
     const int64_t nnz = sym.Rp[N];
-    sym.Rc.resize(nnz);
-    sym.kp_tgt.resize(sym.kp_ptr[N]);
-    sym.kp_src.resize(sym.kp_ptr[N]);
+    {
+        // the five large outputs are zero-filled on their own threads: the first touch of fresh
+        // pages (kernel faults) is the cost of a resize, and it runs in parallel this way
+        std::vector<std::thread> al;
+        al.emplace_back([&] { sym.Rc.resize(nnz); });
+        al.emplace_back([&] { sym.kp_tgt.resize(sym.kp_ptr[N]); });
+        al.emplace_back([&] { sym.kp_src.resize(sym.kp_ptr[N]); });
+        al.emplace_back([&] { f.Li.resize(nnz); });
+        al.emplace_back([&] { f.Lp.assign(N + 1, 0); });
+        sym.Rcsc.resize(nnz);
+        for (auto &x : al) x.join();
+    }
     lap("alloc");
     {
         std::vector<std::thread> cp;
@@ -136,33 +145,59 @@ static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &
     }
     lap("concat");
     // columns of L: rows in ascending order within each column (the serial loop's lnz[i]++ order)
-    f.Lp.assign(N + 1, 0);
-    for (int64_t q = 0; q < nnz; q++) f.Lp[sym.Rc[q] + 1]++;
+    parallel_for(nnz, [&](int64_t lo, int64_t hi) {  // column counts: a histogram, order-free
+        for (int64_t q = lo; q < hi; q++) __atomic_fetch_add(&f.Lp[sym.Rc[q] + 1], (int64_t)1, __ATOMIC_RELAXED);
+    }, 1 << 18);
     for (int64_t i = 0; i < N; i++) f.Lp[i + 1] += f.Lp[i];
-    f.Li.resize(nnz);
-    sym.Rcsc.resize(nnz);
+    lap("column counts");
     {
-        // threads own column ranges of equal entry counts; each scans the rows in ascending
-        // order and places the entries of its columns (so a column's rows stay ascending)
-        std::vector<int64_t> cut(T + 1, N);
-        cut[0] = 0;
-        for (int t = 1; t < T; t++)
-            cut[t] = std::upper_bound(f.Lp.begin(), f.Lp.end(), nnz * t / T) - f.Lp.begin() - 1;
+        // a parallel transpose: thread t owns the row range rcut[t] .. rcut[t+1) and the column
+        // range ccut[t] .. ccut[t+1) (equal entry counts each).  Every thread sorts its rows'
+        // entries into one bucket per column owner (row entries in ascending row order); each
+        // owner then places its buckets in thread order, so a column's rows stay ascending: the
+        // placement of the serial lnz[i]++ loop, with each entry visited three times in all
+        // rather than once per thread
+        std::vector<int64_t> ccut(T + 1, N), rcut(T + 1, N);
+        ccut[0] = rcut[0] = 0;
+        for (int t = 1; t < T; t++) {
+            ccut[t] = std::upper_bound(f.Lp.begin(), f.Lp.end(), nnz * t / T) - f.Lp.begin() - 1;
+            rcut[t] = std::upper_bound(sym.Rp.begin(), sym.Rp.end(), (int32_t)(nnz * t / T)) - sym.Rp.begin() - 1;
+        }
+        std::vector<uint8_t> owner(N);
+        for (int t = 0; t < T; t++) std::fill(owner.begin() + ccut[t], owner.begin() + ccut[t + 1], (uint8_t)t);
+        // bucket (t, u): row entries q of thread t's rows whose column thread u owns
+        std::vector<std::vector<int64_t>> boff(T, std::vector<int64_t>(T + 1, 0));
+        std::vector<std::vector<int32_t>> bq(T);  // thread t's entries, grouped by owner
         std::vector<std::thread> cth;
-        auto place = [&](int t) {
-            const int32_t c0 = (int32_t)cut[t], c1 = (int32_t)cut[t + 1];
-            if (c0 >= c1) return;
-            std::vector<int64_t> nx(f.Lp.begin() + c0, f.Lp.begin() + c1);
-            for (int64_t k = 0; k < N; k++)
-                for (int32_t q = sym.Rp[k]; q < sym.Rp[k + 1]; q++) {
-                    const int32_t i = sym.Rc[q];
-                    if (i < c0 || i >= c1) continue;
-                    const int64_t p2 = nx[i - c0]++;
+        auto bucket = [&](int t) {
+            const int32_t q0 = sym.Rp[rcut[t]], q1 = sym.Rp[rcut[t + 1]];
+            std::vector<int64_t> &o = boff[t];
+            for (int32_t q = q0; q < q1; q++) o[owner[sym.Rc[q]] + 1]++;
+            for (int u = 0; u < T; u++) o[u + 1] += o[u];
+            std::vector<int64_t> nx(o.begin(), o.end() - 1);
+            bq[t].resize((size_t)(q1 - q0));
+            for (int32_t q = q0; q < q1; q++) bq[t][nx[owner[sym.Rc[q]]]++] = q;
+        };
+        auto place = [&](int u) {
+            const int64_t c0 = ccut[u];
+            std::vector<int64_t> nx(f.Lp.begin() + c0, f.Lp.begin() + ccut[u + 1]);
+            for (int t = 0; t < T; t++) {  // row ranges ascending, rows ascending within each
+                int64_t k = rcut[t];
+                for (int64_t s = boff[t][u]; s < boff[t][u + 1]; s++) {
+                    const int32_t q = bq[t][s];
+                    while (sym.Rp[k + 1] <= q) k++;
+                    const int64_t p2 = nx[sym.Rc[q] - c0]++;
                     f.Li[p2] = (int32_t)k;
                     sym.Rcsc[q] = (int32_t)p2;
                 }
+            }
         };
-        for (int t = 1; t < T; t++) cth.emplace_back(place, t);
+        for (int t = 1; t < T; t++) cth.emplace_back(bucket, t);
+        bucket(0);
+        for (auto &x : cth) x.join();
+        lap("column buckets");
+        cth.clear();
+        for (int u = 1; u < T; u++) cth.emplace_back(place, u);
         place(0);
         for (auto &x : cth) x.join();
     }
@@ -308,7 +343,9 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     // entries (rows of L) and at most CAP backward entries (columns of L).  With
     // wt(v) = max(CAP/R, fwd(v), bwd(v)), a cluster of total weight <= CAP meets all three.
     std::vector<int32_t> ent(N), nfwd(N, 0);  // nfwd: forward entries (row counts of L)
-    for (int32_t i : f.Li) nfwd[i]++;
+    parallel_for((int64_t)f.Li.size(), [&](int64_t lo, int64_t hi) {  // a histogram: order-free
+        for (int64_t p = lo; p < hi; p++) __atomic_fetch_add(&nfwd[f.Li[p]], 1, __ATOMIC_RELAXED);
+    }, 1 << 18);
     parallel_for(N, [&](int64_t lo, int64_t hi) {
         for (int64_t v = lo; v < hi; v++)
             ent[v] = (int32_t)std::max<int64_t>(nfwd[v], f.Lp[v + 1] - f.Lp[v] + (extra_bwd ? (*extra_bwd)[v] : 0));
@@ -511,18 +548,22 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
 Factor relabel(const Factor &f, const Schedule &s, std::vector<int32_t> *src) {
     const int64_t N = f.N;
     std::vector<int32_t> pos(N);
-    for (int64_t q = 0; q < N; q++) pos[s.order[q]] = (int32_t)q;
+    parallel_for(N, [&](int64_t lo, int64_t hi) {  // order is a permutation: disjoint writes
+        for (int64_t q = lo; q < hi; q++) pos[s.order[q]] = (int32_t)q;
+    }, 1 << 16);
     Factor g;
     g.N = N;
     g.perm.resize(N);
     if (!f.D.empty()) g.D.resize(N);
-    g.parent.assign(N, -1);
-    for (int64_t q = 0; q < N; q++) {
-        int32_t old = s.order[q];
-        g.perm[q] = f.perm[old];
-        if (!f.D.empty()) g.D[q] = f.D[old];
-        if (f.parent[old] >= 0) g.parent[q] = pos[f.parent[old]];
-    }
+    g.parent.resize(N);
+    parallel_for(N, [&](int64_t lo, int64_t hi) {
+        for (int64_t q = lo; q < hi; q++) {
+            int32_t old = s.order[q];
+            g.perm[q] = f.perm[old];
+            if (!f.D.empty()) g.D[q] = f.D[old];
+            g.parent[q] = f.parent[old] >= 0 ? pos[f.parent[old]] : -1;
+        }
+    }, 1 << 16);
     g.Lp.assign(N + 1, 0);
     for (int64_t q = 0; q < N; q++) {
         int32_t old = s.order[q];

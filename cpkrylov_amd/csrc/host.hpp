@@ -64,6 +64,12 @@ void parallel_for(int64_t n, F f, int64_t grain = 4096) {
     f(int64_t(0), std::min(n, chunk));
     for (auto &x : th) x.join();
 }
+// Rows of a column-compressed pattern (columns Lp / Li of an N x N matrix): rptr (N + 1), and
+// for row i its columns rcol[rptr[i] ..) ascending with their column slots ridx (the serial
+// column-by-column transpose, exactly), on host_threads() threads: each thread buckets the
+// entries of an equal share of the columns by the thread owning their row, then places the
+// rows it owns from those buckets in column order.  rcol / ridx must hold Lp[N] entries.
+void transpose_pattern(int64_t N, const int64_t *Lp, const int32_t *Li, uint32_t *rptr, int32_t *rcol, int32_t *ridx);
 // CPK_TIMING=1: wall times of the sub-phases of a host phase on stderr (diagnostic)
 struct SubClock {
     bool on = getenv("CPK_TIMING") != nullptr;

@@ -1,11 +1,69 @@
 // hostsparse.cpp -- host CSR conversions and the Kp = [A B'; B C] assembly (ops/opLDL2.m:81).
 #include <algorithm>
 #include <numeric>
+#include <thread>
 
 #include "cpk.h"
 #include "host.hpp"
 
 namespace cpk {
+
+void transpose_pattern(int64_t N, const int64_t *Lp, const int32_t *Li, uint32_t *rptr, int32_t *rcol, int32_t *ridx) {
+    const int64_t nnz = Lp[N];
+    const int T = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), (nnz + 262143) / 262144));
+    // thread t: columns ccut[t] .. ccut[t+1) (equal entry counts) for the bucketing, rows
+    // t * rs .. (t + 1) * rs for the placement
+    std::vector<int64_t> ccut(T + 1, N);
+    ccut[0] = 0;
+    for (int t = 1; t < T; t++) ccut[t] = std::upper_bound(Lp, Lp + N + 1, nnz * t / T) - Lp - 1;
+    const int64_t rs = (N + T - 1) / T;
+    std::vector<std::vector<int64_t>> boff(T, std::vector<int64_t>(T + 1, 0));
+    std::vector<std::vector<int32_t>> bp(T);  // thread t's column slots, grouped by row owner
+    std::vector<std::thread> th;
+    auto bucket = [&](int t) {
+        const int64_t p0 = Lp[ccut[t]], p1 = Lp[ccut[t + 1]];
+        std::vector<int64_t> &o = boff[t];
+        for (int64_t p = p0; p < p1; p++) o[Li[p] / rs + 1]++;
+        for (int u = 0; u < T; u++) o[u + 1] += o[u];
+        std::vector<int64_t> nx(o.begin(), o.end() - 1);
+        bp[t].resize((size_t)(p1 - p0));
+        for (int64_t p = p0; p < p1; p++) bp[t][nx[Li[p] / rs]++] = (int32_t)p;
+    };
+    std::vector<int64_t> base(T + 1, 0);  // entries of the rows before each row range
+    auto place = [&](int u) {
+        const int64_t r0 = std::min<int64_t>(N, u * rs), r1 = std::min<int64_t>(N, r0 + rs);
+        std::vector<uint32_t> cnt(r1 - r0 + 1, 0);
+        for (int t = 0; t < T; t++)
+            for (int64_t s = boff[t][u]; s < boff[t][u + 1]; s++) cnt[Li[bp[t][s]] - r0 + 1]++;
+        uint32_t acc = (uint32_t)base[u];
+        for (int64_t i = r0; i < r1; i++) acc += cnt[i - r0 + 1], cnt[i - r0 + 1] = acc;
+        cnt[0] = (uint32_t)base[u];
+        for (int64_t i = r0; i < r1; i++) rptr[i + 1] = cnt[i - r0 + 1];
+        for (int t = 0; t < T; t++) {  // column ranges ascending, columns ascending within each
+            int64_t j = ccut[t];
+            for (int64_t s = boff[t][u]; s < boff[t][u + 1]; s++) {
+                const int32_t p = bp[t][s];
+                while (Lp[j + 1] <= p) j++;
+                const uint32_t q = cnt[Li[p] - r0]++;
+                rcol[q] = (int32_t)j;
+                ridx[q] = p;
+            }
+        }
+    };
+    for (int t = 1; t < T; t++) th.emplace_back(bucket, t);
+    bucket(0);
+    for (auto &x : th) x.join();
+    th.clear();
+    for (int u = 0; u < T; u++) {
+        int64_t tot = 0;
+        for (int t = 0; t < T; t++) tot += boff[t][u + 1] - boff[t][u];
+        base[u + 1] = base[u] + tot;
+    }
+    rptr[0] = 0;
+    for (int u = 1; u < T; u++) th.emplace_back(place, u);
+    place(0);
+    for (auto &x : th) x.join();
+}
 
 // Canonicalise: sort each row by column, sum duplicates (MATLAB sparse arrays never hold any).
 static void canonicalise(HCsr &a) {
@@ -104,15 +162,24 @@ HCsr assemble_kp(const HCsr &A, const HCsr &B, const HCsr &C) {
     if (B.ncols != A.nrows || B.nrows != C.nrows) throw Error(CPK_ERR_DIM, "Incompatible dimensions.");
     const int64_t n = A.nrows, m = C.nrows, N = n + m;
     if (N > INT32_MAX) throw Error(CPK_ERR_DIM, "N exceeds the 32-bit index range");
-    HCsr Bt = transpose(B);
     HCsr K;
     K.nrows = K.ncols = N;
+    // the entry arrays are zero-filled (first touch of fresh pages) on their own threads while
+    // this one transposes B
+    const int64_t nnz = A.nnz() + 2 * B.nnz() + C.nnz();
+    std::thread zi([&] { K.ind.resize(nnz); }), zv([&] { K.val.resize(nnz); });
+    HCsr Bt;
+    try {
+        Bt = transpose(B);
+    } catch (...) {
+        zi.join(), zv.join();
+        throw;
+    }
     K.ptr.assign(N + 1, 0);
     for (int64_t i = 0; i < n; i++) K.ptr[i + 1] = K.ptr[i] + (A.ptr[i + 1] - A.ptr[i]) + (Bt.ptr[i + 1] - Bt.ptr[i]);
     for (int64_t i = 0; i < m; i++)
         K.ptr[n + i + 1] = K.ptr[n + i] + (B.ptr[i + 1] - B.ptr[i]) + (C.ptr[i + 1] - C.ptr[i]);
-    K.ind.resize(K.ptr[N]);
-    K.val.resize(K.ptr[N]);
+    zi.join(), zv.join();
     // row i: [A row; B' row shifted by n] (i < n), [B row; C row shifted by n] (i >= n)
     auto put = [&](int64_t row, const HCsr &L, int64_t li, int32_t lshift, const HCsr &R, int64_t ri, int32_t rshift) {
         int64_t q = K.ptr[row];

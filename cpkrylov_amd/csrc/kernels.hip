@@ -79,20 +79,12 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     // forward rows: transpose of the CSC, then each row ordered by the key of its columns;
     // fidx[q] = the CSC slot of forward entry q
     std::vector<uint32_t> fptr(N + 1, 0);
-    for (int32_t i : f.Li) fptr[i + 1]++;
-    for (int64_t i = 0; i < N; i++) fptr[i + 1] += fptr[i];
     const int64_t nf = (int64_t)f.Li.size();
     std::vector<int32_t> fcol, fidx(nf);
     fcol.reserve((size_t)nf + kFactorPadEntries);  // the padding below appends without a reallocation
     fcol.resize(nf);
     {
-        std::vector<uint32_t> nx(fptr.begin(), fptr.end() - 1);
-        for (int64_t j = 0; j < N; j++)
-            for (int64_t p = f.Lp[j]; p < f.Lp[j + 1]; p++) {
-                uint32_t q = nx[f.Li[p]]++;
-                fcol[q] = (int32_t)j;
-                fidx[q] = (int32_t)p;
-            }
+        transpose_pattern(N, f.Lp.data(), f.Li.data(), fptr.data(), fcol.data(), fidx.data());
         if (key)
             parallel_for(N, [&](int64_t lo, int64_t hi) {  // rows sort independently
                 std::vector<std::pair<int64_t, std::pair<int32_t, int32_t>>> row;
@@ -207,21 +199,27 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     d.fcol16.release();
     d.nnz16 = 0;
     if (s.ndet == 0 && s.round_ptr.size() >= 2 && !d.no_col16) {
-        bool ok = true;
+        const int64_t b0 = s.round_ptr[0], nb0 = s.round_ptr[1] - b0;
+        std::atomic<bool> bad{false};
         int64_t e_end = 0;
-        for (int64_t b = s.round_ptr[0]; b < s.round_ptr[1] && ok; b++) {
-            const int32_t *m = &meta[(size_t)b * 8];
-            if (m[1] - m[0] > INT16_MAX) ok = false;
-            for (int32_t e = m[4]; e < m[5] && ok; e++) ok = fcol[e] >= m[0] && fcol[e] < m[1];
-            e_end = std::max<int64_t>(e_end, m[5]);
-        }
-        if (ok) {
-            std::vector<int16_t> c16((size_t)e_end + kFactorPadEntries, 0);
-            for (int64_t b = s.round_ptr[0]; b < s.round_ptr[1]; b++) {
+        for (int64_t b = b0; b < b0 + nb0; b++) e_end = std::max<int64_t>(e_end, meta[(size_t)b * 8 + 5]);
+        parallel_for(nb0, [&](int64_t lo, int64_t hi) {  // blocks check independently
+            for (int64_t b = b0 + lo; b < b0 + hi && !bad.load(std::memory_order_relaxed); b++) {
                 const int32_t *m = &meta[(size_t)b * 8];
-                for (int32_t e = m[4]; e < m[5]; e++) c16[e] = (int16_t)(fcol[e] - m[0]);
-                d.nnz16 += m[5] - m[4];
+                bool ok = m[1] - m[0] <= INT16_MAX;
+                for (int32_t e = m[4]; e < m[5] && ok; e++) ok = fcol[e] >= m[0] && fcol[e] < m[1];
+                if (!ok) bad = true;
             }
+        }, 1024);
+        if (!bad) {
+            std::vector<int16_t> c16((size_t)e_end + kFactorPadEntries, 0);
+            parallel_for(nb0, [&](int64_t lo, int64_t hi) {
+                for (int64_t b = b0 + lo; b < b0 + hi; b++) {
+                    const int32_t *m = &meta[(size_t)b * 8];
+                    for (int32_t e = m[4]; e < m[5]; e++) c16[e] = (int16_t)(fcol[e] - m[0]);
+                }
+            }, 1024);
+            for (int64_t b = b0; b < b0 + nb0; b++) d.nnz16 += meta[(size_t)b * 8 + 5] - meta[(size_t)b * 8 + 4];
             d.fcol16.upload(c16);
         }
     }
