@@ -25,7 +25,8 @@ namespace cpk {
 // serial loop below with numeric == false: the elimination tree by Liu's algorithm with path
 // compression (cs_etree), then every row's pattern -- the union of the tree paths from its Kp
 // entries up to the row, sorted ascending -- rows in parallel (each thread stamps its own
-// marker array), then the columns of L by a counting pass over the rows in ascending order.
+// marker array), then the columns of L by a parallel transpose that keeps each column's rows
+// ascending (the serial loop's order).
 static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &perm, LdlSymbolic &sym) {
     const int64_t N = Kp.nrows;
     auto T0 = std::chrono::steady_clock::now();
@@ -109,7 +110,7 @@ static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &
     lap("prefix");
     const int64_t nnz = sym.Rp[N];
     {
-        // the five large outputs are zero-filled on their own threads: the first touch of fresh
+        // the large outputs are zero-filled on threads of their own: the first touch of fresh
         // pages (kernel faults) is the cost of a resize, and it runs in parallel this way
         std::vector<std::thread> al;
         al.emplace_back([&] { sym.Rc.resize(nnz); });
@@ -569,15 +570,37 @@ Factor relabel(const Factor &f, const Schedule &s, std::vector<int32_t> *src) {
         int32_t old = s.order[q];
         g.Lp[q + 1] = g.Lp[q] + (f.Lp[old + 1] - f.Lp[old]);
     }
-    g.Li.resize(f.Li.size());
     const bool vals = (int64_t)f.D.size() == N;  // numeric factor (Lx may be empty: no entries)
-    if (vals) g.Lx.resize(f.Lx.size());
-    if (src) src->resize(f.Li.size());
+    {
+        std::vector<std::thread> al;  // zero-fills (first touch of fresh pages) side by side
+        if (vals) al.emplace_back([&] { g.Lx.resize(f.Lx.size()); });
+        if (src) al.emplace_back([&] { src->resize(f.Li.size()); });
+        g.Li.resize(f.Li.size());
+        for (auto &x : al) x.join();
+    }
     std::atomic<bool> bad{false};
     parallel_for(N, [&](int64_t lo, int64_t hi) {  // columns relabel independently
         std::vector<std::pair<int32_t, int64_t>> col;
         for (int64_t q = lo; q < hi; q++) {
             int32_t old = s.order[q];
+            const int64_t len = f.Lp[old + 1] - f.Lp[old];
+            if (len <= 32) {  // short columns: insertion sort in place (new indices are distinct)
+                const int64_t b = g.Lp[q];
+                int64_t sp[32];
+                for (int64_t t = 0; t < len; t++) {
+                    const int64_t p = f.Lp[old] + t;
+                    const int32_t r = pos[f.Li[p]];
+                    int64_t u = t;
+                    for (; u > 0 && g.Li[b + u - 1] > r; u--) g.Li[b + u] = g.Li[b + u - 1], sp[u] = sp[u - 1];
+                    g.Li[b + u] = r, sp[u] = p;
+                }
+                for (int64_t t = 0; t < len; t++) {
+                    if (g.Li[b + t] <= q) bad = true;
+                    if (vals) g.Lx[b + t] = f.Lx[sp[t]];
+                    if (src) (*src)[b + t] = (int32_t)sp[t];
+                }
+                continue;
+            }
             col.clear();
             for (int64_t p = f.Lp[old]; p < f.Lp[old + 1]; p++) col.emplace_back(pos[f.Li[p]], p);
             std::sort(col.begin(), col.end(), [](auto &a, auto &b) { return a.first < b.first; });

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <atomic>
 #include <array>
+#include <thread>
 #include <tuple>
 #include <cstdlib>
 #include <cstring>
@@ -60,6 +61,7 @@ void make_dmat(const HCsr &a, DMat &d) {
 // by descending key of the row.  key[q] is the pre-relabel index of relabelled row q (so a
 // relabelled factor still sums in the exported factor's order); extra[q] are backward entries
 // of row q that refer to rows outside this factor (distributed separators).
+constexpr int64_t kInsertionSortMax = 32;  // rows up to this long sort by insertion (keys are distinct)
 void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vector<int64_t> *key,
                   const std::vector<std::vector<BwdExtra>> *extra, std::vector<int32_t> *fsrc,
                   std::vector<int32_t> *bsrc) {
@@ -80,20 +82,39 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     // fidx[q] = the CSC slot of forward entry q
     std::vector<uint32_t> fptr(N + 1, 0);
     const int64_t nf = (int64_t)f.Li.size();
-    std::vector<int32_t> fcol, fidx(nf);
-    fcol.reserve((size_t)nf + kFactorPadEntries);  // the padding below appends without a reallocation
-    fcol.resize(nf);
+    std::vector<int32_t> fcol, fidx, bcol, bidx;
+    {
+        // the large index arrays are zero-filled (first touch of fresh pages) on threads of their
+        // own; the padding below appends without a reallocation
+        std::vector<std::thread> al;
+        al.emplace_back([&] { fcol.reserve((size_t)nf + kFactorPadEntries), fcol.resize(nf); });
+        al.emplace_back([&] { bcol.reserve((size_t)d.nnz + kFactorPadEntries), bcol.resize(d.nnz); });
+        al.emplace_back([&] { bidx.resize(bsrc ? d.nnz : 0); });
+        fidx.resize(nf);
+        for (auto &x : al) x.join();
+    }
     {
         transpose_pattern(N, f.Lp.data(), f.Li.data(), fptr.data(), fcol.data(), fidx.data());
         if (key)
-            parallel_for(N, [&](int64_t lo, int64_t hi) {  // rows sort independently
+            parallel_for(N, [&](int64_t lo, int64_t hi) {  // rows sort independently (keys distinct)
                 std::vector<std::pair<int64_t, std::pair<int32_t, int32_t>>> row;
                 for (int64_t i = lo; i < hi; i++) {
+                    const uint32_t a = fptr[i], z = fptr[i + 1];
+                    if (z - a <= kInsertionSortMax) {  // short rows: insertion sort in place
+                        for (uint32_t q = a + 1; q < z; q++) {
+                            const int32_t c = fcol[q], x = fidx[q];
+                            const int64_t kc = K(c);
+                            uint32_t r = q;
+                            for (; r > a && K(fcol[r - 1]) > kc; r--) fcol[r] = fcol[r - 1], fidx[r] = fidx[r - 1];
+                            fcol[r] = c, fidx[r] = x;
+                        }
+                        continue;
+                    }
                     row.clear();
-                    for (uint32_t q = fptr[i]; q < fptr[i + 1]; q++) row.push_back({K(fcol[q]), {fcol[q], fidx[q]}});
+                    for (uint32_t q = a; q < z; q++) row.push_back({K(fcol[q]), {fcol[q], fidx[q]}});
                     std::sort(row.begin(), row.end(), [](auto &x, auto &y) { return x.first < y.first; });
                     for (size_t t = 0; t < row.size(); t++)
-                        fcol[fptr[i] + t] = row[t].second.first, fidx[fptr[i] + t] = row[t].second.second;
+                        fcol[a + t] = row[t].second.first, fidx[a + t] = row[t].second.second;
                 }
             });
     }
@@ -109,14 +130,30 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     std::vector<uint32_t> bptr(N + 1, 0);
     for (int64_t j = 0; j < N; j++)
         bptr[j + 1] = bptr[j] + (uint32_t)(f.Lp[j + 1] - f.Lp[j]) + (uint32_t)(extra ? (*extra)[j].size() : 0);
-    std::vector<int32_t> bcol, bidx(bsrc ? d.nnz : 0);
-    bcol.reserve((size_t)d.nnz + kFactorPadEntries);
-    bcol.resize(d.nnz);
     const bool bvals = vals || nextra > 0;
     std::vector<double> bval(bvals ? d.nnz : 0, 0.0);
     parallel_for(N, [&](int64_t lo, int64_t hi) {  // rows (columns of L) sort independently
         std::vector<std::pair<int64_t, std::pair<int32_t, int64_t>>> row;  // (key, (col, CSC slot | ~extra))
         for (int64_t j = lo; j < hi; j++) {
+            const int64_t len = f.Lp[j + 1] - f.Lp[j];
+            const uint32_t b = bptr[j];
+            if ((!extra || (*extra)[j].empty()) && len <= kInsertionSortMax) {
+                // short columns without extra entries: insertion sort (keys descending) in place
+                int64_t src[kInsertionSortMax];
+                for (int64_t t = 0; t < len; t++) {
+                    const int64_t p = f.Lp[j] + t;
+                    const int32_t c = f.Li[p];
+                    const int64_t kc = K(c);
+                    int64_t r = t;
+                    for (; r > 0 && K(bcol[b + r - 1]) < kc; r--) bcol[b + r] = bcol[b + r - 1], src[r] = src[r - 1];
+                    bcol[b + r] = c, src[r] = p;
+                }
+                for (int64_t t = 0; t < len; t++) {
+                    if (vals) bval[b + t] = f.Lx[src[t]];
+                    if (bsrc) bidx[b + t] = (int32_t)src[t];
+                }
+                continue;
+            }
             row.clear();
             for (int64_t p = f.Lp[j]; p < f.Lp[j + 1]; p++) row.push_back({K(f.Li[p]), {f.Li[p], p}});
             if (extra)
@@ -124,10 +161,10 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
             std::sort(row.begin(), row.end(), [](auto &x, auto &y) { return x.first > y.first; });
             for (size_t t = 0; t < row.size(); t++) {
                 const int64_t src = row[t].second.second;
-                bcol[bptr[j] + t] = row[t].second.first;
-                if (src < 0) bval[bptr[j] + t] = (*extra)[j][~src].val;
-                else if (vals) bval[bptr[j] + t] = f.Lx[src];
-                if (bsrc) bidx[bptr[j] + t] = (int32_t)src;
+                bcol[b + t] = row[t].second.first;
+                if (src < 0) bval[b + t] = (*extra)[j][~src].val;
+                else if (vals) bval[b + t] = f.Lx[src];
+                if (bsrc) bidx[b + t] = (int32_t)src;
             }
         }
     });

@@ -9,6 +9,7 @@
 //     by nested dissection (large) or minimum degree (small);
 //   - otherwise nested dissection / minimum degree on the whole graph of Kp.
 #include <algorithm>
+#include <cstdio>
 #include <atomic>
 #include <cstdlib>
 #include <memory>
@@ -55,6 +56,65 @@ static HCsr graph_from_edges(int64_t nv, std::vector<std::pair<int32_t, int32_t>
     for (int64_t i = 0; i < nv; i++) g.ptr[i + 1] = g.ptr[i] + deg[i];
     g.ind.resize(g.ptr[nv]);
     parallel_for(nv, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; i++) std::copy(adj.begin() + cnt[i], adj.begin() + cnt[i] + deg[i], g.ind.begin() + g.ptr[i]);
+    });
+    return g;
+}
+
+// The Schur-complement graph on the m constraint rows of Kp (G diagonal): the clique of each G
+// column's B entries plus C's pattern, the graph graph_from_edges builds from those edges.  Its
+// neighbour lists end sorted and unique, so the order in which entries land does not matter:
+// threads count and place theirs concurrently (relaxed atomic slots), with no edge list.
+static HCsr schur_graph(const HCsr &Kp, int64_t n, int64_t m) {
+    std::vector<int64_t> cnt(m + 1, 0);
+    auto cliques = [&](auto &&add) {
+        parallel_for(n, [&](int64_t lo, int64_t hi) {
+            int32_t nb[64];
+            std::vector<int32_t> big;
+            for (int64_t j = lo; j < hi; j++) {
+                int k = 0;
+                big.clear();
+                for (int64_t p = Kp.ptr[j]; p < Kp.ptr[j + 1]; p++)
+                    if (Kp.ind[p] >= n) {
+                        if (k < 64) nb[k] = Kp.ind[p] - (int32_t)n;
+                        else big.push_back(Kp.ind[p] - (int32_t)n);
+                        k++;
+                    }
+                auto at = [&](int t) { return t < 64 ? nb[t] : big[t - 64]; };
+                for (int a = 0; a < k; a++)
+                    for (int b = a + 1; b < k; b++)
+                        if (at(a) != at(b)) add(at(a), at(b)), add(at(b), at(a));
+            }
+        }, 1 << 16);
+        parallel_for(m, [&](int64_t lo, int64_t hi) {
+            for (int64_t i = lo; i < hi; i++)
+                for (int64_t p = Kp.ptr[n + i]; p < Kp.ptr[n + i + 1]; p++) {
+                    const int32_t c = Kp.ind[p];
+                    if (c >= n && c - n != i) add((int32_t)i, c - (int32_t)n), add(c - (int32_t)n, (int32_t)i);
+                }
+        }, 1 << 16);
+    };
+    cliques([&](int32_t u, int32_t) { __atomic_fetch_add(&cnt[u + 1], (int64_t)1, __ATOMIC_RELAXED); });
+    for (int64_t i = 0; i < m; i++) cnt[i + 1] += cnt[i];
+    std::vector<int32_t> adj(cnt[m]);
+    {
+        std::vector<int64_t> nx(cnt.begin(), cnt.end() - 1);
+        cliques([&](int32_t u, int32_t v) { adj[__atomic_fetch_add(&nx[u], (int64_t)1, __ATOMIC_RELAXED)] = v; });
+    }
+    std::vector<int64_t> deg(m, 0);
+    parallel_for(m, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; i++) {
+            auto b0 = adj.begin() + cnt[i], b1 = adj.begin() + cnt[i + 1];
+            std::sort(b0, b1);
+            deg[i] = std::unique(b0, b1) - b0;
+        }
+    });
+    HCsr g;
+    g.nrows = g.ncols = m;
+    g.ptr.assign(m + 1, 0);
+    for (int64_t i = 0; i < m; i++) g.ptr[i + 1] = g.ptr[i] + deg[i];
+    g.ind.resize(g.ptr[m]);
+    parallel_for(m, [&](int64_t lo, int64_t hi) {
         for (int64_t i = lo; i < hi; i++) std::copy(adj.begin() + cnt[i], adj.begin() + cnt[i] + deg[i], g.ind.begin() + g.ptr[i]);
     });
     return g;
@@ -172,7 +232,19 @@ struct Nd {
     // (the near half of a dissection: the parent's BFS restricted to it), so the component
     // search is skipped -- it would visit the same nodes in the same order
     void run(std::vector<int32_t> nodes, int32_t lab, int64_t pos, bool bfs_ordered = false) {
+        // CPK_TIMING: the phases of the top subsets (at least 1/16 of the graph), on stderr
+        const size_t n0 = nodes.size();
+        SubClock clk;
+        clk.on = clk.on && (int64_t)n0 * 16 >= g.nrows && n0 > 100000;
+        int nbfs = 0;
+        auto phase = [&](const char *w) {
+            if (!clk.on) return;
+            char buf[96];
+            snprintf(buf, sizeof buf, "  nd %zu: %s (%d BFS)", n0, w, nbfs);
+            clk.lap(buf);
+        };
         std::vector<int32_t> order;
+        order.reserve(n0);  // capacity only: no pages are touched until used, no regrowth copies
         int32_t st = 0;
         if ((int64_t)nodes.size() <= leaf) {
             emit(nodes, pos);
@@ -180,7 +252,7 @@ struct Nd {
         }
         // split into connected components first (one linear pass over the subset)
         if (bfs_ordered) order = nodes;
-        else bfs(nodes[0], lab, order, st);
+        else bfs(nodes[0], lab, order, st), nbfs++;
         if (order.size() < nodes.size()) {
             std::vector<std::pair<int32_t, std::vector<int32_t>>> comps;
             const int32_t stamp0 = st;  // this subset's later BFS get newer stamps
@@ -202,12 +274,16 @@ struct Nd {
         // pseudo-peripheral node; the best start's BFS stays in buffer `cur`, so it is not redone
         int32_t start = order.back();
         int cur = 0;
+        phase("components");
         int32_t ecc = bfs(start, lab, order, st, cur);
+        nbfs = 1;
         for (int it = 0; it < 4; it++) {
             int32_t cand = order.back();
             std::vector<int32_t> o2;
+            o2.reserve(n0);
             int32_t st2;
             int32_t e2 = bfs(cand, lab, o2, st2, 1 - cur);
+            nbfs++;
             if (e2 <= ecc) break;
             ecc = e2, start = cand, order.swap(o2), st = st2, cur = 1 - cur;
         }
@@ -232,6 +308,7 @@ struct Nd {
         // separator: level-s nodes adjacent to level s+1 (the rest join part A)
         const int32_t la = next_label.fetch_add(1), lb = next_label.fetch_add(1), ls = next_label.fetch_add(1);
         std::vector<int32_t> a, b, sep;
+        a.reserve(order.size()), b.reserve(order.size()), sep.reserve(order.size());
         for (int32_t v : order) {
             int32_t d = dist[v];
             if (d < s) a.push_back(v);
@@ -252,6 +329,7 @@ struct Nd {
         nodes.shrink_to_fit();
         const int64_t pa = pos, pb = pos + (int64_t)a.size(), ps = pb + (int64_t)b.size();
         emit(sep, ps);
+        phase("peripheral search");
         const size_t na = std::min(a.size(), b.size());
         // part A (levels < s, and level-s nodes without a neighbour at s + 1) is connected through
         // the BFS tree and listed in BFS order from `start`; part B may fall apart
@@ -305,22 +383,7 @@ std::vector<int32_t> order_kp(const HCsr &Kp, int64_t n, int *kind_out) {
     std::vector<int32_t> perm(N);
     if (g_diag && m > 0) {
         // Schur-complement graph on the m block: cliques of each G column's B entries + C pattern
-        std::vector<std::pair<int32_t, int32_t>> edges;
-        std::vector<int32_t> nb;
-        for (int64_t j = 0; j < n; j++) {
-            nb.clear();
-            for (int64_t p = Kp.ptr[j]; p < Kp.ptr[j + 1]; p++)
-                if (Kp.ind[p] >= n) nb.push_back(Kp.ind[p] - (int32_t)n);
-            for (size_t a = 0; a < nb.size(); a++)
-                for (size_t b = a + 1; b < nb.size(); b++) edges.emplace_back(nb[a], nb[b]);
-        }
-        for (int64_t i = 0; i < m; i++)
-            for (int64_t p = Kp.ptr[n + i]; p < Kp.ptr[n + i + 1]; p++) {
-                int32_t c = Kp.ind[p];
-                if (c >= n && c - n != i) edges.emplace_back((int32_t)i, c - (int32_t)n);
-            }
-        sub_lap("order: Schur-graph edges");
-        HCsr S = graph_from_edges(m, edges);
+        HCsr S = schur_graph(Kp, n, m);
         sub_lap("order: Schur graph");
         std::vector<int32_t> os;
         if (m <= kMdLimit) {
