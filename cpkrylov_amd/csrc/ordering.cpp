@@ -172,7 +172,27 @@ struct Nd {
     std::vector<int32_t> dist_[2], stamp_[2];
     std::vector<int32_t> &dist = dist_[0], &stamp = stamp_[0];
     std::vector<int32_t> out;
-    std::atomic<int32_t> next_label{1}, next_stamp{0};
+    // Subset labels only need to be unique: each thread draws them from a block of its own (one
+    // shared atomic per kLabelBlock labels).  Visit stamps only need to grow along a node's
+    // chain of subsets (a subset's BFS stamps exceed every stamp its ancestors left on its
+    // nodes; disjoint subsets never see each other's), so each subset counts them on from the
+    // value its parent reached: no shared counter, the same decisions
+    static constexpr int32_t kLabelBlock = 1 << 12;
+    std::atomic<int32_t> next_block{1};
+    const uint64_t gen = [] {
+        static std::atomic<uint64_t> g{1};
+        return g.fetch_add(1);
+    }();  // which dissection a thread's block belongs to
+    int32_t new_label() {
+        thread_local uint64_t owner = 0;
+        thread_local int32_t next = 0, end = 0;
+        if (owner != gen || next == end) {
+            owner = gen;
+            next = next_block.fetch_add(kLabelBlock, std::memory_order_relaxed);
+            end = next + kLabelBlock;
+        }
+        return next++;
+    }
     std::atomic<int> spare_threads;
     int leaf;
     Nd(const HCsr &gg, int lf, int threads)
@@ -187,9 +207,9 @@ struct Nd {
     // BFS within nodes of `lab` from `src`; fills `bfs` in visit order, returns eccentricity.
     // Nodes of other subsets (possibly relabelled concurrently by another thread) never carry
     // `lab`, so reading their labels is harmless.
-    int32_t bfs(int32_t src, int32_t lab, std::vector<int32_t> &bfs_order, int32_t &st, int buf = 0) {
+    int32_t bfs(int32_t src, int32_t lab, std::vector<int32_t> &bfs_order, int32_t &st, int32_t &ctr, int buf = 0) {
         std::vector<int32_t> &dst = dist_[buf], &stm = stamp_[buf];
-        st = next_stamp.fetch_add(1, std::memory_order_relaxed) + 1;
+        st = ++ctr;
         bfs_order.clear();
         bfs_order.push_back(src);
         stm[src] = st;
@@ -231,7 +251,7 @@ struct Nd {
     // bfs_ordered: the subset is connected and `nodes` is already its BFS order from nodes[0]
     // (the near half of a dissection: the parent's BFS restricted to it), so the component
     // search is skipped -- it would visit the same nodes in the same order
-    void run(std::vector<int32_t> nodes, int32_t lab, int64_t pos, bool bfs_ordered = false) {
+    void run(std::vector<int32_t> nodes, int32_t lab, int64_t pos, int32_t ctr, bool bfs_ordered = false) {
         // CPK_TIMING: the phases of the top subsets (at least 1/16 of the graph), on stderr
         const size_t n0 = nodes.size();
         SubClock clk;
@@ -252,7 +272,7 @@ struct Nd {
         }
         // split into connected components first (one linear pass over the subset)
         if (bfs_ordered) order = nodes;
-        else bfs(nodes[0], lab, order, st), nbfs++;
+        else bfs(nodes[0], lab, order, st, ctr), nbfs++;
         if (order.size() < nodes.size()) {
             std::vector<std::pair<int32_t, std::vector<int32_t>>> comps;
             const int32_t stamp0 = st;  // this subset's later BFS get newer stamps
@@ -260,29 +280,29 @@ struct Nd {
                 if (lab_of(v) != lab || (stamp[v] != stamp0 && stamp[v] > stamp0)) continue;  // relabelled or seen
                 int32_t c_st;
                 if (stamp[v] == stamp0) {  // the component found by the first BFS
-                    comps.emplace_back(next_label.fetch_add(1), order);
+                    comps.emplace_back(new_label(), order);
                 } else {
                     std::vector<int32_t> c;
-                    bfs(v, lab, c, c_st);
-                    comps.emplace_back(next_label.fetch_add(1), std::move(c));
+                    bfs(v, lab, c, c_st, ctr);
+                    comps.emplace_back(new_label(), std::move(c));
                 }
                 for (int32_t w : comps.back().second) set_lab(w, comps.back().first);
             }
-            run_comps(comps, 0, pos);
+            run_comps(comps, 0, pos, ctr);
             return;
         }
         // pseudo-peripheral node; the best start's BFS stays in buffer `cur`, so it is not redone
         int32_t start = order.back();
         int cur = 0;
         phase("components");
-        int32_t ecc = bfs(start, lab, order, st, cur);
+        int32_t ecc = bfs(start, lab, order, st, ctr, cur);
         nbfs = 1;
         for (int it = 0; it < 4; it++) {
             int32_t cand = order.back();
             std::vector<int32_t> o2;
             o2.reserve(n0);
             int32_t st2;
-            int32_t e2 = bfs(cand, lab, o2, st2, 1 - cur);
+            int32_t e2 = bfs(cand, lab, o2, st2, ctr, 1 - cur);
             nbfs++;
             if (e2 <= ecc) break;
             ecc = e2, start = cand, order.swap(o2), st = st2, cur = 1 - cur;
@@ -306,7 +326,7 @@ struct Nd {
         }
         s = std::max<int32_t>(1, std::min<int32_t>(s, ecc - 1));
         // separator: level-s nodes adjacent to level s+1 (the rest join part A)
-        const int32_t la = next_label.fetch_add(1), lb = next_label.fetch_add(1), ls = next_label.fetch_add(1);
+        const int32_t la = new_label(), lb = new_label(), ls = new_label();
         std::vector<int32_t> a, b, sep;
         a.reserve(order.size()), b.reserve(order.size()), sep.reserve(order.size());
         for (int32_t v : order) {
@@ -333,20 +353,20 @@ struct Nd {
         const size_t na = std::min(a.size(), b.size());
         // part A (levels < s, and level-s nodes without a neighbour at s + 1) is connected through
         // the BFS tree and listed in BFS order from `start`; part B may fall apart
-        both(na, [&] { run(std::move(a), la, pa, true); }, [&] { run(std::move(b), lb, pb); });
+        both(na, [&] { run(std::move(a), la, pa, ctr, true); }, [&] { run(std::move(b), lb, pb, ctr); });
     }
 
     // components [i, end) into consecutive output ranges starting at pos
-    void run_comps(std::vector<std::pair<int32_t, std::vector<int32_t>>> &comps, size_t i, int64_t pos) {
+    void run_comps(std::vector<std::pair<int32_t, std::vector<int32_t>>> &comps, size_t i, int64_t pos, int32_t ctr) {
         for (; i < comps.size(); i++) {
             const size_t sz = comps[i].second.size();
             if (i + 1 < comps.size() && sz > 20000) {
                 auto &c = comps[i];
-                both(sz, [&] { run(std::move(c.second), c.first, pos); },
-                     [&, i] { run_comps(comps, i + 1, pos + (int64_t)sz); });
+                both(sz, [&] { run(std::move(c.second), c.first, pos, ctr); },
+                     [&, i] { run_comps(comps, i + 1, pos + (int64_t)sz, ctr); });
                 return;
             }
-            run(std::move(comps[i].second), comps[i].first, pos);
+            run(std::move(comps[i].second), comps[i].first, pos, ctr);
             pos += (int64_t)sz;
         }
     }
@@ -365,7 +385,7 @@ std::vector<int32_t> nested_dissection(const HCsr &g, int leaf_size) {
     Nd nd(g, leaf_size, host_threads());
     std::vector<int32_t> all(g.nrows);
     std::iota(all.begin(), all.end(), 0);
-    if (g.nrows) nd.run(std::move(all), 0, 0);
+    if (g.nrows) nd.run(std::move(all), 0, 0, 0);
     return std::move(nd.out);
 }
 
