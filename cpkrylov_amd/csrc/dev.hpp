@@ -4,6 +4,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <memory>
 #include <tuple>
@@ -325,8 +326,14 @@ struct DLdl {
     DBuf<int64_t> kp_from;  // Kp entry -> (block << 40 | entry) of A11 / B / C22 (refactorization)
     DBuf<double> Lx, D, Y;  // L in CSC order, D in pivot order, per-row-entry scratch
     DBuf<int> bad;
+    bool sym_ready = false;  // dldl_setup_sym done
     bool ready = false;
 };
+// the two halves of dldl_setup: the symbolic data (uploadable while the host still builds the
+// schedule) and the value sources of the sweep layouts; ready after both
+void dldl_setup_sym(DLdl &d, const LdlSymbolic &sym, const Factor &f);
+void dldl_setup_src(DLdl &d, const std::vector<int32_t> &fsrc, const std::vector<int32_t> &bsrc,
+                    const std::vector<int32_t> &order);
 void dldl_setup(DLdl &d, const LdlSymbolic &sym, const Factor &f, const std::vector<int32_t> &fsrc,
                 const std::vector<int32_t> &bsrc, const std::vector<int32_t> &order);
 // numeric factorization from the device Kp values, then DFactor's sweep values and D;
@@ -362,7 +369,12 @@ struct Analysis {
     LdlSymbolic sym;
     std::vector<int32_t> rsrc;  // F's entry t came from F0's entry rsrc[t]
 };
-Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOpts &o, bool device_numeric = false);
+// on_symbolic (optional) runs on a second host thread as soon as the symbolic factor exists,
+// beside the schedule and the relabelling (which only read it), and is joined before analyze
+// returns: precond_create uploads the device factorization's symbolic data there
+using SymbolicHook = std::function<void(const Factor &, const LdlSymbolic &)>;
+Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOpts &o, bool device_numeric = false,
+                 const SymbolicHook &on_symbolic = {});
 
 // The separator solve of a distributed preconditioner, device copy.
 constexpr int64_t kSepPiggy = 2;  // spare payload slots per rank in the separator exchange
@@ -482,7 +494,7 @@ Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22)
 // with: Kp and the numeric factorization on the device, symbolic analysis reused; returns seconds
 double precond_refactor(Precond &p, const DMat &A11, const DMat &B, const DMat &C22);
 uint64_t pattern_hash(const HCsr &A11, const HCsr &B, const HCsr &C22);
-Precond *precond_create(Ctx &c, Analysis &&an);
+Precond *precond_create(Ctx &c, Analysis &&an, DLdl *pre = nullptr);  // pre: symbolic data already uploaded
 // distributed preconditioner of rank c.rank out of c.nranks
 // Akry (optional): the Krylov operator's A, a placement hint for isolated rows (split_tree)
 Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry = nullptr);

@@ -161,11 +161,9 @@ __global__ void kp_assemble_kernel(int64_t nnz, const int64_t *__restrict__ src,
     }
 }
 
-void dldl_setup(DLdl &d, const LdlSymbolic &sym, const Factor &f, const std::vector<int32_t> &fsrc,
-                const std::vector<int32_t> &bsrc, const std::vector<int32_t> &order) {
+void dldl_setup_sym(DLdl &d, const LdlSymbolic &sym, const Factor &f) {
     d.N = f.N;
     d.nnz = (int64_t)f.Li.size();
-    d.nf = (int64_t)fsrc.size(), d.nb = (int64_t)bsrc.size();
     d.lev_ptr = sym.lev_ptr;
     // within each height: the short rows first, then the long ones (ldl_rows_wave_kernel)
     std::vector<int32_t> rows = sym.lev_rows;
@@ -189,15 +187,28 @@ void dldl_setup(DLdl &d, const LdlSymbolic &sym, const Factor &f, const std::vec
     d.kp_ptr.upload(sym.kp_ptr);
     d.kp_tgt.upload(sym.kp_tgt);
     d.kp_src.upload(sym.kp_src);
-    d.fsrc.upload(fsrc);
-    d.bsrc.upload(bsrc);
-    d.dsrc.upload(order);
     d.Lx.alloc((size_t)std::max<int64_t>(d.nnz, 1));
     d.D.alloc((size_t)std::max<int64_t>(d.N, 1));
     d.Y.alloc((size_t)std::max<int64_t>(d.nnz, 1));
     d.bad.alloc(2);
+    d.sym_ready = true;
+    clk.lap("ldl setup: symbolic uploads");
+}
+
+void dldl_setup_src(DLdl &d, const std::vector<int32_t> &fsrc, const std::vector<int32_t> &bsrc,
+                    const std::vector<int32_t> &order) {
+    if (!d.sym_ready) throw Error(CPK_ERR_ARGS, "internal: value sources before the symbolic data");
+    d.nf = (int64_t)fsrc.size(), d.nb = (int64_t)bsrc.size();
+    d.fsrc.upload(fsrc);
+    d.bsrc.upload(bsrc);
+    d.dsrc.upload(order);
     d.ready = true;
-    clk.lap("ldl setup: uploads");
+}
+
+void dldl_setup(DLdl &d, const LdlSymbolic &sym, const Factor &f, const std::vector<int32_t> &fsrc,
+                const std::vector<int32_t> &bsrc, const std::vector<int32_t> &order) {
+    dldl_setup_sym(d, sym, f);
+    dldl_setup_src(d, fsrc, bsrc, order);
 }
 
 void dldl_assemble_kp(Ctx &c, const DLdl &d, const double *a, const double *b, const double *cc, double *kpv) {

@@ -36,7 +36,8 @@ struct PhaseClock {
     }
 };
 
-Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOpts &o, bool device_numeric) {
+Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOpts &o, bool device_numeric,
+                 const SymbolicHook &on_symbolic) {
     auto t0 = std::chrono::steady_clock::now();
     PhaseClock pc("analyze");
     Analysis an;
@@ -48,18 +49,37 @@ Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOp
     an.device_numeric = device_numeric;
     Factor f0 = ldl_factor(an.Kp, perm, 1, device_numeric ? &an.sym : nullptr, !device_numeric);
     pc.lap(device_numeric ? "factor (symbolic)" : "factor");
-    an.sweep = o.sweep;
-    an.S = build_schedule(f0, an.sweep.rows[0], an.sweep.cap[0], an.sweep.rows[1], an.sweep.cap[1], an.sweep.sub0,
-                          nullptr, o.detach);
-    pc.lap("schedule");
-    an.F = relabel(f0, an.S, device_numeric ? &an.rsrc : nullptr);
+    // the hook reads f0 and an.sym on its own thread while this one only reads them too
+    std::exception_ptr hook_err;
+    std::thread hook;
+    if (on_symbolic)
+        hook = std::thread([&] {
+            try {
+                on_symbolic(f0, an.sym);
+            } catch (...) {
+                hook_err = std::current_exception();
+            }
+        });
+    try {
+        an.sweep = o.sweep;
+        an.S = build_schedule(f0, an.sweep.rows[0], an.sweep.cap[0], an.sweep.rows[1], an.sweep.cap[1], an.sweep.sub0,
+                              nullptr, o.detach);
+        pc.lap("schedule");
+        an.F = relabel(f0, an.S, device_numeric ? &an.rsrc : nullptr);
+        pc.lap("relabel");
+    } catch (...) {
+        if (hook.joinable()) hook.join();
+        throw;
+    }
+    if (hook.joinable()) hook.join();
+    if (hook_err) std::rethrow_exception(hook_err);
     an.F0 = std::move(f0);
-    pc.lap("relabel");
+    if (on_symbolic) pc.lap("symbolic hook (overlapped)");
     an.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return an;
 }
 
-Precond *precond_create(Ctx &c, Analysis &&an) {
+Precond *precond_create(Ctx &c, Analysis &&an, DLdl *pre) {
     auto t0 = std::chrono::steady_clock::now();
     PhaseClock clk("precond_create");
     auto pc = std::make_unique<Precond>();
@@ -123,7 +143,9 @@ Precond *precond_create(Ctx &c, Analysis &&an) {
             parallel_for((int64_t)bsrc.size(), [&](int64_t lo, int64_t hi) {
                 for (int64_t q = lo; q < hi; q++) bsrc[q] = an.rsrc[bsrc[q]];
             });
-            dldl_setup(pc->dl, an.sym, an.F0, fsrc, bsrc, pc->S.order);
+            if (pre && pre->sym_ready) pc->dl = std::move(*pre);  // uploaded during the analysis
+            else dldl_setup_sym(pc->dl, an.sym, an.F0);
+            dldl_setup_src(pc->dl, fsrc, bsrc, pc->S.order);
         } else {
             make_dfactor(an.F, pc->S, pc->dF, &key);
         }
@@ -441,15 +463,23 @@ Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22)
         if (dev) src = kp_value_sources(A11, B, C22);
         hash = pattern_hash(A11, B, C22);
     });
+    // the device factorization's symbolic data is uploaded while the host builds the schedule
+    DLdl pre;
+    SymbolicHook hook;
+    if (dev)
+        hook = [&](const Factor &f, const LdlSymbolic &sym) {
+            CPK_HIP(hipSetDevice(c.device));
+            dldl_setup_sym(pre, sym, f);
+        };
     Analysis an;
     try {
-        an = analyze(A11, B, C22, c.opts, dev);
+        an = analyze(A11, B, C22, c.opts, dev, hook);
     } catch (...) {
         side.join();
         throw;
     }
     side.join();
-    Precond *pc = precond_create(c, std::move(an));
+    Precond *pc = precond_create(c, std::move(an), dev ? &pre : nullptr);
     pc->pattern_hash = hash;
     if (dev) pc->dl.kp_from.upload(src);
     return pc;
