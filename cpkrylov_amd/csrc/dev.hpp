@@ -372,7 +372,7 @@ struct Analysis {
 // on_symbolic (optional) runs on a second host thread as soon as the symbolic factor exists,
 // beside the schedule and the relabelling (which only read it), and is joined before analyze
 // returns: precond_create uploads the device factorization's symbolic data there
-using SymbolicHook = std::function<void(const Factor &, const LdlSymbolic &)>;
+using SymbolicHook = std::function<void(const HCsr &Kp, const Factor &, const LdlSymbolic &)>;
 Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOpts &o, bool device_numeric = false,
                  const SymbolicHook &on_symbolic = {});
 
@@ -494,7 +494,13 @@ Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22)
 // with: Kp and the numeric factorization on the device, symbolic analysis reused; returns seconds
 double precond_refactor(Precond &p, const DMat &A11, const DMat &B, const DMat &C22);
 uint64_t pattern_hash(const HCsr &A11, const HCsr &B, const HCsr &C22);
-Precond *precond_create(Ctx &c, Analysis &&an, DLdl *pre = nullptr);  // pre: symbolic data already uploaded
+// device data uploaded ahead of precond_create (during the analysis, SymbolicHook)
+struct PrecondPre {
+    DLdl dl;   // dldl_setup_sym done when dl.sym_ready
+    DMat dKp;  // Kp uploaded when kp
+    bool kp = false;
+};
+Precond *precond_create(Ctx &c, Analysis &&an, PrecondPre *pre = nullptr);
 // distributed preconditioner of rank c.rank out of c.nranks
 // Akry (optional): the Krylov operator's A, a placement hint for isolated rows (split_tree)
 Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry = nullptr);

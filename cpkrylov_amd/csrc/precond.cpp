@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <exception>
 #include <memory>
@@ -49,13 +50,13 @@ Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOp
     an.device_numeric = device_numeric;
     Factor f0 = ldl_factor(an.Kp, perm, 1, device_numeric ? &an.sym : nullptr, !device_numeric);
     pc.lap(device_numeric ? "factor (symbolic)" : "factor");
-    // the hook reads f0 and an.sym on its own thread while this one only reads them too
+    // the hook reads Kp, f0 and an.sym on its own thread while this one only reads f0 too
     std::exception_ptr hook_err;
     std::thread hook;
     if (on_symbolic)
         hook = std::thread([&] {
             try {
-                on_symbolic(f0, an.sym);
+                on_symbolic(an.Kp, f0, an.sym);
             } catch (...) {
                 hook_err = std::current_exception();
             }
@@ -79,7 +80,7 @@ Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOp
     return an;
 }
 
-Precond *precond_create(Ctx &c, Analysis &&an, DLdl *pre) {
+Precond *precond_create(Ctx &c, Analysis &&an, PrecondPre *pre) {
     auto t0 = std::chrono::steady_clock::now();
     PhaseClock clk("precond_create");
     auto pc = std::make_unique<Precond>();
@@ -103,7 +104,8 @@ Precond *precond_create(Ctx &c, Analysis &&an, DLdl *pre) {
     std::thread kp_thread([&] {
         try {
             CPK_HIP(hipSetDevice(c.device));
-            make_dmat(pc->Kp, pc->dKp);
+            if (pre && pre->kp) pc->dKp = std::move(pre->dKp);  // uploaded during the analysis
+            else make_dmat(pc->Kp, pc->dKp);
             if (pc->Kp.nnz() > (int64_t)INT32_MAX) return;
             // Kp in schedule order: row q = Kp row perm_s[q] with its entries in Kp's order, columns
             // renumbered to schedule positions (perm_s = the relabelled factor's pivot order)
@@ -143,7 +145,7 @@ Precond *precond_create(Ctx &c, Analysis &&an, DLdl *pre) {
             parallel_for((int64_t)bsrc.size(), [&](int64_t lo, int64_t hi) {
                 for (int64_t q = lo; q < hi; q++) bsrc[q] = an.rsrc[bsrc[q]];
             });
-            if (pre && pre->sym_ready) pc->dl = std::move(*pre);  // uploaded during the analysis
+            if (pre && pre->dl.sym_ready) pc->dl = std::move(pre->dl);  // uploaded during the analysis
             else dldl_setup_sym(pc->dl, an.sym, an.F0);
             dldl_setup_src(pc->dl, fsrc, bsrc, pc->S.order);
         } else {
@@ -221,21 +223,30 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     // Those become value maps (vmap_capture), and the device factorization of the whole system
     // fills them (fill_vmaps): the values a host-factored plan would copy, bit for bit.
     const bool devnum = an.device_numeric;
+    SubClock sub;
     if (devnum) {
         an.F0.Lx.resize(an.F0.Li.size());
-        for (size_t p = 0; p < an.F0.Lx.size(); p++) an.F0.Lx[p] = (double)(p + 1);
         an.F0.D.resize((size_t)an.F0.N);
-        for (int64_t v = 0; v < an.F0.N; v++) an.F0.D[v] = (double)(v + 1);
+        parallel_for((int64_t)an.F0.Lx.size(), [&](int64_t lo, int64_t hi) {
+            for (int64_t p = lo; p < hi; p++) an.F0.Lx[p] = (double)(p + 1);
+        }, 1 << 16);
+        parallel_for(an.F0.N, [&](int64_t lo, int64_t hi) {
+            for (int64_t v = lo; v < hi; v++) an.F0.D[v] = (double)(v + 1);
+        }, 1 << 16);
     }
+    sub.lap("dist: index-valued factor");
     auto pc = std::make_unique<Precond>();
     pc->ctx = &c;
     pc->dist = true;
     pc->gn = an.n, pc->gm = an.m, pc->gN = an.N;
     pc->ordering = an.ordering;
     const TreeSplit ts = split_tree(an.F0, c.nranks, c.opts.split_tol, -1, Akry);
+    sub.lap("dist: split");
     check_plan_agreement(c, plan_hash(c, an, ts));
+    sub.lap("dist: plan hash + agreement");
     auto dm = std::make_shared<DofMap>(make_dofmap(an.F0, ts, an.n));
     RankPlan rp = make_rank_plan(an.F0, ts, *dm, c.rank);
+    sub.lap("dist: dof map + rank plan");
     pc->n = dm->n_loc[c.rank], pc->m = dm->m_loc[c.rank], pc->N = pc->n + pc->m;
     pc->nsub = rp.nsub;
     if (rp.nT * (int64_t)sizeof(double) > 64 * 1024)
@@ -270,6 +281,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
         for (size_t i = 0; i < send.size(); i++) tsl[send[i]] = (int32_t)i;
         pc->sep.tslot.upload(tsl);
     }
+    sub.lap("dist: local schedule + layout");
     // separator solve
     DSep &T = pc->sep;
     // payload per rank: the plan's kt values, then kSepPiggy slots that can carry a solver's
@@ -296,13 +308,17 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
         for (int64_t t = 0; t < rp.nT; t++) tof[an.F0.perm[ts.T[t]]] = (int32_t)t;
         // Kp(i, j) != 0 joins an ancestor and a descendant, so outside T a row couples only with
         // its own rank's rows: checked over the whole matrix (the same verdict on every rank)
-        bool ok = !c.opts.no_tkr && rp.kt > 0 && rp.nT > 0;
-        for (int64_t d = 0; d < K.nrows && ok; d++)
-            if (tof[d] < 0)
-                for (int64_t p = K.ptr[d]; p < K.ptr[d + 1] && ok; p++) {
-                    const int32_t g = K.ind[p];
-                    ok = tof[g] >= 0 || dm->owner[g] == dm->owner[d];
-                }
+        std::atomic<bool> coupled{!c.opts.no_tkr && rp.kt > 0 && rp.nT > 0};
+        if (coupled)
+            parallel_for(K.nrows, [&](int64_t lo, int64_t hi) {
+                for (int64_t d = lo; d < hi && coupled.load(std::memory_order_relaxed); d++)
+                    if (tof[d] < 0)
+                        for (int64_t p = K.ptr[d]; p < K.ptr[d + 1]; p++) {
+                            const int32_t g = K.ind[p];
+                            if (tof[g] < 0 && dm->owner[g] != dm->owner[d]) coupled = false;
+                        }
+            }, 1 << 16);
+        const bool ok = coupled;
         std::vector<std::vector<int32_t>> need((size_t)c.nranks);
         for (int64_t t = 0; t < rp.nT && ok; t++) {
             const int32_t d = an.F0.perm[ts.T[t]];
@@ -360,6 +376,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
             pc->tkr = true;
         }
     }
+    sub.lap("dist: refinement without the Kp halo");
     T.nT = rp.nT, T.kt = rp.kt, T.nlev = (int64_t)rp.tlev_ptr.size() - 1, T.ntdof = (int64_t)rp.tdof.size();
     T.tsolve_global = c.opts.tsolve_global, T.tsolve_onepass = c.opts.tsolve_onepass;
     T.kt_data = kt1 > 0 ? kt1 - kSepPiggy : 0;
@@ -373,12 +390,24 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     T.sbuf.alloc((size_t)std::max<int64_t>(T.kt, 1));
     T.sbuf.zero(c.stream);
     T.rbuf.alloc((size_t)std::max<int64_t>(T.kt * c.nranks, 1));
+    sub.lap("dist: separator solve data");
     // refinement residual rows of Kp with their halo
     std::vector<int32_t> kp_send;
     if (devnum) {
-        HCsr kidx = an.Kp;
-        for (size_t q = 0; q < kidx.val.size(); q++) kidx.val[q] = (double)(q + 1);
-        DistCsr dk = dist_csr(kidx, *dm, c.rank, false);
+        // index-valued Kp (entry q -> q + 1) in place of the values for the slice, then back
+        std::vector<double> idx(an.Kp.val.size());
+        parallel_for((int64_t)idx.size(), [&](int64_t lo, int64_t hi) {
+            for (int64_t q = lo; q < hi; q++) idx[q] = (double)(q + 1);
+        }, 1 << 16);
+        std::swap(an.Kp.val, idx);
+        DistCsr dk;
+        try {
+            dk = dist_csr(an.Kp, *dm, c.rank, false);
+        } catch (...) {
+            std::swap(an.Kp.val, idx);
+            throw;
+        }
+        std::swap(an.Kp.val, idx);
         kp_send = dk.send;
         make_dist_dmat(dk, c.nranks, pc->dKp);
     } else {
@@ -392,6 +421,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
         for (size_t i = 0; i < kp_send.size(); i++) hs[kp_send[i]] = (int32_t)i;
         if (!kp_send.empty()) pc->hslot.upload(hs);
     }
+    sub.lap("dist: Kp slice");
     clk.lap("rank plan + upload");
     if (devnum) {
         auto add = [&](DBuf<double> &x, int src) {
@@ -463,13 +493,16 @@ Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22)
         if (dev) src = kp_value_sources(A11, B, C22);
         hash = pattern_hash(A11, B, C22);
     });
-    // the device factorization's symbolic data is uploaded while the host builds the schedule
-    DLdl pre;
+    // Kp and the device factorization's symbolic data are uploaded while the host builds the
+    // schedule
+    PrecondPre pre;
     SymbolicHook hook;
     if (dev)
-        hook = [&](const Factor &f, const LdlSymbolic &sym) {
+        hook = [&](const HCsr &Kp, const Factor &f, const LdlSymbolic &sym) {
             CPK_HIP(hipSetDevice(c.device));
-            dldl_setup_sym(pre, sym, f);
+            dldl_setup_sym(pre.dl, sym, f);
+            make_dmat(Kp, pre.dKp);
+            pre.kp = true;
         };
     Analysis an;
     try {
