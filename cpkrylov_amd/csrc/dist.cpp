@@ -23,9 +23,15 @@ TreeSplit split_tree(const Factor &f, int P, double tol, int64_t tmax, const HCs
     if (tmax < 0) tmax = std::max<int64_t>(256, N / 100);
     if (!(tol > 0 && tol < 1)) throw Error(CPK_ERR_ARGS, "split_tree: load tolerance must lie in (0, 1)");
     // work weight of a row: its forward and backward entries plus the row itself
-    std::vector<double> W(N, 1.0);
-    for (int32_t i : f.Li) W[i] += 1.0;
-    for (int64_t v = 0; v < N; v++) W[v] += (double)(f.Lp[v + 1] - f.Lp[v]);
+    // (row counts of L by a relaxed-atomic histogram; every weight is an exact integer)
+    std::vector<int32_t> nrow(N, 0);
+    parallel_for((int64_t)f.Li.size(), [&](int64_t lo, int64_t hi) {
+        for (int64_t p = lo; p < hi; p++) __atomic_fetch_add(&nrow[f.Li[p]], 1, __ATOMIC_RELAXED);
+    }, 1 << 18);
+    std::vector<double> W(N);
+    parallel_for(N, [&](int64_t lo, int64_t hi) {
+        for (int64_t v = lo; v < hi; v++) W[v] = 1.0 + (double)nrow[v] + (double)(f.Lp[v + 1] - f.Lp[v]);
+    }, 1 << 16);
     for (int64_t v = 0; v < N; v++)  // subtree weights (children precede parents)
         if (f.parent[v] >= 0) W[f.parent[v]] += W[v];
     std::vector<int64_t> cptr(N + 1, 0);
@@ -43,9 +49,10 @@ TreeSplit split_tree(const Factor &f, int P, double tol, int64_t tmax, const HCs
     std::vector<char> is_cand(N, 0), inT(N, 0), iso(N, 0);
     // isolated rows (no factor entries at all: e.g. G pivots no constraint touches) are solved
     // by a division; they are placed by dof locality at the end instead of by the tree
-    for (int32_t i : f.Li) iso[i] = 2;
-    for (int64_t v = 0; v < N; v++)
-        iso[v] = f.parent[v] < 0 && iso[v] == 0 && f.Lp[v + 1] == f.Lp[v] && cptr[v + 1] == cptr[v];
+    parallel_for(N, [&](int64_t lo, int64_t hi) {
+        for (int64_t v = lo; v < hi; v++)
+            iso[v] = f.parent[v] < 0 && nrow[v] == 0 && f.Lp[v + 1] == f.Lp[v] && cptr[v + 1] == cptr[v];
+    }, 1 << 16);
     for (int64_t v = 0; v < N; v++)
         if (f.parent[v] < 0 && !iso[v]) heap.push({W[v], (int32_t)v}), is_cand[v] = 1, total += W[v];
     // cut below the heaviest subtree until every candidate is light: a contiguous split of the
@@ -98,10 +105,12 @@ TreeSplit split_tree(const Factor &f, int P, double tol, int64_t tmax, const HCs
             rank_of[v] = rank_of[p];
         }
     }
+    std::vector<int32_t> node_of(N);  // dof -> tree node
+    parallel_for(N, [&](int64_t lo, int64_t hi) {
+        for (int64_t v = lo; v < hi; v++) node_of[f.perm[v]] = (int32_t)v;
+    }, 1 << 16);
     // isolated rows take the rank of the nearest preceding (else following) dof
     {
-        std::vector<int32_t> node_of(N);
-        for (int64_t v = 0; v < N; v++) node_of[f.perm[v]] = (int32_t)v;
         int32_t last = -1;
         for (int64_t g = 0; g < N; g++) {
             const int32_t v = node_of[g];
@@ -121,8 +130,6 @@ TreeSplit split_tree(const Factor &f, int P, double tol, int64_t tmax, const HCs
     // couples (in A) with the bounded variable at the same relative position of its block, so
     // equal parts in dof order land next to each rank's share of those variables.
     {
-        std::vector<int32_t> node_of(N);
-        for (int64_t v = 0; v < N; v++) node_of[f.perm[v]] = (int32_t)v;
         const int64_t min_run = 64 * (int64_t)ts.P;
         for (int64_t g = 0; g < N;) {
             if (!iso[node_of[g]]) {
@@ -140,8 +147,6 @@ TreeSplit split_tree(const Factor &f, int P, double tol, int64_t tmax, const HCs
     // couples it with that the tree placed (the slack rows of S50 couple with one bounded
     // variable each): the halo of A then holds only the coupling across rank boundaries
     if (Akry) {
-        std::vector<int32_t> node_of(N);
-        for (int64_t v = 0; v < N; v++) node_of[f.perm[v]] = (int32_t)v;
         for (int64_t v = 0; v < N; v++) {
             if (!iso[v] || inT[v]) continue;
             const int64_t g = f.perm[v];
