@@ -295,8 +295,13 @@ def host_cpu():
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     omp = os.environ.get("OMP_NUM_THREADS")
     threads = max(1, min(aff or 1, int(omp) if omp and omp.isdigit() else (aff or 1)))
+    limit = ("OMP_NUM_THREADS" if omp and omp.isdigit() and int(omp) < (aff or 1)
+             else "affinity mask" if (aff or 0) < (os.cpu_count() or 0) else "none")
     return {"model": model, "nproc_all": os.cpu_count(), "affinity": aff, "omp_num_threads": omp,
-            "threads": threads}
+            "threads": threads,
+            "thread_limit": limit + (": the GPU box grants this process that many CPU threads (its CPU "
+                                     "share of the shared host), so the OpenMP leg uses all of them"
+                                     if limit != "none" else "")}
 
 
 def cpu_baseline(S, b1, M_gpu, args, hist_gpu, niters_gpu):
