@@ -373,8 +373,10 @@ struct Analysis {
 // beside the schedule and the relabelling (which only read it), and is joined before analyze
 // returns: precond_create uploads the device factorization's symbolic data there
 using SymbolicHook = std::function<void(const HCsr &Kp, const Factor &, const LdlSymbolic &)>;
+// global_schedule = false: no schedule / relabelled factor of the whole system (a distributed
+// preconditioner schedules each rank's subtrees itself; an.S and an.F stay empty)
 Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOpts &o, bool device_numeric = false,
-                 const SymbolicHook &on_symbolic = {});
+                 const SymbolicHook &on_symbolic = {}, bool global_schedule = true);
 
 // The separator solve of a distributed preconditioner, device copy.
 constexpr int64_t kSepPiggy = 2;  // spare payload slots per rank in the separator exchange

@@ -38,7 +38,7 @@ struct PhaseClock {
 };
 
 Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOpts &o, bool device_numeric,
-                 const SymbolicHook &on_symbolic) {
+                 const SymbolicHook &on_symbolic, bool global_schedule) {
     auto t0 = std::chrono::steady_clock::now();
     PhaseClock pc("analyze");
     Analysis an;
@@ -63,11 +63,13 @@ Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOp
         });
     try {
         an.sweep = o.sweep;
-        an.S = build_schedule(f0, an.sweep.rows[0], an.sweep.cap[0], an.sweep.rows[1], an.sweep.cap[1], an.sweep.sub0,
-                              nullptr, o.detach);
-        pc.lap("schedule");
-        an.F = relabel(f0, an.S, device_numeric ? &an.rsrc : nullptr);
-        pc.lap("relabel");
+        if (global_schedule) {
+            an.S = build_schedule(f0, an.sweep.rows[0], an.sweep.cap[0], an.sweep.rows[1], an.sweep.cap[1],
+                                  an.sweep.sub0, nullptr, o.detach);
+            pc.lap("schedule");
+            an.F = relabel(f0, an.S, device_numeric ? &an.rsrc : nullptr);
+            pc.lap("relabel");
+        }
     } catch (...) {
         if (hook.joinable()) hook.join();
         throw;
@@ -459,7 +461,8 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
 
 Precond *precond_create_dist(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22, const HCsr *Akry) {
     const bool dev = !c.opts.host_factor;
-    Precond *pc = precond_create_dist(c, analyze(A11, B, C22, c.opts, dev), Akry);
+    // each rank schedules its own subtrees: no schedule of the whole system
+    Precond *pc = precond_create_dist(c, analyze(A11, B, C22, c.opts, dev, {}, false), Akry);
     pc->pattern_hash = pattern_hash(A11, B, C22);
     if (dev) pc->dl.kp_from.upload(kp_value_sources(A11, B, C22));
     return pc;
