@@ -106,6 +106,7 @@ struct EngineOpts {
     bool dist_graph = true;       // dist_graph:         capture collectives in the graphs
     int batch = 0;                // batch:              fixed iterations per graph (0: adaptive)
     bool profile_fwd_nolevels = false;  // profile_fwd_nolevels: diagnostic (cpk_profile_kernels)
+    bool profile_fwd_sched = false;     // profile_fwd_sched: diagnostic, the profiled forward reads its input in schedule order
 };
 EngineOpts engine_opts_from_env();
 // name as in the comments above; throws CPK_ERR_ARGS on an unknown name or a bad value

@@ -71,6 +71,7 @@ const BoolOpt kBool[] = {
     {"no_minres_fuse", &EngineOpts::no_minres_fuse},
     {"dist_graph", &EngineOpts::dist_graph},
     {"profile_fwd_nolevels", &EngineOpts::profile_fwd_nolevels},
+    {"profile_fwd_sched", &EngineOpts::profile_fwd_sched},
 };
 
 }  // namespace

@@ -2096,14 +2096,17 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
     // one LDL solve as the apply runs it: the forward sweep (its last round deferred when fused),
     // then the pair forward + backward; the backward's time is the pair's minus the forward's.
     // Launch order (bench.py's PMC parser): (1 + reps) forward sweeps, (1 + reps) pairs
+    // profile_fwd_sched (diagnostic): the forward reads x as if it were the signed input in schedule
+    // order (no perm gather; the values are meaningless, the time and traffic are not)
     FwdIn last;
+    const bool fsched = c.opts.profile_fwd_sched;
     if (c.opts.profile_fwd_nolevels)
         out->fwd_ms = timeit([&]() { launch_sptrsv_fwd_diag(c, M.dF, x.p, M.n, M.w.p); });
     else
-        out->fwd_ms = timeit([&]() { launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr, false, nullptr, &last); });
+        out->fwd_ms = timeit([&]() { launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr, fsched, nullptr, &last); });
     out->fwd_bytes = 12.0 * l - 2.0 * (double)M.dF.nnz16 + 4.0 * (Nn + 1) + 4.0 * Nn /*perm*/ + 8.0 * Nn /*x*/ + 8.0 * Nn /*w*/;
     const double pair_ms = timeit([&]() {
-        launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr, false, nullptr, &last);
+        launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr, fsched, nullptr, &last);
         launch_sptrsv_bwd(c, M.dF, M.w.p, z.p, false, nullptr, nullptr, nullptr, &last);
     });
     out->bwd_ms = pair_ms - out->fwd_ms;

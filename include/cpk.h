@@ -123,7 +123,7 @@ int cpk_ctx_create_sim(int device, cpk_simgroup group, int rank, int nranks, cpk
  * no_pipe, no_upper, no_col16, no_sched_resid, no_fused_resid, fused_tail_launch, r0_stride,
  * r0_xcd_chunk, tsolve_global, tsolve_onepass, no_piggy, no_halo_merge, no_graph, no_fuse_last, no_tkr,
  * no_minres_fuse,
- * dist_graph, batch, profile_fwd_nolevels.  Booleans as "0"/"1".  A distributed preconditioner allgathers a hash
+ * dist_graph, batch, profile_fwd_nolevels, profile_fwd_sched.  Booleans as "0"/"1".  A distributed preconditioner allgathers a hash
  * of its plan and of every option at creation and fails (CPK_ERR_ARGS) on every rank unless
  * all ranks agree. */
 int cpk_ctx_set_option(cpk_ctx ctx, const char *name, const char *value);
