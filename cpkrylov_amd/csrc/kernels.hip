@@ -1651,7 +1651,8 @@ __global__ __launch_bounds__(TPB) void sptrsv_last_kernel(
 // the last round fused (fwd + bwd) when it is an upper round whose blocks fit sptrsv_last_kernel
 bool fuse_last_ok(const DFactor &F) {
     const int64_t R = (int64_t)F.round_ptr.size() - 1;
-    return F.fuse_last && R >= 2 && F.sweep_threads[1] == 512 && F.sweep_rows[1] <= 1024 && F.sweep_cap[1] <= 4096 &&
+    return F.fuse_last && R >= 2 && (F.sweep_threads[1] == 512 || F.sweep_threads[1] == 256) &&
+           F.sweep_rows[1] <= 1024 && F.sweep_cap[1] <= 4096 &&
            (int64_t)F.round_fits.size() >= R && F.round_fits[R - 1] && !F.no_upper;
 }
 
@@ -1721,7 +1722,10 @@ static bool upper_round(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool add,
                         int64_t neg_from, double *w, double *out, const int *run, const int *active, int sched_in,
                         double *ys, double *xs, const PackArgs &pk) {
     if (F.no_upper) return false;
-    return upper_round_t<512, 2, 8>(c, F, r, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs, pk);
+    // 256 threads (blocks of <= 512 rows / 3072 entries, a 38 KB image): four blocks per CU, for a
+    // schedule whose first upper round has more blocks than 512-thread images keep resident
+    return upper_round_t<512, 2, 8>(c, F, r, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs, pk) ||
+           upper_round_t<256, 2, 12>(c, F, r, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs, pk);
 }
 
 // SPLIT > 1: the workgroup is one wave holding SPLIT independent logical blocks of TPB lanes
