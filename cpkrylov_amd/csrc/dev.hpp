@@ -71,9 +71,13 @@ struct Comm {
 
 // Sweep configuration: rows and entries staged per block, threads per block, round 0 / upper
 // rounds (engine option "sweep": "rows,cap,threads" for both, or "R0,CAP0,T0,R1,CAP1,T1[,SUB0]").
+// Default (r03 v40, profiles/r03_sub0_ab_v39.txt / r03_upper256_ab_v40.txt): round 0 peels subtrees
+// of weight <= 480 (fewer levels per round-0 block: 9.75 -> 8.57 at S10) and the upper rounds use
+// 256-thread blocks of <= 512 rows / 3072 entries, four per CU, so the doubled first upper round
+// (1024 blocks at S10) stays co-resident: S10 875-879 -> 887-898 it/s.
 struct SweepConfig {
-    int rows[2] = {192, 1024}, cap[2] = {576, 4096}, threads[2] = {64, 512};
-    int sub0 = 0;  // round-0 subtree cap (0: cap[0])
+    int rows[2] = {192, 512}, cap[2] = {576, 3072}, threads[2] = {64, 256};
+    int sub0 = 480;  // round-0 subtree cap (0: cap[0])
 };
 
 // Engine options of a context (opts.cpp; cpk_ctx_set_option).  None changes a result: they

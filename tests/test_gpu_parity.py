@@ -176,9 +176,12 @@ def test_divide_and_transpose(gpu_ctx):
     assert np.linalg.norm(Kp @ y - z) <= 1e-8 * np.linalg.norm(z)
 
 
-# One configuration per distinct code path of the sweeps (engine option "sweep"):
-#   192,576,64                     the default: persistent round-0 kernel <64,3,9> (its fused-residual
-#                                  and int16-column forms) and the single-wave upper-round kernel
+# One configuration per distinct code path of the sweeps (engine option "sweep"; the default,
+# 192,576,64,512,3072,256,480, runs in every other test: persistent round-0 kernel <64,3,9> with its
+# fused-residual and int16-column forms, the 256-thread upper-round kernel and the fused last round):
+#   192,576,64,1024,4096,512       the 512-thread upper-round kernel <512,2,8> (the default until r03
+#                                  v40), round 0 without a subtree cap
+#   192,576,64                     round 0 as the default, upper rounds through the generic kernels
 #   64,128,64                      one-workgroup-per-block kernels at 64 threads, and the direct
 #                                  (unstaged) path of rows with more entries than a block holds
 #   1024,3072,256                  the same kernels at 256 threads with the largest LDS image
@@ -190,7 +193,7 @@ def test_divide_and_transpose(gpu_ctx):
 # Dropped in round 3 (same templates as a kept case, other register counts; the suite's time):
 # 512,1536,128 and 128,512,128 (generic / persistent at 128 threads), 256,768,64 <64,4,12> and
 # 384,1152,64,...,400 <64,6,18> (both still run in the fused-residual test), 128,384,32,... <32,4,12,2>.
-SWEEP_PATHS = ["192,576,64", "64,128,64", "1024,3072,256", "256,768,128,2048,8192,512",
+SWEEP_PATHS = ["192,576,64,1024,4096,512", "192,576,64", "64,128,64", "1024,3072,256", "256,768,128,2048,8192,512",
                "512,1536,64,1024,4096,256,300", "192,576,32,1024,4096,512"]
 
 
