@@ -121,8 +121,11 @@ def main():
             uid = [cpk.get_unique_id() if rank == 0 else None]
             if dist:
                 dist.broadcast_object_list(uid, src=0)
+            # per-rank subtrees keep the previous sweep configuration: the single-GPU default's
+            # lower round-0 subtrees give each rank a third round
+            opts = None if os.environ.get("CPK_SWEEP") else {"sweep": "192,576,64,1024,4096,512"}
             with _quiet_stdout():
-                ctx = cpk.Context(device=local, rank=rank, nranks=world, unique_id=uid[0])
+                ctx = cpk.Context(device=local, rank=rank, nranks=world, unique_id=uid[0], options=opts)
             A, B, Cm, G = (cpk.Matrix(S[k], ctx) for k in ("Q", "B", "C", "G"))
             M = cpk.opLDL2(G, B, -S["C"], ctx=ctx, krylov_A=A)  # A: placement hint (cpk_pc_create_hint)
         except Exception as e:  # noqa: BLE001  (reported, then every rank exits)
