@@ -8,15 +8,20 @@ Metric (BASELINE.json): "Krylov iters/sec + SpMV GB/s (% HBM peak), cpminres 10M
             solution are HBM-resident, the factorization (ptime) and the shift are outside the
             timed region.
   value     Krylov iterations completed by all ranks / max over ranks of the timed wall time.
-  roofline  the dominant kernel, the triangular sweeps of one LDL' solve (4 sweeps per M*z):
-            algorithmic bytes / HIP-event-timed duration, vs 8 TB/s; spmv_roofline the same for
-            the saddle-point SpMV r = x - Kp*y (the refinement residual inside every M*z).
+  roofline  the dominant kernel, the triangular sweeps of one LDL' solve (a forward and a
+            backward sweep, every round; an M*z runs two solves): algorithmic bytes / HIP-event-
+            timed duration, vs 8 TB/s; spmv_roofline the same for the saddle-point SpMV
+            r = x - Kp*y (the refinement residual inside every M*z).
   cpu_baseline  the C restatement (oracle/) of the same solve on the host, timed on a
             bounded sample of the same workload: one core, and OpenMP on the cores the box grants.
-Multi-GPU (torchrun, one process per GPU): ONE solve of the same S10 system row-block
-partitioned over the ranks (strong scaling): RCCL allreduce for the inner
-products, allgathered halos for the SpMVs and the separator exchange of the distributed LDL'
-sweeps.  value = that solve's iterations / max-over-ranks wall time.
+Multi-GPU (one process per GPU): ONE solve of the same S10 system row-block partitioned over
+the ranks (strong scaling): RCCL allreduce for the inner products,
+allgathered halos for the SpMVs and the separator exchange of the distributed LDL' sweeps.
+value = that solve's iterations / max-over-ranks wall time.  `bench.py --gpus N` (N > 1) outside
+torchrun starts `python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child
+process before anything touches a GPU and exits with its return code; under torchrun,
+WORLD_SIZE must equal --gpus, and the line's config.rccl_ranks is the communicator's own rank
+count (ncclCommCount), so a run cannot silently measure fewer GPUs than it claims.
 """
 import argparse
 import ctypes as C
@@ -35,9 +40,12 @@ EXPROG_OPTS = dict(print=False, atol=1.0e-6, rtol=1.0e-6, itmax=500,
                    residual_update=True, nitref=1, force_itref=True, itref_tol=1.0e-8)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of the job; default WORLD_SIZE under torchrun, else 1")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print the launch plan (the torchrun command for --gpus N > 1) as JSON and exit")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", choices=("s10", "s50"), default="s10",
@@ -55,7 +63,7 @@ def parse():
     ap.add_argument("--rhs-perturb", type=float, default=0.0,
                     help="scale the rhs by (1 + eps*u), u uniform in [-1, 1] (sensitivity runs; never the bench line)")
     ap.add_argument("--perturb-seed", type=int, default=1)
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     s50 = a.config == "s50"
     if a.size is None:
         a.size = 50_000_000 if s50 else 10_000_000
@@ -84,10 +92,50 @@ class _quiet_stdout:
         os.close(self.saved)
 
 
-def main():
-    args = parse()
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(args, argv):
+    """What this invocation does before any GPU work: ("run", None) in-process, ("launch", cmd)
+    to start torchrun with one rank per GPU, or ("error", message) for a world-size mismatch."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        world = int(env_world)
+        if args.gpus is not None and args.gpus != world:
+            return "error", f"--gpus {args.gpus} but WORLD_SIZE={world}: the job would measure {world} GPU(s)"
+        return "run", None
+    gpus = 1 if args.gpus is None else args.gpus
+    if gpus < 1:
+        return "error", f"--gpus {gpus}"
+    if gpus == 1:
+        return "run", None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)]
+    return "launch", cmd + [a for a in argv if a != "--dry-run"]
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
     if args.pmc_probe:
         return pmc_probe(args)
+    kind, what = launch_plan(args, argv)
+    if args.dry_run:
+        print(json.dumps({"plan": kind, "cmd" if kind == "launch" else "detail": what}), flush=True)
+        return 2 if kind == "error" else 0
+    if kind == "error":
+        print(f"bench: {what}", file=sys.stderr, flush=True)
+        return 2
+    if kind == "launch":
+        # a child process, not an exec: nothing in this process has touched a GPU; rank 0's JSON
+        # line reaches our stdout through the inherited descriptor
+        import subprocess
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        return subprocess.run(what, env=env).returncode
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -121,11 +169,11 @@ def main():
             uid = [cpk.get_unique_id() if rank == 0 else None]
             if dist:
                 dist.broadcast_object_list(uid, src=0)
-            # per-rank subtrees keep the previous sweep configuration: the single-GPU default's
-            # lower round-0 subtrees give each rank a third round
-            opts = None if os.environ.get("CPK_SWEEP") else {"sweep": "192,576,64,1024,4096,512"}
             with _quiet_stdout():
-                ctx = cpk.Context(device=local, rank=rank, nranks=world, unique_id=uid[0], options=opts)
+                ctx = cpk.Context(device=local, rank=rank, nranks=world, unique_id=uid[0])
+            cinfo = ctx.info()
+            if cinfo["comm"] != "rccl" or cinfo["comm_ranks"] != world:
+                raise RuntimeError(f"the RCCL communicator holds {cinfo['comm_ranks']} rank(s), expected {world}")
             A, B, Cm, G = (cpk.Matrix(S[k], ctx) for k in ("Q", "B", "C", "G"))
             M = cpk.opLDL2(G, B, -S["C"], ctx=ctx, krylov_A=A)  # A: placement hint (cpk_pc_create_hint)
         except Exception as e:  # noqa: BLE001  (reported, then every rank exits)
@@ -141,6 +189,7 @@ def main():
             sys.exit(3)
     else:
         ctx = cpk.Context(device=local)
+        cinfo = ctx.info()
         A, B, Cm, G = (cpk.Matrix(S[k], ctx) for k in ("Q", "B", "C", "G"))
         M = cpk.opLDL2(G, B, -S["C"], ctx=ctx)
     M.nitref, M.itref_tol = EXPROG_OPTS["nitref"], EXPROG_OPTS["itref_tol"]
@@ -261,6 +310,8 @@ def main():
                        "N": N, "n": n, "m": m, "nnz_kp": M.info["nnz_kp"], "nnz_l": M.info["nnz_l"],
                        "sweep_launches": M.info["nrounds"], "elim_tree_depth": M.info["depth"],
                        "parallelism": f"rowblock{world}" if distributed else "single",
+                       "rccl_ranks": cinfo["comm_ranks"] if cinfo["comm"] == "rccl" else 0,
+                       "sweep": ctx.get_option("sweep"),
                        "seed": S["seed"],
                        "rows_local_rank0": N_loc,
                        **({"rhs_perturb": args.rhs_perturb, "perturb_seed": args.perturb_seed}
@@ -473,4 +524,4 @@ def pmc_traffic(args):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

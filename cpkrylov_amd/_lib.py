@@ -17,6 +17,7 @@ lib = C.CDLL(LIB_PATH)
 
 CPK_OK, CPK_ERR_INDEFINITE, CPK_ERR_DIM, CPK_ERR_ARGS, CPK_ERR_HIP, CPK_ERR_RCCL, CPK_ERR_FACTOR, \
     CPK_ERR_NOMEM, CPK_ERR_UNSUPPORTED = range(9)
+COMM_KINDS = {0: "none", 1: "rccl", 2: "sim", 3: "null"}  # CPK_COMM_* (cpk_ctx_get_info)
 METHODS = {"cg": 0, "cglanczos": 1, "minres": 2, "symmlq": 3, "gmres": 4, "dqgmres": 5}
 _OPT_FIELDS = ("atol", "rtol", "btol", "itmax", "restart", "mem", "print",
                "nitref", "itref_tol", "force_itref", "residual_update")
@@ -53,6 +54,9 @@ _SIGS = {
     "cpk_abi_version": ([], C.c_int),
     "cpk_get_unique_id": ([P(C.c_ubyte)], C.c_int),
     "cpk_ctx_create": ([C.c_int, C.c_int, C.c_int, P(C.c_ubyte), P(vp)], C.c_int),
+    "cpk_ctx_create_null": ([C.c_int, C.c_int, C.c_int, P(vp)], C.c_int),
+    "cpk_ctx_get_info": ([vp, P(C.c_int64)], C.c_int),
+    "cpk_ctx_get_options": ([vp, C.c_char_p, C.c_size_t], C.c_int),
     "cpk_ctx_destroy": ([vp], C.c_int),
     "cpk_ctx_synchronize": ([vp], C.c_int),
     "cpk_mat_create_csc": ([vp, C.c_int64, C.c_int64, P(C.c_size_t), P(C.c_size_t), P(C.c_double), P(vp)], C.c_int),
@@ -71,7 +75,7 @@ _SIGS = {
     "cpk_pc_divide": ([vp, P(C.c_double), P(C.c_double)], C.c_int),
     "cpk_pc_get_info": ([vp, P(PcInfo)], C.c_int),
     "cpk_pc_export": ([vp, P(C.c_int64), P(C.c_int32), P(C.c_double), P(C.c_double), P(C.c_int32)], C.c_int),
-    "cpk_analyze": ([vp, vp, vp, P(vp)], C.c_int),
+    "cpk_analyze": ([vp, vp, vp, C.c_char_p, P(vp)], C.c_int),
     "cpk_analysis_destroy": ([vp], C.c_int),
     "cpk_analysis_get_info": ([vp, P(PcInfo)], C.c_int),
     "cpk_analysis_export": ([vp, P(C.c_int64), P(C.c_int32), P(C.c_double), P(C.c_double), P(C.c_int32)],

@@ -32,14 +32,21 @@ def _dptr(a):
 
 
 class Context:
-    """One GPU, one HIP stream (and an RCCL communicator when nranks > 1)."""
+    """One GPU, one HIP stream (and an RCCL communicator when nranks > 1).
 
-    def __init__(self, device=None, rank=0, nranks=1, unique_id=None, simgroup=None, options=None):
+    timing_standin=True (diagnostic, cpk_ctx_create_null): rank `rank` of an nranks-way context
+    whose collectives are no-ops -- one rank's share of the work, timed on one GPU; its results
+    are meaningless."""
+
+    def __init__(self, device=None, rank=0, nranks=1, unique_id=None, simgroup=None, options=None,
+                 timing_standin=False):
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         h = C.c_void_p()
         if simgroup is not None:  # ranks as threads on one GPU (tests), see cpk_ctx_create_sim
             check(lib.cpk_ctx_create_sim(device, simgroup.h, rank, nranks, C.byref(h)))
+        elif timing_standin:
+            check(lib.cpk_ctx_create_null(device, rank, nranks, C.byref(h)))
         else:
             uid = None
             if unique_id is not None:
@@ -58,9 +65,25 @@ class Context:
         check(lib.cpk_ctx_set_option(self.h, name.encode(), str(value).encode()))
 
     def get_option(self, name):
+        """The value this context's objects use (sweep: the per-path default unless set)."""
         buf = C.create_string_buffer(256)
         check(lib.cpk_ctx_get_option(self.h, name.encode(), buf, 256))
         return buf.value.decode()
+
+    def options_string(self):
+        """Every engine option as "name=value;..." (cpk_ctx_get_options): analyze(options=...)
+        and dist_plan(options=...) then plan exactly as this context's preconditioners."""
+        buf = C.create_string_buffer(4096)
+        check(lib.cpk_ctx_get_options(self.h, buf, 4096))
+        return buf.value.decode()
+
+    def info(self):
+        """device, rank, nranks, the communicator's kind and rank count (RCCL: ncclCommCount),
+        and whether preconditioners built here take the distributed path (cpk_ctx_get_info)."""
+        v = (C.c_int64 * 8)()
+        check(lib.cpk_ctx_get_info(self.h, v))
+        return {"device": v[0], "rank": v[1], "nranks": v[2], "comm": _lib.COMM_KINDS.get(v[3], str(v[3])),
+                "comm_ranks": v[4], "distributed": bool(v[5])}
 
     def synchronize(self):
         check(lib.cpk_ctx_synchronize(self.h))
@@ -328,11 +351,25 @@ class opLDL2:
             self.h = None
 
 
-def analyze(A, B, Cm):
-    """Host-only half of opLDL2(A, B, C) (no GPU): ordering, LDL', sweep schedule."""
+def _options_spec(ctx, options):
+    """The engine-option spec of cpk_analyze: a context's full set (so the analysis plans as that
+    context's preconditioner would), then `options` (dict or "name=value;..." string) on top."""
+    parts = []
+    if ctx is not None:
+        parts.append(ctx.options_string())
+    if isinstance(options, dict):
+        parts.append("".join(f"{k}={('1' if v else '0') if isinstance(v, bool) else v};" for k, v in options.items()))
+    elif options:
+        parts.append(str(options))
+    return ";".join(p.strip(";") for p in parts if p).encode() if parts else None
+
+
+def analyze(A, B, Cm, ctx=None, options=None):
+    """Host-only half of opLDL2(A, B, C) (no GPU): ordering, LDL', sweep schedule.  Engine
+    options: the CPK_* environment, then those of `ctx` (if given), then `options`."""
     mats = [M if isinstance(M, Matrix) else Matrix(M, host_only=True) for M in (A, B, Cm)]
     h = C.c_void_p()
-    check(lib.cpk_analyze(mats[0].h, mats[1].h, mats[2].h, C.byref(h)))
+    check(lib.cpk_analyze(mats[0].h, mats[1].h, mats[2].h, _options_spec(ctx, options), C.byref(h)))
     try:
         info = _lib.PcInfo()
         check(lib.cpk_analysis_get_info(h, C.byref(info)))
@@ -366,12 +403,14 @@ _PLAN_NAMES = ("sizes", "dofs", "node_rank", "T", "fsub_Lp", "fsub_Li", "fsub_Lx
     tuple(f"{k}_{a}" for k in ("kp", "ac", "ab") for a in ("ptr", "col", "val", "send"))
 
 
-def dist_plan(G, B, Cneg, A, Cop, nranks, rank):
+def dist_plan(G, B, Cneg, A, Cop, nranks, rank, ctx=None, options=None):
     """Host-only row-block plan of `rank` for opLDL2(G, B, Cneg) and the
-    Krylov operator blocks A, Cop: a dict of numpy arrays (see cpk_plan_array in cpk.h)."""
+    Krylov operator blocks A, Cop: a dict of numpy arrays (see cpk_plan_array in cpk.h).  Engine
+    options (split_tol) as in analyze(): pass the distributed context to get exactly the plan its
+    preconditioner builds."""
     mats = [Matrix(M, host_only=True) for M in (G, B, Cneg, A, Cop)]
     h = C.c_void_p()
-    check(lib.cpk_analyze(mats[0].h, mats[1].h, mats[2].h, C.byref(h)))
+    check(lib.cpk_analyze(mats[0].h, mats[1].h, mats[2].h, _options_spec(ctx, options), C.byref(h)))
     p = C.c_void_p()
     try:
         check(lib.cpk_analysis_plan(h, mats[3].h, mats[4].h, int(nranks), int(rank), C.byref(p)))

@@ -95,6 +95,7 @@ struct cpk_mat_s {
 
 struct cpk_analysis_s {
     Analysis an;
+    EngineOpts opts;  // the options it was built with (cpk_analysis_plan's split_tol)
 };
 
 struct cpk_plan_s {
@@ -195,17 +196,43 @@ static std::unique_ptr<cpk_ctx_s> ctx_base(int device, int rank, int nranks) {
 int cpk_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id, cpk_ctx *out) {
     API_BEGIN
     need(out != nullptr, "out is NULL");
+    need(nranks == 1 || unique_id != nullptr, "unique_id required when nranks > 1");
     auto ctx = ctx_base(device, rank, nranks);
-    const char *cm = getenv("CPK_COMM");
-    if (nranks > 1 && cm && std::string(cm) == "null") {  // diagnostic timing stand-in (comm.cpp)
-        ctx->comm.reset(make_null_comm(rank));
-        ctx->c.comm = ctx->comm.get();
-    } else if (nranks > 1 || unique_id) {  // a 1-rank communicator runs the distributed path (tests)
-        need(unique_id != nullptr, "unique_id required when nranks > 1");
+    if (unique_id) {  // a 1-rank communicator runs the distributed path too
         ctx->comm.reset(make_rccl_comm(nranks, rank, unique_id));
         ctx->c.comm = ctx->comm.get();
     }
     *out = ctx.release();
+    API_END
+}
+
+int cpk_ctx_create_null(int device, int rank, int nranks, cpk_ctx *out) {
+    API_BEGIN
+    need(out != nullptr, "out is NULL");
+    need(nranks > 1, "the timing stand-in needs nranks > 1");
+    auto ctx = ctx_base(device, rank, nranks);
+    ctx->comm.reset(make_null_comm(rank, nranks));  // diagnostic (comm.cpp): collectives are no-ops
+    ctx->c.comm = ctx->comm.get();
+    *out = ctx.release();
+    API_END
+}
+
+int cpk_ctx_get_info(cpk_ctx ctx, int64_t *info) {
+    API_BEGIN
+    need(ctx && info, "NULL argument");
+    const Ctx &c = ctx->c;
+    const int64_t v[8] = {c.device, c.rank, c.nranks, c.comm ? c.comm->kind() : CPK_COMM_NONE,
+                          c.comm ? c.comm->count() : 0, c.dist() ? 1 : 0, 0, 0};
+    std::memcpy(info, v, sizeof v);
+    API_END
+}
+
+int cpk_ctx_get_options(cpk_ctx ctx, char *buf, size_t cap) {
+    API_BEGIN
+    need(ctx && buf && cap > 0, "NULL argument");
+    const std::string v = engine_opts_string(ctx->c.opts, ctx->c.dist());
+    need(v.size() < cap, "buffer too small");
+    std::memcpy(buf, v.c_str(), v.size() + 1);
     API_END
 }
 
@@ -261,7 +288,7 @@ int cpk_ctx_set_option(cpk_ctx ctx, const char *name, const char *value) {
 int cpk_ctx_get_option(cpk_ctx ctx, const char *name, char *buf, size_t cap) {
     API_BEGIN
     need(ctx && name && buf && cap > 0, "NULL argument");
-    const std::string v = get_engine_option(ctx->c.opts, name);
+    const std::string v = get_engine_option(ctx->c.opts, name, ctx->c.dist());
     need(v.size() < cap, "buffer too small");
     std::memcpy(buf, v.c_str(), v.size() + 1);
     API_END
@@ -656,11 +683,13 @@ int cpk_reg_solve(cpk_ctx ctx, int method, const double *b, cpk_mat A, cpk_mat B
     API_END
 }
 
-int cpk_analyze(cpk_mat A11, cpk_mat B, cpk_mat C22, cpk_analysis *out) {
+int cpk_analyze(cpk_mat A11, cpk_mat B, cpk_mat C22, const char *options, cpk_analysis *out) {
     API_BEGIN
     need(A11 && B && C22 && out, "NULL argument");
     auto a = std::make_unique<cpk_analysis_s>();
-    a->an = analyze(A11->h, B->h, C22->h, engine_opts_from_env());
+    a->opts = engine_opts_from_env();
+    if (options) apply_engine_options(a->opts, options);
+    a->an = analyze(A11->h, B->h, C22->h, a->opts);
     *out = a.release();
     API_END
 }
@@ -720,7 +749,7 @@ int cpk_analysis_plan(cpk_analysis a, cpk_mat A, cpk_mat C, int nranks, int rank
          "A and C must match the analysis' n and m");
     auto p = std::make_unique<cpk_plan_s>();
     p->n = an.n, p->m = an.m;
-    p->ts = split_tree(an.F0, nranks, engine_opts_from_env().split_tol, -1, &A->h);
+    p->ts = split_tree(an.F0, nranks, a->opts.split_tol, -1, &A->h);
     p->dm = make_dofmap(an.F0, p->ts, an.n);
     p->rp = make_rank_plan(an.F0, p->ts, p->dm, rank);
     p->kp = dist_csr(an.Kp, p->dm, rank, false);

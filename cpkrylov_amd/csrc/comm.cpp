@@ -37,6 +37,12 @@ struct RcclComm : Comm {
         nccl_check(ncclAllGather(send, recv, n, ncclDouble, c, s), "ncclAllGather");
     }
     bool capturable() const override { return true; }  // the solvers also check the dist_graph option
+    int kind() const override { return CPK_COMM_RCCL; }
+    int count() const override {
+        int n = 0;
+        nccl_check(ncclCommCount(c, &n), "ncclCommCount");
+        return n;
+    }
 };
 
 }  // namespace
@@ -61,22 +67,24 @@ void rccl_unique_id(unsigned char *uid) {
 }
 
 // ---- timing stand-in ---------------------------------------------------------------------------
-// NullComm (diagnostic only, CPK_COMM=null): rank `rank` of a P-way partition with no peers.
-// Collectives leave the local contribution in place, so results are meaningless; it exists to
-// time one rank's share of a P-way solve on a single GPU (tools/dist_timing.py).
+// NullComm (diagnostic only, cpk_ctx_create_null): rank `rank` of a P-way partition with no
+// peers.  Collectives leave the local contribution in place, so results are meaningless; it
+// exists to time one rank's share of a P-way solve on a single GPU (tools/dist_timing.py).
 namespace {
 struct NullComm : Comm {
-    int rank;
-    explicit NullComm(int r) : rank(r) {}
+    int rank, P;
+    NullComm(int r, int p) : rank(r), P(p) {}
     void allreduce_sum(double *, size_t, hipStream_t) override {}
     void allgather(const double *send, double *recv, size_t n, hipStream_t s) override {
         if (n) CPK_HIP(hipMemcpyAsync(recv + (size_t)rank * n, send, n * sizeof(double), hipMemcpyDeviceToDevice, s));
     }
     bool capturable() const override { return true; }
     bool has_peers() const override { return false; }
+    int kind() const override { return CPK_COMM_NULL; }
+    int count() const override { return 1; }  // no peers: the communicator holds this rank only
 };
 }  // namespace
-Comm *make_null_comm(int rank) { return new NullComm(rank); }
+Comm *make_null_comm(int rank, int nranks) { return new NullComm(rank, nranks); }
 
 // ---- simulated group --------------------------------------------------------------------------
 struct SimGroup {
@@ -133,6 +141,8 @@ struct SimComm : Comm {
         g->barrier();
     }
     bool capturable() const override { return false; }
+    int kind() const override { return CPK_COMM_SIM; }
+    int count() const override { return g->P; }
 };
 }  // namespace
 

@@ -67,6 +67,8 @@ struct Comm {
     virtual void allgather(const double *send, double *recv, size_t n, hipStream_t s) = 0;
     virtual bool capturable() const = 0;  // may be captured into a hipGraph
     virtual bool has_peers() const { return true; }  // false: the timing stand-in (no exchange)
+    virtual int kind() const = 0;   // CPK_COMM_RCCL / _SIM / _NULL (cpk_ctx_get_info)
+    virtual int count() const = 0;  // ranks of the communicator (RCCL: ncclCommCount)
 };
 
 // Sweep configuration: rows and entries staged per block, threads per block, round 0 / upper
@@ -79,6 +81,11 @@ struct SweepConfig {
     int rows[2] = {192, 512}, cap[2] = {576, 3072}, threads[2] = {64, 256};
     int sub0 = 480;  // round-0 subtree cap (0: cap[0])
 };
+// The distributed preconditioner's default (each rank schedules only its own subtrees): the
+// single-GPU default's lower round-0 subtrees give a rank's 1.25 M rows at S10 / P = 8 a third
+// sweep round, 0.337 against 0.311-0.321 ms per iteration (profiles/r03_dist_timing_v41.log), so
+// a distributed context keeps the round-0 blocks uncapped with 512-thread upper blocks.
+SweepConfig dist_sweep_default();
 
 // Engine options of a context (opts.cpp; cpk_ctx_set_option).  None changes a result: they
 // select equivalent execution paths (each is tested bit-exact against the default) or the
@@ -88,7 +95,7 @@ struct SweepConfig {
 // is created; objects built later see its current values.
 struct EngineOpts {
     SweepConfig sweep;            // sweep:              LDS staging of the sweep schedule
-    bool detach = false;          // detach:             entry-less rows outside the blocks
+    bool sweep_set = false;       //                     sweep given explicitly (else the per-path default)
     double split_tol = 0.03;      // split_tol:          distributed subtree weight tolerance
     bool host_factor = false;     // host_factor:        numeric LDL' on the host (reference path)
     bool no_pipe = false;         // no_pipe:            round 0 one workgroup per block
@@ -96,11 +103,8 @@ struct EngineOpts {
     bool no_col16 = false;        // no_col16:           round-0 forward columns as int32
     bool no_sched_resid = false;  // no_sched_resid:     refinement residual in original order
     bool no_fused_resid = false;  // no_fused_resid:     refinement residual as its own SpMV
-    bool fused_tail_launch = false;  // fused_tail_launch: rows above round 0 by a residual launch
-    bool r0_stride = false;       // r0_stride:          round-0 blocks by stride, not by cost
     int r0_xcd_chunk = 16;        // r0_xcd_chunk:       K > 0: runs of K consecutive round-0 blocks share an XCD
     bool tsolve_global = false;   // tsolve_global:      separator records read from HBM
-    bool tsolve_onepass = false;  // tsolve_onepass:     one-pass separator solve
     bool no_piggy = false;        // no_piggy:           cpminres alpha by its own allreduce
     bool no_halo_merge = false;   // no_halo_merge:      cpminres beta by its own allreduce
     bool no_graph = false;        // no_graph:           no hipGraph capture of iterations
@@ -109,13 +113,19 @@ struct EngineOpts {
     bool no_minres_fuse = false;  // no_minres_fuse:     cpminres update as its own pass (normalise + w, x)
     bool dist_graph = true;       // dist_graph:         capture collectives in the graphs
     int batch = 0;                // batch:              fixed iterations per graph (0: adaptive)
-    bool profile_fwd_nolevels = false;  // profile_fwd_nolevels: diagnostic (cpk_profile_kernels)
     bool profile_fwd_sched = false;     // profile_fwd_sched: diagnostic, the profiled forward reads its input in schedule order
 };
 EngineOpts engine_opts_from_env();
 // name as in the comments above; throws CPK_ERR_ARGS on an unknown name or a bad value
 void set_engine_option(EngineOpts &o, const std::string &name, const std::string &value);
-std::string get_engine_option(const EngineOpts &o, const std::string &name);
+// dist: the value a distributed preconditioner uses (the sweep's per-path default)
+std::string get_engine_option(const EngineOpts &o, const std::string &name, bool dist = false);
+// the sweep configuration a preconditioner of this path is built with
+SweepConfig effective_sweep(const EngineOpts &o, bool dist);
+// every option as "name=value;name=value;..." (the effective sweep, and sweep_set as its own
+// entry), and the inverse: a spec of that form applied on top of o
+std::string engine_opts_string(const EngineOpts &o, bool dist);
+void apply_engine_options(EngineOpts &o, const std::string &spec);
 uint64_t engine_opts_hash(const EngineOpts &o);  // FNV-1a over every option
 
 // Execution context: one GPU, one stream, reduction workspace (and a Comm when nranks > 1).
@@ -166,7 +176,6 @@ void launch_spmv_resid_loc(Ctx &c, const DMat &A, const double *xin, int64_t neg
 // HBM-resident factor + sweep schedule (rows in schedule order).
 struct DFactor {
     int64_t N = 0, nnz = 0, nblk = 0, nlvl = 0;
-    int64_t ndet = 0;     // detached rows [0, ndet): no forward entries, in no block (Schedule::ndet)
     DBuf<uint32_t> fptr;  // forward rows of strict lower L, columns ascending
     DBuf<int32_t> fcol;
     DBuf<int16_t> fcol16;  // round 0 when every forward entry is local: column - block's first row (else empty)
@@ -184,7 +193,7 @@ struct DFactor {
     bool no_upper = false;  // upper rounds through the generic kernels (set before make_dfactor)
     bool no_col16 = false;  // no int16 round-0 forward columns (set before make_dfactor)
     // engine options of the preconditioner's context when it was built (launch-time paths)
-    bool no_fused_resid = false, fused_tail_launch = false;
+    bool no_fused_resid = false;
     bool fuse_last = false;  // single GPU, no entries outside the factor: the last round fwd + bwd in one launch
     int64_t round0_rows = -1;  // round 0 is the rows [0, round0_rows) (-1: not a leading row range)
     std::vector<int32_t> hmeta;  // host copy of meta
@@ -261,8 +270,6 @@ bool fuse_last_ok(const DFactor &F);
 bool launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
                        const int *active, bool sched_in = false, double *xs = nullptr, FwdIn *defer = nullptr,
                        const PackArgs *pk = nullptr);
-// diagnostic: the forward sweep without its level phase (staging + write-back only)
-void launch_sptrsv_fwd_diag(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w);
 // out == null: the solution stays in schedule order in w (and with add, ys += it in place);
 // add with ys: out = P * (ys + solution), ys the previous solution in schedule order
 // pk (optional, distributed): the Kp halo of the output packed by the write-back; returns whether
@@ -276,15 +283,14 @@ bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
 void launch_spmv_resid_sched(Ctx &c, const DMat &A, const int32_t *perm, const double *xin, int64_t neg_from,
                              const double *y, double *r, const int *run);
 // fused refinement input: r = xs - Kps*y, then the forward sweep in place on r (schedule order);
-// round 0 forms r inside the sweep, the rows above it (tail_blk: Kps row blocks of rows >=
-// round0_rows) through the residual SpMV.  Bit-identical to launch_spmv_resid_sched +
-// launch_sptrsv_fwd(sched_in).  False (nothing launched): no matching configuration.
-bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const int32_t *tail_blk, int64_t tail_nblk,
-                             const double *xs, const double *y, double *r, const int *run, FwdIn *defer = nullptr);
+// round 0 forms r inside the sweep, the rows above it by the round-0 kernel's workgroups after
+// their blocks.  Bit-identical to launch_spmv_resid_sched + launch_sptrsv_fwd(sched_in).  False
+// (nothing launched): no matching configuration.
+bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const double *xs, const double *y, double *r,
+                             const int *run, FwdIn *defer = nullptr);
 int debug_pipe_stamps(uint64_t *out, int npairs);  // diagnostic build only (CPK_PIPE_STAMPS)
 int64_t debug_blk_cycles(uint64_t *out, int64_t n);  // likewise: [4][1 << 17] per-block cycles
 // Kps row blocks of the rows [row0, nrows) (A.blk with a boundary at row0)
-void make_tail_blk(const DMat &A, int64_t row0, DBuf<int32_t> &blk, int64_t &nblk);
 // out[i] = x[idx[i]]
 void launch_gather(Ctx &c, const double *x, const int32_t *idx, int64_t n, double *out);
 // small vector helpers
@@ -297,7 +303,7 @@ struct SimGroup;
 SimGroup *simgroup_create(int nranks);
 void simgroup_destroy(SimGroup *g);
 Comm *make_sim_comm(SimGroup *g, int rank);
-Comm *make_null_comm(int rank);  // diagnostic: CPK_COMM=null
+Comm *make_null_comm(int rank, int nranks);  // diagnostic timing stand-in (cpk_ctx_create_null)
 void launch_sum_slots(hipStream_t s, const double *slots, int P, size_t n, double *out);
 struct DSep;
 // pack this rank's separator payload (w rows read by T, rank 0: +-x at the T dofs), allgather
@@ -405,7 +411,7 @@ struct DSep {
     int64_t nsf = 0, nsb = 0, nrec = 0;
     size_t lds = 0;    // LDS bytes of the stepped solve with its records staged, 0 = too large
     size_t lds_g = 0;  // LDS bytes with the records left in HBM; 0 (or no records): one-pass kernel
-    bool tsolve_global = false, tsolve_onepass = false;  // engine options at construction
+    bool tsolve_global = false;  // engine option at construction
 };
 struct RankPlan;
 // Split the forward rows of T and build the steps of the separator level solve.
@@ -433,9 +439,7 @@ struct Precond {
     // accumulated solution all stay in schedule order (apply); kps_from: Kps entry -> Kp entry
     DMat dKps;
     DBuf<int32_t> kps_from;
-    // fused refinement residual (launch_sptrsv_fwd_resid): Kps row blocks of the rows above round 0
-    DBuf<int32_t> kps_tail_blk;
-    int64_t kps_tail_nblk = -1;  // -1: the fused path is off
+    bool fused_resid = false;  // the refinement residual fused into the forward sweep (launch_sptrsv_fwd_resid)
     DBuf<double> xs;     // the apply's signed input in schedule order (captured by the first forward sweep)
     uint64_t pattern_hash = 0;  // sparsity of (A11, B, C22): a refactorization must keep it
     DBuf<int> active;    // refinement predicate

@@ -334,7 +334,7 @@ static void height_levels(const Factor &f, LdlSymbolic *sym) {
 }
 
 Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1, int64_t SUB0,
-                        const std::vector<int64_t> *extra_bwd, bool detach) {
+                        const std::vector<int64_t> *extra_bwd) {
     if (SUB0 <= 0 || SUB0 > CAP0) SUB0 = CAP0;
     const int64_t N = f.N;
     SubClock clk;
@@ -376,22 +376,9 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     // (1) Layer peeling: round r takes the maximal subtrees of at most R rows of the tree that
     //     remains after rounds 0..r-1.  On bushy (nested-dissection) trees the remainder
     //     shrinks geometrically and a few rounds suffice.
-    // Detached rows (opt-in, engine option detach): rows of L without entries (the G pivots of a
-    // G-first ordering, leaves of the elimination tree).  Their forward value is their input and
-    // nothing reads them before the backward sweep's last step, so they can stay out of the
-    // blocks: they come first in the new order and are solved by one streaming pass per sweep
-    // (DFactor::ndet).  Measured at S10: the round-0 blocks stay as many
-    // (the entry cap binds, not the rows) and the streaming passes cost more than the G rows
-    // did inside the blocks, so the default keeps them in.
-    std::vector<char> detached(N, 0);
-    if (detach)
-        for (int64_t v = 0; v < N; v++) detached[v] = nfwd[v] == 0;
-    std::vector<int32_t> alive;
-    alive.reserve(N);
-    for (int64_t v = 0; v < N; v++)
-        if (!detached[v]) alive.push_back((int32_t)v);
-    std::vector<char> is_alive(N, 0);
-    for (int32_t v : alive) is_alive[v] = 1;
+    std::vector<int32_t> alive(N);
+    for (int64_t v = 0; v < N; v++) alive[v] = (int32_t)v;
+    std::vector<char> is_alive(N, 1);
     // per round, written for every alive row before any read (the parent of an alive row is alive)
     std::unique_ptr<int64_t[]> sz(new int64_t[N]);
     std::unique_ptr<int32_t[]> root_of(new int32_t[N]);
@@ -427,12 +414,9 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     //     open cluster absorbs its children's open clusters, closing the largest ones until it
     //     fits in R rows.  Peeled children are already-closed clusters.
     // read only for alive nodes (a peeled row's parent is peeled too), each written before its
-    // parent reads it: no initialisation, except for detached rows (leaves outside the peeling)
+    // parent reads it: no initialisation
     std::unique_ptr<int64_t[]> open_size(new int64_t[N]);
     std::unique_ptr<int32_t[]> open_dep(new int32_t[N]);
-    if (detach)
-        for (int64_t v = 0; v < N; v++)
-            if (detached[v]) open_size[v] = 0, open_dep[v] = -1;
     std::vector<int32_t> tmp;
     const int64_t CAP = CAP1;
     for (int32_t v : alive) {
@@ -466,7 +450,6 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     int32_t nrounds = 0;
     for (int64_t v = N - 1; v >= 0; v--) {
         if (closed_round[v] >= 0) nrounds = std::max(nrounds, closed_round[v] + 1);
-        if (detached[v]) continue;
         const bool root = closed_round[v] >= 0;
         const int32_t c = root ? (int32_t)v : cl[f.parent[v]];
         cl[v] = c;
@@ -494,21 +477,19 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
         }
         s.round_ptr.push_back(nb);
     }
-    // new order: detached rows (ascending), then blocks ascending (= rounds ascending), then
-    // level, then old index
-    std::vector<int32_t> block(N);  // -1: detached
-    std::vector<int64_t> bcount(nb + 2, 0);  // bcount[0]: detached
+    // new order: blocks ascending (= rounds ascending), then level, then old index
+    std::vector<int32_t> block(N);
+    std::vector<int64_t> bcount(nb + 1, 0);
     for (int64_t v = 0; v < N; v++) {
-        block[v] = cl[v] >= 0 ? cluster_block[cl[v]] : -1;
-        bcount[block[v] + 2]++;
+        block[v] = cluster_block[cl[v]];
+        bcount[block[v] + 1]++;
     }
-    for (int32_t b = 0; b <= nb; b++) bcount[b + 1] += bcount[b];
-    s.ndet = bcount[1];
-    s.blk_row.assign(bcount.begin() + 1, bcount.end());
+    for (int32_t b = 0; b < nb; b++) bcount[b + 1] += bcount[b];
+    s.blk_row.assign(bcount.begin(), bcount.end());
     s.order.resize(N);
     {
         std::vector<int64_t> nx(bcount.begin(), bcount.end() - 1);
-        for (int64_t v = 0; v < N; v++) s.order[nx[block[v] + 1]++] = (int32_t)v;
+        for (int64_t v = 0; v < N; v++) s.order[nx[block[v]]++] = (int32_t)v;
     }
     clk.lap("schedule: blocks and order");
     // intra-block levels, blocks in parallel: a block's rows are disjoint from every other

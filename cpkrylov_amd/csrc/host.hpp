@@ -31,10 +31,11 @@ struct HCsr {
 HCsr csr_from_csr(int64_t nr, int64_t nc, const int64_t *rp, const int32_t *ci, const double *v);
 HCsr csr_from_csc(int64_t nr, int64_t nc, const size_t *jc, const size_t *ir, const double *pr);
 HCsr transpose(const HCsr &a);
-// Kp = [A B'; B C]  (opLDL2.m:81)
+// Kp = [A B'; B C]  (opLDL2.m:81); throws CPK_ERR_DIM unless check_kp_dims passes
+void check_kp_dims(const HCsr &A, const HCsr &B, const HCsr &C);  // opLDL2.m:61-75
 HCsr assemble_kp(const HCsr &A, const HCsr &B, const HCsr &C);
 // source of every Kp entry: (block << 40) | entry index, block 0 = A, 1 = B (B and B' entries),
-// 2 = C, in assemble_kp's entry order
+// 2 = C, in assemble_kp's entry order (inputs that pass check_kp_dims)
 std::vector<int64_t> kp_value_sources(const HCsr &A, const HCsr &B, const HCsr &C);
 // blkdiag(A, C): the Krylov operator's diagonal blocks, used to fuse u = A*v and t = C*q.
 HCsr blkdiag(const HCsr &A, const HCsr &C);
@@ -132,7 +133,6 @@ struct Schedule {
     std::vector<int64_t> lvl_row;      // level boundaries (row positions), one array for all blocks
     int64_t max_levels = 0;
     int64_t depth = 0;
-    int64_t ndet = 0;                  // detached rows (no L entries): positions [0, ndet), in no block
 };
 // Round 0 (the wide bottom of the tree) uses blocks of (R0 rows, CAP0 entries); the upper
 // rounds use (R1, CAP1), typically larger so that few launches cover the top of the tree.
@@ -140,9 +140,8 @@ struct Schedule {
 // a block's level count is that of its tallest subtree, so packing several short subtrees
 // per block cuts the barrier-separated level passes per row.
 // extra_bwd[v]: backward entries of row v outside the factor (distributed separators)
-// detach: rows without forward entries stay out of the blocks (engine option detach)
 Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1, int64_t SUB0 = 0,
-                        const std::vector<int64_t> *extra_bwd = nullptr, bool detach = false);
+                        const std::vector<int64_t> *extra_bwd = nullptr);
 // Apply the schedule's relabel to the factor (values unchanged, exact data movement).
 // src (optional): src[t] = index into f.Li / f.Lx of the relabelled factor's entry t.
 Factor relabel(const Factor &f, const Schedule &s, std::vector<int32_t> *src = nullptr);

@@ -156,12 +156,16 @@ HCsr transpose(const HCsr &a) {
     return t;
 }
 
-HCsr assemble_kp(const HCsr &A, const HCsr &B, const HCsr &C) {
+void check_kp_dims(const HCsr &A, const HCsr &B, const HCsr &C) {
     // dimension checks of opLDL2.m:61-75 (same messages)
     if (A.nrows != A.ncols || C.nrows != C.ncols) throw Error(CPK_ERR_DIM, "First and last arguments must be square.");
     if (B.ncols != A.nrows || B.nrows != C.nrows) throw Error(CPK_ERR_DIM, "Incompatible dimensions.");
+    if (A.nrows + C.nrows > INT32_MAX) throw Error(CPK_ERR_DIM, "N exceeds the 32-bit index range");
+}
+
+HCsr assemble_kp(const HCsr &A, const HCsr &B, const HCsr &C) {
+    check_kp_dims(A, B, C);
     const int64_t n = A.nrows, m = C.nrows, N = n + m;
-    if (N > INT32_MAX) throw Error(CPK_ERR_DIM, "N exceeds the 32-bit index range");
     HCsr K;
     K.nrows = K.ncols = N;
     // the entry arrays are zero-filled (first touch of fresh pages) on their own threads while

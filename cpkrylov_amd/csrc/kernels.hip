@@ -210,7 +210,6 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     d.blk_lvl.upload(bl);
     d.lvl_row.upload(lr);
     d.round_ptr = s.round_ptr;
-    d.ndet = s.ndet;
     // per-block metadata records for the pipelined round-0 kernel
     std::vector<int32_t> meta((size_t)d.nblk * 8);
     for (int64_t b = 0; b < d.nblk; b++) {
@@ -224,18 +223,18 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     d.hmeta = meta;
     clk.lap("layout: uploads, block records");
     d.round0_rows = -1;
-    if (s.ndet == 0 && s.round_ptr.size() >= 2) {  // round 0 a leading, contiguous row range?
+    if (s.round_ptr.size() >= 2) {  // round 0 a leading, contiguous row range?
         int64_t r = 0;
         for (int64_t b = s.round_ptr[0]; b < s.round_ptr[1] && r >= 0; b++)
             r = meta[(size_t)b * 8] == r ? meta[(size_t)b * 8 + 1] : -1;
         d.round0_rows = r;
     }
     // round 0's forward entries as 16-bit block-local columns: a round-0 block holds whole
-    // subtrees, so a row's forward columns (its descendants) are in its own block unless rows
-    // were detached; checked here, and the image is only built when it holds for every block
+    // subtrees, so a row's forward columns (its descendants) are in its own block; checked here,
+    // and the image is only built when it holds for every block
     d.fcol16.release();
     d.nnz16 = 0;
-    if (s.ndet == 0 && s.round_ptr.size() >= 2 && !d.no_col16) {
+    if (s.round_ptr.size() >= 2 && !d.no_col16) {
         const int64_t b0 = s.round_ptr[0], nb0 = s.round_ptr[1] - b0;
         std::atomic<bool> bad{false};
         int64_t e_end = 0;
@@ -916,7 +915,7 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
     const bool grec = S.tsolve_global || !fits(S.lds);  // engine option: records in HBM
     const size_t lds = grec ? S.lds_g : S.lds;
     const TkrArgs tkr{tkr_ptr, tkr_col, tkr_val, wT};  // wT: still y's T values (this solve writes it last)
-    if (S.nrec > 0 && fits(lds) && !S.tsolve_onepass) {
+    if (S.nrec > 0 && fits(lds)) {
         hipLaunchKernelGGL(tprefix_kernel, dim3((unsigned)((S.nT + 3) / 4)), dim3(256), 0, c.stream, (int)S.nT,
                            S.tk_ptr.p, S.tk_col.p, S.tk_val.p, S.tr_ptr.p, S.tr_col.p, S.tr_val.p, S.tr_slot.p,
                            S.tf_src.p, S.rbuf.p, S.pre.p, S.rec_v.p, run, active, tkr);
@@ -1222,7 +1221,7 @@ __device__ __forceinline__ void bwd_store(double *out, double *ys, const int32_t
     }
 }
 
-template <int TPB, int MODE = 0>  // MODE 1 (diagnostic): staging + write-back only, no level phase
+template <int TPB>
 __global__ __launch_bounds__(TPB) void sptrsv_fwd_kernel(
     int64_t blk0, int R, int CAP, int skip_first, const int32_t *__restrict__ blk_lvl, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
@@ -1257,13 +1256,11 @@ __global__ __launch_bounds__(TPB) void sptrsv_fwd_kernel(
             S.v[e] = local ? v : v * w[c];
         }
         __syncthreads();
-        if (MODE == 0) {
-            if (skip_first) {
-                sweep_levels<TPB, false>(S, l1 - l0, true);  // round 0: no outside references
-            } else {
-                fold_prefix<TPB>(S, nr);
-                sweep_levels<TPB, false, true, 8>(S, l1 - l0);
-            }
+        if (skip_first) {
+            sweep_levels<TPB, false>(S, l1 - l0, true);  // round 0: no outside references
+        } else {
+            fold_prefix<TPB>(S, nr);
+            sweep_levels<TPB, false, true, 8>(S, l1 - l0);
         }
         for (int i = tid; i < nr; i += TPB) w[r0 + i] = S.w[i];
         return;
@@ -1969,8 +1966,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
             nxt = msrc[bn];
             issue(nxt);  // in flight during the level phase
         }
-        // skip0: level 0 holds only rows without entries (no detached rows: the G pivots are in
-        // the blocks); with detached rows a block's level 0 subtracts their (outside) terms
+        // skip0: level 0 holds only rows without entries (the G pivots are in the blocks)
         // lane-owned rows for the backward sweep only: A/B at S10 (profiles/r03_level_ab_v2.txt),
         // backward 193.9 -> 186.7 us, but forward 211 -> 232 us and the fused forward 270 -> 286
         if (CPK_LEVEL_OWN && SPLIT == 1 && BWD) levels_owned<TPB, RPT, BWD, CPK_PIPE_CH>(S, nl, nr, skip0 != 0, tid);
@@ -2058,17 +2054,17 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
     else if (!bwd)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, 1, xs,
                            (const int16_t *)nullptr, ResArgs{}, am, ap, pk ? *pk : PackArgs{});
     else if (add)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, 1, xs,
                            (const int16_t *)nullptr, ResArgs{}, am, ap, pk ? *pk : PackArgs{});
     else
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.ndet == 0 ? 1 : 0, xs,
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, 1, xs,
                            (const int16_t *)nullptr, ResArgs{}, am, ap, pk ? *pk : PackArgs{});
     return true;
 }
@@ -2127,7 +2123,7 @@ static const double kR0SlotSpeed[2][kR0Slots] = {{1.0, 0.970, 0.964, 0.914}, {1.
 
 void plan_round0(Ctx &c, DFactor &d, const int64_t *kps_ptr) {
     for (int v = 0; v < 3; v++) d.agrid[v] = 0, d.aptr[v].release(), d.ameta[v].release();
-    if (!d.pipelined || d.round_ptr.size() < 2 || c.opts.r0_stride) return;
+    if (!d.pipelined || d.round_ptr.size() < 2) return;
     const int64_t b0 = d.round_ptr[0], nb = d.round_ptr[1] - b0;
     if (nb <= 0 || d.hmeta.size() < (size_t)(b0 + nb) * 8) return;
     int64_t grid[3] = {0, 0, 0};
@@ -2136,7 +2132,7 @@ void plan_round0(Ctx &c, DFactor &d, const int64_t *kps_ptr) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     pipe_round0(c, d, false, false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, &grid[0]);
     pipe_round0(c, d, true, false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, &grid[2]);
-    if (kps_ptr && d.fcol16.n > 0 && d.ndet == 0) pipe_round0_resid(c, d, nullptr, nullptr, ResArgs{}, &grid[1]);
+    if (kps_ptr && d.fcol16.n > 0) pipe_round0_resid(c, d, nullptr, nullptr, ResArgs{}, &grid[1]);
     for (int v = 0; v < 3; v++) {
         const int64_t G = grid[v];
         if (G <= 1 || G >= nb) continue;
@@ -2198,15 +2194,15 @@ void plan_round0(Ctx &c, DFactor &d, const int64_t *kps_ptr) {
     }
 }
 
-template <int TPB, int MODE>
+template <int TPB>
 static void fwd_round(Ctx &c, const DFactor &F, int64_t r, const double *xin, int64_t neg_from, double *w,
                       const int *run, const int *active, int sched_in, double *xs) {
     const int i = r == 0 ? 0 : 1;
     const int64_t b0 = F.round_ptr[r], nb = F.round_ptr[r + 1] - b0;
     if (!nb) return;
-    hipLaunchKernelGGL((sptrsv_fwd_kernel<TPB, MODE>), dim3((unsigned)nb), dim3(TPB),
+    hipLaunchKernelGGL((sptrsv_fwd_kernel<TPB>), dim3((unsigned)nb), dim3(TPB),
                        sweep_lds_bytes(F.sweep_rows[i], F.sweep_cap[i]), c.stream, b0, F.sweep_rows[i],
-                       F.sweep_cap[i], (r == 0 && F.ndet == 0) ? 1 : 0, F.blk_lvl.p, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.perm.p,
+                       F.sweep_cap[i], r == 0 ? 1 : 0, F.blk_lvl.p, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.perm.p,
                        xin, neg_from, w, run, active, sched_in, xs);
 }
 
@@ -2222,89 +2218,47 @@ static void bwd_round(Ctx &c, const DFactor &F, int64_t r, double *w, double *ou
                        out, run, active, ys);
 }
 
-// ---- detached rows (Schedule::ndet): rows of L without entries ------------------------------
-// forward: their value is their input, w = P'x (or x itself in schedule order)
-__global__ void det_fwd_kernel(int64_t ndet, const int32_t *__restrict__ perm, const double *__restrict__ xin,
-                               int64_t neg_from, int sched_in, double *__restrict__ w, const int *run, const int *active) {
-    if (skip(run, active)) return;
-    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < ndet; q += (int64_t)gridDim.x * blockDim.x) {
-        if (sched_in) {
-            w[q] = xin[q];
-        } else {
-            const int32_t s = perm[q];
-            const double x = xin[s];
-            w[q] = s >= neg_from ? -x : x;
-        }
-    }
-}
-// backward, after every block: y = w / D minus their terms (columns of L, stored order), one
-// row per thread, the same operations as a block row; then the write-back of bwd_store
-template <bool ADD>
-__global__ void det_bwd_kernel(int64_t ndet, const uint32_t *__restrict__ bptr, const int32_t *__restrict__ bcol,
-                               const double *__restrict__ bval, const double *__restrict__ D,
-                               const int32_t *__restrict__ perm, double *w, double *out, double *ys, const int *run,
-                               const int *active) {
-    if (skip(run, active)) return;
-    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < ndet; q += (int64_t)gridDim.x * blockDim.x) {
-        double acc = w[q] / D[q];
-        const uint32_t e1 = bptr[q + 1];
-        for (uint32_t e = bptr[q]; e < e1; e++) acc -= bval[e] * w[bcol[e]];
-        w[q] = acc;
-        bwd_store<ADD>(out, ys, perm, q, acc);
-    }
-}
-static inline unsigned det_grid(int64_t n) { return (unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 8192); }
-
-template <int MODE>
 static bool fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
                     const int *active, int sched_in, double *xs = nullptr, int64_t rfirst = 0, FwdIn *defer = nullptr,
                     const PackArgs *pk = nullptr) {
     int64_t R = (int64_t)F.round_ptr.size() - 1;
-    bool packed = pk != nullptr && F.ndet == 0 && rfirst == 0;  // every round through a packing kernel
-    if (defer && MODE == 0 && fuse_last_ok(F)) {  // the last round runs with the backward sweep
+    bool packed = pk != nullptr && rfirst == 0;  // every round through a packing kernel
+    if (defer && fuse_last_ok(F)) {  // the last round runs with the backward sweep
         *defer = FwdIn{xin, neg_from, sched_in, xs, true, R - 1};
         R -= 1;
     }
-    if (F.ndet > 0 && !(sched_in && xin == w) && rfirst == 0)  // in place in schedule order: already there
-        hipLaunchKernelGGL(det_fwd_kernel, dim3(det_grid(F.ndet)), dim3(kBlock), 0, c.stream, F.ndet, F.perm.p, xin,
-                           neg_from, sched_in, w, run, active);
     const PackArgs none{};
     for (int64_t r = rfirst; r < R; r++) {
         bool used = true;
-        if (r == 0 && MODE == 0 &&
+        if (r == 0 &&
             pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr, xs, nullptr, pk,
                         &used)) {
             packed = packed && used;
             continue;
         }
-        if (r > 0 && MODE == 0 &&
+        if (r > 0 &&
             upper_round(c, F, r, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr, xs,
                         pk ? *pk : none))
             continue;
         packed = false;
         switch (F.sweep_threads[r == 0 ? 0 : 1]) {
-        case 32: fwd_round<32, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
-        case 64: fwd_round<64, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
-        case 128: fwd_round<128, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
-        case 512: fwd_round<512, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
-        case 1024: fwd_round<1024, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
-        default: fwd_round<256, MODE>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
+        case 32: fwd_round<32>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
+        case 64: fwd_round<64>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
+        case 128: fwd_round<128>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
+        case 512: fwd_round<512>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
+        case 1024: fwd_round<1024>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
+        default: fwd_round<256>(c, F, r, xin, neg_from, w, run, active, sched_in, xs); break;
         }
     }
     CPK_HIP(hipGetLastError());
     return packed && R > 0;
 }
 
-void launch_sptrsv_fwd_diag(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w) {
-    fwd_all<1>(c, F, xin, neg_from, w, nullptr, nullptr, 0);
-}
-
 bool launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
                        const int *active, bool sched_in, double *xs, FwdIn *defer, const PackArgs *pk) {
     // schedule-order input: no perm gather and no negation (neg_from applies to original indices)
-    if (xs && F.ndet > 0) throw Error(CPK_ERR_UNSUPPORTED, "internal: input capture with detached rows");
     if (defer) defer->valid = false;
-    return fwd_all<0>(c, F, xin, sched_in ? INT64_MAX : neg_from, w, run, active, sched_in ? 1 : 0, xs, 0, defer, pk);
+    return fwd_all(c, F, xin, sched_in ? INT64_MAX : neg_from, w, run, active, sched_in ? 1 : 0, xs, 0, defer, pk);
 }
 
 // diagnostic: the per-workgroup stamps of the last round-0 launch (0 unless built with
@@ -2333,37 +2287,17 @@ int debug_pipe_stamps(uint64_t *out, int npairs) {
 #endif
 }
 
-void make_tail_blk(const DMat &A, int64_t row0, DBuf<int32_t> &blk, int64_t &nblk) {
-    std::vector<int32_t> h((size_t)A.nblk + 1);
-    CPK_HIP(hipMemcpy(h.data(), A.blk.p, h.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
-    std::vector<int32_t> t{(int32_t)row0};  // splitting a block at row0 only shrinks it
-    for (int32_t b : h)
-        if (b > row0) t.push_back(b);
-    nblk = (int64_t)t.size() - 1;
-    blk.upload(t);
-}
-
-bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const int32_t *tail_blk, int64_t tail_nblk,
-                             const double *xs, const double *y, double *r, const int *run, FwdIn *defer) {
+bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const double *xs, const double *y, double *r, const int *run, FwdIn *defer) {
     if (defer) defer->valid = false;
     const bool off = F.no_fused_resid;  // A/B switch: separate residual SpMV
-    if (off || tail_nblk < 0 || !F.pipelined || F.ndet != 0 || F.round0_rows < 0 || F.fcol16.n == 0 ||
-        F.round_ptr.size() < 2 || Kps.halo())
+    if (off || !F.pipelined || F.round0_rows < 0 || F.fcol16.n == 0 || F.round_ptr.size() < 2 ||
+        Kps.halo())
         return false;
-    // the rows above round 0 inside the round-0 kernel (fused_tail_launch: a residual launch)
-    const bool tail_launch = F.fused_tail_launch;
-    const ResArgs ra{Kps.ptr.p, Kps.col.p, Kps.val.p, y, xs, F.round0_rows, tail_launch ? F.round0_rows : F.N};
-    // round 0: r of its rows formed in the sweep (nothing is launched unless a configuration matches)
+    // round 0: r of its rows formed in the sweep (nothing is launched unless a configuration
+    // matches); the rows above round 0 by the round-0 kernel's workgroups after their blocks
+    const ResArgs ra{Kps.ptr.p, Kps.col.p, Kps.val.p, y, xs, F.round0_rows, F.N};
     if (!pipe_round0_resid(c, F, r, run, ra)) return false;
-    // the rows above round 0: their r by the residual SpMV over those rows, then the upper rounds
-    if (tail_launch && tail_nblk > 0) {
-        const EpiResidSched e{xs, nullptr, 0, r, run};
-        const unsigned grid = spmv_grid<EpiResidSched, false>(tail_nblk);
-        hipLaunchKernelGGL((spmv_stream<EpiResidSched, false>), dim3(grid), dim3(kBlock), 0, c.stream, Kps.ptr.p,
-                           Kps.col.p, Kps.val.p, tail_blk, tail_nblk, y, (int64_t)0, e, (const double *)nullptr,
-                           (int64_t)0);
-    }
-    fwd_all<0>(c, F, r, INT64_MAX, r, run, nullptr, 1, nullptr, 1, defer);
+    fwd_all(c, F, r, INT64_MAX, r, run, nullptr, 1, nullptr, 1, defer);
     return true;
 }
 
@@ -2371,7 +2305,7 @@ bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
                        const int *active, double *ys, const FwdIn *last, const PackArgs *pk) {
     if (!out && add && !ys) throw Error(CPK_ERR_ARGS, "internal: accumulating backward sweep without a base");
     int64_t R = (int64_t)F.round_ptr.size() - 1;
-    bool packed = pk != nullptr && out != nullptr && F.ndet == 0 && !(last && last->valid);
+    bool packed = pk != nullptr && out != nullptr && !(last && last->valid);
     const PackArgs none{};
     if (last && last->valid) {  // the deferred last round, forward and backward (sptrsv_last_kernel)
         launch_last(c, F, *last, w, out, add, run, active, ys);
@@ -2396,14 +2330,6 @@ bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
         case 513: bwd_round<256, true>(c, F, r, w, out, run, active, ys); break;
         default: bwd_round<256, false>(c, F, r, w, out, run, active, ys); break;
         }
-    }
-    if (F.ndet > 0) {
-        if (add)
-            hipLaunchKernelGGL(det_bwd_kernel<true>, dim3(det_grid(F.ndet)), dim3(kBlock), 0, c.stream, F.ndet, F.bptr.p,
-                               F.bcol.p, F.bval.p, F.D.p, F.perm.p, w, out, ys, run, active);
-        else
-            hipLaunchKernelGGL(det_bwd_kernel<false>, dim3(det_grid(F.ndet)), dim3(kBlock), 0, c.stream, F.ndet,
-                               F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, w, out, ys, run, active);
     }
     CPK_HIP(hipGetLastError());
     return packed && R > 0;

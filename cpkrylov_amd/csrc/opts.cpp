@@ -52,17 +52,13 @@ struct BoolOpt {
     bool EngineOpts::*m;
 };
 const BoolOpt kBool[] = {
-    {"detach", &EngineOpts::detach},
     {"host_factor", &EngineOpts::host_factor},
     {"no_pipe", &EngineOpts::no_pipe},
     {"no_upper", &EngineOpts::no_upper},
     {"no_col16", &EngineOpts::no_col16},
     {"no_sched_resid", &EngineOpts::no_sched_resid},
     {"no_fused_resid", &EngineOpts::no_fused_resid},
-    {"fused_tail_launch", &EngineOpts::fused_tail_launch},
-    {"r0_stride", &EngineOpts::r0_stride},
     {"tsolve_global", &EngineOpts::tsolve_global},
-    {"tsolve_onepass", &EngineOpts::tsolve_onepass},
     {"no_piggy", &EngineOpts::no_piggy},
     {"no_halo_merge", &EngineOpts::no_halo_merge},
     {"no_graph", &EngineOpts::no_graph},
@@ -70,11 +66,20 @@ const BoolOpt kBool[] = {
     {"no_tkr", &EngineOpts::no_tkr},
     {"no_minres_fuse", &EngineOpts::no_minres_fuse},
     {"dist_graph", &EngineOpts::dist_graph},
-    {"profile_fwd_nolevels", &EngineOpts::profile_fwd_nolevels},
     {"profile_fwd_sched", &EngineOpts::profile_fwd_sched},
 };
 
 }  // namespace
+
+SweepConfig dist_sweep_default() {
+    SweepConfig c;
+    c.rows[0] = 192, c.cap[0] = 576, c.threads[0] = 64;
+    c.rows[1] = 1024, c.cap[1] = 4096, c.threads[1] = 512;
+    c.sub0 = 0;
+    return c;
+}
+
+SweepConfig effective_sweep(const EngineOpts &o, bool dist) { return (dist && !o.sweep_set) ? dist_sweep_default() : o.sweep; }
 
 void set_engine_option(EngineOpts &o, const std::string &name, const std::string &value) {
     for (const BoolOpt &b : kBool)
@@ -84,6 +89,9 @@ void set_engine_option(EngineOpts &o, const std::string &name, const std::string
         }
     if (name == "sweep") {
         o.sweep = parse_sweep(value);
+        o.sweep_set = true;
+    } else if (name == "sweep_set") {  // engine_opts_string's round trip: "0" restores the per-path default
+        o.sweep_set = parse_bool(name, value);
     } else if (name == "split_tol") {
         char *end = nullptr;
         const double v = strtod(value.c_str(), &end);
@@ -101,10 +109,11 @@ void set_engine_option(EngineOpts &o, const std::string &name, const std::string
     }
 }
 
-std::string get_engine_option(const EngineOpts &o, const std::string &name) {
+std::string get_engine_option(const EngineOpts &o, const std::string &name, bool dist) {
     for (const BoolOpt &b : kBool)
         if (name == b.name) return o.*b.m ? "1" : "0";
-    if (name == "sweep") return sweep_str(o.sweep);
+    if (name == "sweep") return sweep_str(effective_sweep(o, dist));
+    if (name == "sweep_set") return o.sweep_set ? "1" : "0";
     if (name == "split_tol") {
         char b[64];
         snprintf(b, sizeof b, "%.17g", o.split_tol);
@@ -130,6 +139,36 @@ EngineOpts engine_opts_from_env() {
     return o;
 }
 
+std::string engine_opts_string(const EngineOpts &o, bool dist) {
+    std::string s;
+    auto put = [&](const std::string &name) { s += name + "=" + get_engine_option(o, name, dist) + ";"; };
+    for (const BoolOpt &b : kBool) put(b.name);
+    put("sweep");
+    put("sweep_set");
+    put("split_tol");
+    put("batch");
+    put("r0_xcd_chunk");
+    return s;
+}
+
+void apply_engine_options(EngineOpts &o, const std::string &spec) {
+    size_t p = 0;
+    std::string sweep_set;
+    while (p < spec.size()) {
+        size_t q = spec.find(';', p);
+        if (q == std::string::npos) q = spec.size();
+        const std::string item = spec.substr(p, q - p);
+        p = q + 1;
+        if (item.empty()) continue;
+        const size_t eq = item.find('=');
+        if (eq == std::string::npos) throw Error(CPK_ERR_ARGS, "engine options: expected name=value, got '" + item + "'");
+        const std::string name = item.substr(0, eq), value = item.substr(eq + 1);
+        if (name == "sweep_set") sweep_set = value;  // after "sweep", whatever the order
+        else set_engine_option(o, name, value);
+    }
+    if (!sweep_set.empty()) set_engine_option(o, "sweep_set", sweep_set);
+}
+
 uint64_t engine_opts_hash(const EngineOpts &o) {
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](const std::string &s) {
@@ -138,6 +177,7 @@ uint64_t engine_opts_hash(const EngineOpts &o) {
     };
     for (const BoolOpt &b : kBool) mix(b.name), mix(o.*b.m ? "1" : "0");
     mix(sweep_str(o.sweep));
+    mix(o.sweep_set ? "1" : "0");
     mix(get_engine_option(o, "split_tol"));
     mix(std::to_string(o.batch));
     mix(std::to_string(o.r0_xcd_chunk));

@@ -65,7 +65,7 @@ Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOp
         an.sweep = o.sweep;
         if (global_schedule) {
             an.S = build_schedule(f0, an.sweep.rows[0], an.sweep.cap[0], an.sweep.rows[1], an.sweep.cap[1],
-                                  an.sweep.sub0, nullptr, o.detach);
+                                  an.sweep.sub0, nullptr);
             pc.lap("schedule");
             an.F = relabel(f0, an.S, device_numeric ? &an.rsrc : nullptr);
             pc.lap("relabel");
@@ -96,7 +96,7 @@ Precond *precond_create(Ctx &c, Analysis &&an, PrecondPre *pre) {
         pc->dF.sweep_rows[i] = an.sweep.rows[i], pc->dF.sweep_cap[i] = an.sweep.cap[i],
         pc->dF.sweep_threads[i] = an.sweep.threads[i];
     pc->dF.pipelined = !c.opts.no_pipe, pc->dF.no_upper = c.opts.no_upper, pc->dF.no_col16 = c.opts.no_col16;
-    pc->dF.no_fused_resid = c.opts.no_fused_resid, pc->dF.fused_tail_launch = c.opts.fused_tail_launch;
+    pc->dF.no_fused_resid = c.opts.no_fused_resid;
     pc->dF.fuse_last = !c.opts.no_fuse_last;  // single GPU: no entries outside the factor
     pc->no_sched = c.opts.no_sched_resid;
     // Kp and Kp in schedule order depend only on Kp and the pivot order: they are built and
@@ -167,9 +167,9 @@ Precond *precond_create(Ctx &c, Analysis &&an, PrecondPre *pre) {
         clk.lap("numeric factorization (device)");
     }
     plan_round0(c, pc->dF, kps_ptr.empty() ? nullptr : kps_ptr.data());
-    if (pc->dKps.nnz && pc->dF.ndet == 0) pc->xs.alloc(pc->N);
+    if (pc->dKps.nnz) pc->xs.alloc(pc->N);
     if (pc->dKps.nnz && pc->dF.round0_rows >= 0 && pc->dF.fcol16.n > 0)
-        make_tail_blk(pc->dKps, pc->dF.round0_rows, pc->kps_tail_blk, pc->kps_tail_nblk);
+        pc->fused_resid = true;
     clk.lap("round-0 assignment");
     an.F = Factor();
     pc->F = std::move(an.F0);
@@ -256,12 +256,12 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     // local sweeps: schedule + relabel of this rank's subtrees, rows summed in exported order
     std::vector<int64_t> nextra(rp.nsub);
     for (int64_t j = 0; j < rp.nsub; j++) nextra[j] = (int64_t)rp.extra[j].size();
-    const SweepConfig &sw = an.sweep;
-    Schedule S = build_schedule(rp.Fsub, sw.rows[0], sw.cap[0], sw.rows[1], sw.cap[1], sw.sub0, &nextra, c.opts.detach);
+    const SweepConfig sw = effective_sweep(c.opts, true);  // the distributed path's (dist_sweep_default)
+    Schedule S = build_schedule(rp.Fsub, sw.rows[0], sw.cap[0], sw.rows[1], sw.cap[1], sw.sub0, &nextra);
     for (int i = 0; i < 2; i++)
         pc->dF.sweep_rows[i] = sw.rows[i], pc->dF.sweep_cap[i] = sw.cap[i], pc->dF.sweep_threads[i] = sw.threads[i];
     pc->dF.pipelined = !c.opts.no_pipe, pc->dF.no_upper = c.opts.no_upper, pc->dF.no_col16 = c.opts.no_col16;
-    pc->dF.no_fused_resid = c.opts.no_fused_resid, pc->dF.fused_tail_launch = c.opts.fused_tail_launch;
+    pc->dF.no_fused_resid = c.opts.no_fused_resid;
     {
         Factor Fl = relabel(rp.Fsub, S);
         std::vector<int64_t> key(rp.nsub);
@@ -380,7 +380,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     }
     sub.lap("dist: refinement without the Kp halo");
     T.nT = rp.nT, T.kt = rp.kt, T.nlev = (int64_t)rp.tlev_ptr.size() - 1, T.ntdof = (int64_t)rp.tdof.size();
-    T.tsolve_global = c.opts.tsolve_global, T.tsolve_onepass = c.opts.tsolve_onepass;
+    T.tsolve_global = c.opts.tsolve_global;
     T.kt_data = kt1 > 0 ? kt1 - kSepPiggy : 0;
     if (pc->tkr) pc->hslot2.upload(hslot2), pc->tkr_ptr.upload(tkr_ptr), pc->tkr_col.upload(tkr_col), pc->tkr_val.upload(tkr_val);
     auto i32 = [](const std::vector<int64_t> &v) { return std::vector<int32_t>(v.begin(), v.end()); };
@@ -489,12 +489,19 @@ uint64_t pattern_hash(const HCsr &A11, const HCsr &B, const HCsr &C22) {
 Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22) {
     const bool dev = !c.opts.host_factor;
     // the refactorization's inputs (Kp's value sources, the sparsity hash) depend only on the
-    // matrices: computed on a second host thread during the analysis
+    // matrices: computed on a second host thread during the analysis, once the dimensions are
+    // known to be consistent (kp_value_sources indexes by them)
+    check_kp_dims(A11, B, C22);
     std::vector<int64_t> src;
     uint64_t hash = 0;
+    std::exception_ptr side_err;
     std::thread side([&] {
-        if (dev) src = kp_value_sources(A11, B, C22);
-        hash = pattern_hash(A11, B, C22);
+        try {
+            if (dev) src = kp_value_sources(A11, B, C22);
+            hash = pattern_hash(A11, B, C22);
+        } catch (...) {
+            side_err = std::current_exception();
+        }
     });
     // Kp and the device factorization's symbolic data are uploaded while the host builds the
     // schedule
@@ -515,6 +522,7 @@ Precond *precond_create(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22)
         throw;
     }
     side.join();
+    if (side_err) std::rethrow_exception(side_err);
     Precond *pc = precond_create(c, std::move(an), dev ? &pre : nullptr);
     pc->pattern_hash = hash;
     if (dev) pc->dl.kp_from.upload(src);
@@ -660,9 +668,9 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
         // last backward sweep scatters y = P * (ys + dy)
         for (int64_t s = 0; s < steps; s++) {
             // r = x - op.A*y; the refinement solve runs in place on r (each row reads its own
-            // input before it writes, detached rows keep theirs); y += op.LDL*r
+            // input before it writes); y += op.LDL*r
             FwdIn last;
-            if (!(have_xs && launch_sptrsv_fwd_resid(c, dF, dKps, kps_tail_blk.p, kps_tail_nblk, xs.p, w.p, r.p, run, &last))) {
+            if (!(have_xs && (fused_resid && launch_sptrsv_fwd_resid(c, dF, dKps, xs.p, w.p, r.p, run, &last)))) {
                 if (have_xs) launch_spmv_resid_sched(c, dKps, nullptr, xs.p, 0, w.p, r.p, run);
                 else launch_spmv_resid_sched(c, dKps, dF.perm.p, x, neg_from, w.p, r.p, run);
                 launch_sptrsv_fwd(c, dF, r.p, N, r.p, run, nullptr, true, nullptr, &last);
@@ -707,12 +715,12 @@ double Precond::apply_bytes() const {
         const double bwd_keep = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn;
         const double kps = 12 * (double)dKps.nnz + 4 * (Nn + 1) + 8 * Nn /*y*/ +
                            (xs.n ? 8 * Nn /*xs*/ : 12 * Nn /*x(perm)*/) + 8 * Nn /*r*/;
-        const double fwd_s = 12 * l - 2 * (double)dF.nnz16 + 4 * (Nn + 1) + 16 * Nn - 16 * (double)dF.ndet;  // in place: detached rows untouched
+        const double fwd_s = 12 * l - 2 * (double)dF.nnz16 + 4 * (Nn + 1) + 16 * Nn;
         const double bwd_acc = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn + 8 * Nn /*ys*/;
         double b = fwd + (xs.n ? 8 * Nn : 0.0) /*xs written*/ + bwd_keep + steps * (kps + fwd_s + bwd_acc) + (4 + 8) * Nn /*last: perm + scatter*/ +
                    (steps - 1) * 8.0 * Nn /*ys written back in place*/;
         // fused refinement input (launch_sptrsv_fwd_resid): r is neither written nor read back
-        if (xs.n && kps_tail_nblk >= 0 && dF.pipelined && !dF.no_fused_resid)
+        if (xs.n && fused_resid && dF.pipelined && !dF.no_fused_resid)
             b -= steps * 16.0 * Nn;
         return b;
     }

@@ -2100,10 +2100,7 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
     // order (no perm gather; the values are meaningless, the time and traffic are not)
     FwdIn last;
     const bool fsched = c.opts.profile_fwd_sched;
-    if (c.opts.profile_fwd_nolevels)
-        out->fwd_ms = timeit([&]() { launch_sptrsv_fwd_diag(c, M.dF, x.p, M.n, M.w.p); });
-    else
-        out->fwd_ms = timeit([&]() { launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr, fsched, nullptr, &last); });
+    out->fwd_ms = timeit([&]() { launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr, fsched, nullptr, &last); });
     out->fwd_bytes = 12.0 * l - 2.0 * (double)M.dF.nnz16 + 4.0 * (Nn + 1) + 4.0 * Nn /*perm*/ + 8.0 * Nn /*x*/ + 8.0 * Nn /*w*/;
     const double pair_ms = timeit([&]() {
         launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr, fsched, nullptr, &last);
@@ -2118,12 +2115,21 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
     if (last.valid) {  // the deferred last round: one launch inside the backward count
         out->fwd_launches = last.from;
         out->bwd_launches = last.from + 1;
+        // its forward half runs in the backward launch: its bytes move with it, so
+        // fwd / bwd each pair time and bytes of the same launches (the sum is unchanged)
+        const DFactor &F = M.dF;
+        double rows = 0, ents = 0;
+        for (int64_t b = F.round_ptr[last.from]; b < F.round_ptr[last.from + 1]; b++) {
+            const int32_t *m = &F.hmeta[(size_t)b * 8];
+            rows += m[1] - m[0], ents += m[5] - m[4];
+        }
+        const double fl = 12.0 * ents + 4.0 * (rows + 1) + 4.0 * rows + 8.0 * rows + 8.0 * rows;
+        out->fwd_bytes -= fl, out->bwd_bytes += fl;
     }
     out->fwd_resid_ms = out->fwd_resid_bytes = 0;
-    if (M.sched_path() && M.xs.n &&
-        launch_sptrsv_fwd_resid(c, M.dF, M.dKps, M.kps_tail_blk.p, M.kps_tail_nblk, x.p, y.p, z.p, nullptr)) {
+    if (M.sched_path() && M.xs.n && M.fused_resid && launch_sptrsv_fwd_resid(c, M.dF, M.dKps, x.p, y.p, z.p, nullptr)) {
         out->fwd_resid_ms = timeit([&]() {
-            launch_sptrsv_fwd_resid(c, M.dF, M.dKps, M.kps_tail_blk.p, M.kps_tail_nblk, x.p, y.p, z.p, nullptr);
+            launch_sptrsv_fwd_resid(c, M.dF, M.dKps, x.p, y.p, z.p, nullptr);
         });
         // Kps, y, xs (the residual's reads) + the factor and w (the sweep's); r never goes to HBM
         // for round 0 (the tail rows' r write and read are < 1 % and not counted)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CPK_ABI_VERSION 1
+#define CPK_ABI_VERSION 2
 
 typedef enum {
     CPK_OK = 0,
@@ -105,8 +105,21 @@ int cpk_abi_version(void);
 /* Fill `id` (128 bytes) with an RCCL unique id on rank 0; broadcast it to the other ranks. */
 int cpk_get_unique_id(unsigned char id[128]);
 /* device < 0: use the current device.  nranks == 1 and unique_id == NULL: no communicator.
- * With a unique_id the context runs the distributed path even for nranks == 1. */
+ * With a unique_id the context runs the distributed path (RCCL) even for nranks == 1;
+ * nranks > 1 requires a unique_id. */
 int cpk_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id, cpk_ctx *out);
+/* Diagnostic timing stand-in (no reference counterpart): rank `rank` of an nranks-way
+ * distributed context WITHOUT peers.  Every collective is a no-op (an allgather copies the
+ * rank's own slot), so results are meaningless, but each kernel is exactly that rank's share of
+ * the P-way solve: tools/dist_timing.py times one rank's work on one GPU with it.  Never used by
+ * cpk_ctx_create; nranks must be > 1. */
+int cpk_ctx_create_null(int device, int rank, int nranks, cpk_ctx *out);
+/* Communicator kinds reported by cpk_ctx_get_info. */
+enum { CPK_COMM_NONE = 0, CPK_COMM_RCCL = 1, CPK_COMM_SIM = 2, CPK_COMM_NULL = 3 };
+/* info[8] = {device, rank, nranks, communicator kind (CPK_COMM_*), ranks the communicator holds
+ * (RCCL: ncclCommCount; SimComm: the group's ranks; the timing stand-in: 1; none: 0),
+ * distributed path (0/1), 0, 0}. */
+int cpk_ctx_get_info(cpk_ctx ctx, int64_t *info);
 /* Single-GPU rehearsal of the distributed path: `nranks` ranks as host threads of one process,
  * all on one device, exchanging through a shared HBM buffer instead of RCCL (RCCL refuses two
  * ranks on one GPU).  Each thread creates its context with cpk_ctx_create_sim and then makes
@@ -119,15 +132,18 @@ int cpk_ctx_create_sim(int device, cpk_simgroup group, int rank, int nranks, cpk
  * that give identical results, and the sweep schedule / distributed split that every rank
  * must build identically).  A context starts from the CPK_<NAME> environment variables, read
  * once at creation; a change applies to preconditioners and solves created afterwards.
- * Names: sweep ("rows,cap,threads[,rows,cap,threads[,sub0]]"), detach, split_tol, host_factor,
- * no_pipe, no_upper, no_col16, no_sched_resid, no_fused_resid, fused_tail_launch, r0_stride,
- * r0_xcd_chunk, tsolve_global, tsolve_onepass, no_piggy, no_halo_merge, no_graph, no_fuse_last, no_tkr,
- * no_minres_fuse,
- * dist_graph, batch, profile_fwd_nolevels, profile_fwd_sched.  Booleans as "0"/"1".  A distributed preconditioner allgathers a hash
- * of its plan and of every option at creation and fails (CPK_ERR_ARGS) on every rank unless
- * all ranks agree. */
+ * Names: sweep ("rows,cap,threads[,rows,cap,threads[,sub0]]"; unset, each path has its own
+ * default: a distributed context reports and uses the distributed one), split_tol, host_factor,
+ * no_pipe, no_upper, no_col16, no_sched_resid, no_fused_resid, r0_xcd_chunk, tsolve_global,
+ * no_piggy, no_halo_merge, no_graph, no_fuse_last, no_tkr, no_minres_fuse, dist_graph, batch,
+ * profile_fwd_sched (diagnostic), sweep_set ("0" returns sweep to the per-path default).
+ * Booleans as "0"/"1".  A distributed preconditioner allgathers a hash of its plan and of every
+ * option at creation and fails (CPK_ERR_ARGS) on every rank unless all ranks agree. */
 int cpk_ctx_set_option(cpk_ctx ctx, const char *name, const char *value);
 int cpk_ctx_get_option(cpk_ctx ctx, const char *name, char *buf, size_t cap);
+/* Every engine option of the context as "name=value;name=value;..." (the form cpk_analyze's
+ * `options` takes), with the sweep this context's path uses. */
+int cpk_ctx_get_options(cpk_ctx ctx, char *buf, size_t cap);
 int cpk_ctx_destroy(cpk_ctx ctx);
 int cpk_ctx_synchronize(cpk_ctx ctx);
 
@@ -200,9 +216,12 @@ int cpk_pc_export(cpk_pc M, int64_t *Lcolptr, int32_t *Lrowind, double *Lval, do
 
 /* ---- host-only analysis (no GPU needed) ------------------------------------------------- */
 /* The host half of cpk_pc_create: Kp assembly, fill-reducing ordering, static-pivot LDL' and
- * the triangular-sweep schedule.  Matrices for this call may be created with ctx == NULL. */
+ * the triangular-sweep schedule.  Matrices for this call may be created with ctx == NULL.
+ * Engine options: the CPK_<NAME> environment (as a new context starts), then `options`
+ * ("name=value;...", NULL: none) on top -- pass cpk_ctx_get_options of a context to analyse
+ * and plan exactly as that context's preconditioner would (sweep, split_tol). */
 typedef struct cpk_analysis_s *cpk_analysis;
-int cpk_analyze(cpk_mat A11, cpk_mat B, cpk_mat C22, cpk_analysis *out);
+int cpk_analyze(cpk_mat A11, cpk_mat B, cpk_mat C22, const char *options, cpk_analysis *out);
 int cpk_analysis_destroy(cpk_analysis an);
 int cpk_analysis_get_info(cpk_analysis an, cpk_pc_info *info);
 int cpk_analysis_export(cpk_analysis an, int64_t *Lcolptr, int32_t *Lrowind, double *Lval, double *D,
@@ -217,8 +236,9 @@ int cpk_analysis_schedule(cpk_analysis an, int64_t *nlevels, int64_t *round_ptr,
 
 /* ---- distributed plan (host-only) --------------------------------- */
 /* The row-block plan of rank `rank` out of `nranks` for the system the analysis was built on
- * (A: n x n, C: m x m the Krylov operator's blocks).  Every rank computes the same global plan
- * deterministically; a distributed cpk_pc_create builds exactly this.  Exposed for tests and
+ * (A: n x n, C: m x m the Krylov operator's blocks), with the analysis' engine options
+ * (split_tol).  Every rank computes the same global plan deterministically; a distributed
+ * cpk_pc_create on a context with the same options builds exactly this.  Exposed for tests and
  * inspection: cpk_plan_array(plan, name, &count, out) copies array `name` (values as double
  * for *_val, fsub_Lx, fsub_D, extra_val, tf_val, tb_val, DT; every other array as int64) into
  * out (NULL: count only).  Names: sizes [P, rank, n, m, N, n_loc, m_loc, N_loc, nsub, nT, kt,

@@ -22,7 +22,7 @@ def test_every_declared_symbol_is_exported():
 
 
 def test_abi_version():
-    assert _lib.lib.cpk_abi_version() == 1
+    assert _lib.lib.cpk_abi_version() == 2
 
 
 def test_symgivens_host_entry():
@@ -41,3 +41,14 @@ def test_no_silent_fallback_without_gpu():
         assert e.code == _lib.CPK_ERR_HIP
     else:
         raise AssertionError("context creation must fail without a GPU")
+
+
+def test_multi_rank_context_needs_unique_id():
+    """cpk_ctx_create refuses nranks > 1 without an RCCL unique id (checked before any device
+    call): there is no environment switch to a peer-less communicator any more; the timing
+    stand-in has its own constructor (cpk_ctx_create_null), which refuses nranks == 1."""
+    import ctypes as C
+    h = C.c_void_p()
+    assert _lib.lib.cpk_ctx_create(0, 0, 2, None, C.byref(h)) == _lib.CPK_ERR_ARGS
+    assert b"unique_id" in _lib.lib.cpk_last_error()
+    assert _lib.lib.cpk_ctx_create_null(0, 0, 1, C.byref(h)) == _lib.CPK_ERR_ARGS

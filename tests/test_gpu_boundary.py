@@ -130,3 +130,68 @@ def test_dist_operator_cache_follows_preconditioner():
         h, ho = stats["residHistory"], so["residHistory"]
         assert np.max(np.abs(h - ho)) / ho[0] <= 1e-8, i
         assert np.linalg.norm(x - xo) / np.linalg.norm(xo) <= 1e-8, i
+
+
+def test_precond_create_dimension_errors(gpu_ctx):
+    """opLDL2's dimension checks (opLDL2.m:61-75) run before any helper
+    thread reads the blocks, so mismatched G and B raise CPK_ERR_DIM instead of writing past an
+    array -- through the device constructor, not only the host analysis."""
+    import cpkrylov_amd as cpk
+    from cpkrylov_amd import _lib
+    P = F.load("cvxqp1_m")
+    for G, B, Cm in ((P["G"][:10, :10], P["B"], -P["C"]), (P["G"], P["B"][:, :10], -P["C"]),
+                     (P["G"], P["B"], -P["C"][:5, :5]), (P["G"][:, :10], P["B"], -P["C"])):
+        with pytest.raises(cpk.CpkError) as e:
+            cpk.opLDL2(G, B, Cm)
+        assert e.value.code == _lib.CPK_ERR_DIM
+    M = cpk.opLDL2(P["G"], P["B"], -P["C"])  # the library is still usable
+    assert M.n == P["n"] + P["m"]
+
+
+def test_context_info_and_per_path_sweep_default(gpu_ctx):
+    """cpk_ctx_get_info reports the communicator a context holds, and an unset sweep option
+    reports the default of the context's path: the single-GPU one on a plain context, the
+    distributed one (dist_sweep_default) on a distributed context, which its preconditioners
+    then use; an explicit sweep wins on either path.  The timing stand-in is a constructor of
+    its own and says so."""
+    import cpkrylov_amd as cpk
+    single = cpk.Context(device=0)
+    try:
+        assert single.info() == {"device": 0, "rank": 0, "nranks": 1, "comm": "none", "comm_ranks": 0,
+                                 "distributed": False}
+        assert single.get_option("sweep") == "192,576,64,512,3072,256,480"
+        assert "sweep=192,576,64,512,3072,256,480;" in single.options_string()
+    finally:
+        single.close()
+    g = cpk.SimGroup(2)
+
+    def one(r):
+        ctx = cpk.Context(device=0, rank=r, nranks=2, simgroup=g)
+        try:
+            info = ctx.info()
+            default = ctx.get_option("sweep")
+            P = F.load("cvxqp1_m")
+            M = cpk.opLDL2(P["G"], P["B"], -P["C"], ctx=ctx)
+            rounds = M.sweep_info()["rounds"]
+            ctx.set_option("sweep", "192,576,64,512,3072,256,480")
+            explicit = ctx.get_option("sweep")
+            ctx.set_option("sweep_set", "0")
+            back = ctx.get_option("sweep")
+            del M
+            return info, default, explicit, back, rounds
+        finally:
+            ctx.close()
+
+    with ThreadPoolExecutor(2) as ex:
+        res = [f.result(timeout=600) for f in [ex.submit(one, r) for r in range(2)]]
+    for r, (info, default, explicit, back, rounds) in enumerate(res):
+        assert info == {"device": 0, "rank": r, "nranks": 2, "comm": "sim", "comm_ranks": 2, "distributed": True}
+        assert default == "192,576,64,1024,4096,512,0" and back == default
+        assert explicit == "192,576,64,512,3072,256,480"
+        assert rounds >= 1
+    null = cpk.Context(device=0, rank=3, nranks=8, timing_standin=True)
+    try:
+        assert null.info()["comm"] == "null" and null.info()["comm_ranks"] == 1
+        assert null.get_option("sweep") == "192,576,64,1024,4096,512,0"
+    finally:
+        null.close()

@@ -287,11 +287,11 @@ def test_dist_minres_fused_update_bitexact(P):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["tsolve_global", "tsolve_onepass"])
+@pytest.mark.parametrize("path", ["tsolve_global"])
 @pytest.mark.parametrize("P", [2, 4])
 def test_dist_apply_separator_fallbacks_bitexact(P, path):
-    """The separator solve's fallbacks (records left in HBM for a separator too large for LDS;
-    the one-pass global kernel) give the same bits as the staged solve and the oracle."""
+    """The separator solve's fallback (records left in HBM for a separator too large for LDS)
+    gives the same bits as the staged solve and the oracle."""
     import cpkrylov_amd as cpk
     S = _system("synthetic20k")
     z = np.random.default_rng(7).standard_normal(S["n"] + S["m"])

@@ -38,11 +38,7 @@ def replay(an, x):
     Lc = L.tocsc()
     Lc.sort_indices()
     w = np.full(N, np.nan)
-    ndet = lr[0]  # detached rows (no entries of L): positions [0, ndet), in no block
-    for q in range(ndet):
-        k = order[q]
-        assert Lr.indptr[k + 1] == Lr.indptr[k], "a detached row has forward entries"
-        w[k] = x[perm[k]]
+    assert lr[0] == 0  # every row is in a block
     for r in range(len(rp) - 1):
         for b in range(rp[r], rp[r + 1]):
             for lv in range(bl[b], bl[b + 1]):
@@ -67,14 +63,6 @@ def replay(an, x):
                     w[k] = acc
                     done[k] = True
                     y[perm[k]] = acc
-    for q in range(ndet):  # after every block, one pass
-        k = order[q]
-        acc = w[k] / D[k]
-        for e in range(Lc.indptr[k + 1] - 1, Lc.indptr[k] - 1, -1):
-            assert done[Lc.indices[e]], "backward dependency not ready"
-            acc -= Lc.data[e] * w[Lc.indices[e]]
-        w[k] = acc
-        y[perm[k]] = acc
     return y
 
 
@@ -191,6 +179,16 @@ def test_split_tol_option_validated(monkeypatch):
     monkeypatch.delenv("CPK_SPLIT_TOL")
     p3 = cpk.dist_plan(S["G"], S["B"], -S["C"], S["Q"], S["C"], 2, 0)
     assert p6["nT"] <= p3["nT"]
+    # the same option handed over explicitly (as a context's cpk_ctx_get_options string or a
+    # dict): the analysis and the plan follow it, not the environment
+    q6 = cpk.dist_plan(S["G"], S["B"], -S["C"], S["Q"], S["C"], 2, 0, options={"split_tol": 0.06})
+    q6s = cpk.dist_plan(S["G"], S["B"], -S["C"], S["Q"], S["C"], 2, 0, options="split_tol=0.06;")
+    for k in ("T", "dofs", "node_rank"):
+        assert np.array_equal(q6[k], p6[k]) and np.array_equal(q6s[k], p6[k]), k
+    with pytest.raises(cpk.CpkError):
+        cpk.dist_plan(S["G"], S["B"], -S["C"], S["Q"], S["C"], 2, 0, options="split_tol")
+    small = cpk.analyze(S["G"], S["B"], -S["C"], options={"sweep": "64,128,64"})["info"]
+    assert small["nblocks"] > cpk.analyze(S["G"], S["B"], -S["C"])["info"]["nblocks"]
 
 
 @pytest.mark.parametrize("name", ["cvxqp1_m", "cvxqp2_s"])

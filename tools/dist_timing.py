@@ -1,7 +1,8 @@
 """Per-rank work of a P-way distributed S10 solve, timed on ONE GPU (diagnostic).
 
-CPK_COMM=null gives the context a communicator without peers: collectives are no-ops, so the
-numbers are meaningless but the kernels are exactly one rank's share of the P-way solve.
+Context(timing_standin=True) (cpk_ctx_create_null) gives the context a communicator without
+peers: collectives are no-ops, so the numbers are meaningless but the kernels are exactly one
+rank's share of the P-way solve.
 Prints, per (P, rank): the local rows, the construction time of the rank's preconditioner
 (ptime, and a refactorization with the same values), kernel timings (cpk_profile_kernels) and
 the wall time per iteration of a 20-iteration cpminres call (collective latency NOT included).
@@ -15,7 +16,6 @@ import time
 import numpy as np
 import torch  # before libcpk initialises HIP
 
-os.environ["CPK_COMM"] = "null"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import cpkrylov_amd as cpk  # noqa: E402
 from cpkrylov_amd import _lib  # noqa: E402
@@ -30,7 +30,7 @@ runs = [(P, r, sw) for sw in sweeps for P, r in runs]
 for P, r, sw in runs:
     if sw:
         os.environ["CPK_SWEEP"] = sw
-    ctx = cpk.Context(device=0, rank=r, nranks=P) if P > 1 else cpk.Context(device=0)
+    ctx = cpk.Context(device=0, rank=r, nranks=P, timing_standin=True) if P > 1 else cpk.Context(device=0)
     A, B, Cm, G = (cpk.Matrix(S[k], ctx) for k in ("Q", "B", "C", "G"))
     t0 = time.perf_counter()
     M = cpk.opLDL2(G, B, -S["C"], ctx=ctx)
@@ -62,7 +62,7 @@ for P, r, sw in runs:
         per_it = dt / max(int(st.niters), 1) * 1e3
     except cpk.CpkError as e:
         err = str(e)[:120]
-    print(json.dumps({"P": P, "rank": r, "sweep": sw, "N_loc": len(dofs), "nrounds": M.info["nrounds"],
+    print(json.dumps({"P": P, "rank": r, "sweep": ctx.get_option("sweep"), "N_loc": len(dofs), "nrounds": M.info["nrounds"],
                       "construct_s": round(construct_s, 3), "ptime_s": round(ptime_s, 3), "refactor_s": round(refactor_s, 4),
                       "spmv_us": round(p.spmv_ms * 1e3, 1), "resid_us": round(p.resid_ms * 1e3, 1),
                       "fwd_us": round(p.fwd_ms * 1e3, 1), "bwd_us": round(p.bwd_ms * 1e3, 1),
