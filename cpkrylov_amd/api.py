@@ -313,9 +313,9 @@ class opLDL2:
 
     def sep_info(self):
         """Diagnostic: the distributed separator solve's staging (cpk_pc_sep_info)."""
-        v = (C.c_int64 * 8)()
+        v = (C.c_int64 * 10)()
         check(lib.cpk_pc_sep_info(self.h, v))
-        return dict(zip(("dist", "nT", "nlev", "nrec", "lds", "lds_g", "kt", "tkr"), list(v)))
+        return dict(zip(("dist", "nT", "nlev", "nrec", "lds", "lds_g", "kt", "tkr", "sched", "fused"), list(v)))
 
     def sweep_info(self):
         """Diagnostic: the sweep schedule as launched (cpk_pc_sweep_info)."""

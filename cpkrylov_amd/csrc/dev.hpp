@@ -272,8 +272,8 @@ bool launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_
                        const PackArgs *pk = nullptr);
 // out == null: the solution stays in schedule order in w (and with add, ys += it in place);
 // add with ys: out = P * (ys + solution), ys the previous solution in schedule order
-// pk (optional, distributed): the Kp halo of the output packed by the write-back; returns whether
-// every round packed
+// pk (optional, distributed): the output packed by the write-back, keyed by output index (out
+// given) or by schedule row (out == null); returns whether every round packed
 bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
                        const int *active, double *ys = nullptr, const FwdIn *last = nullptr, const PackArgs *pk = nullptr);
 // r = xin(perm) - A*y with A = P'*Kp*P in schedule order (rows and columns), y in schedule
@@ -286,8 +286,13 @@ void launch_spmv_resid_sched(Ctx &c, const DMat &A, const int32_t *perm, const d
 // round 0 forms r inside the sweep, the rows above it by the round-0 kernel's workgroups after
 // their blocks.  Bit-identical to launch_spmv_resid_sched + launch_sptrsv_fwd(sched_in).  False
 // (nothing launched): no matching configuration.
+// pk / packed (distributed): the separator payload packed by the sweep's write-back, and whether
+// every round packed it (else the caller packs with tpack_kernel)
 bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const double *xs, const double *y, double *r,
-                             const int *run, FwdIn *defer = nullptr);
+                             const int *run, FwdIn *defer = nullptr, const PackArgs *pk = nullptr,
+                             bool *packed = nullptr);
+// buf[slot[q]] = w[q] for q < n with slot[q] >= 0 (a payload the sweeps' write-back did not pack)
+void launch_pack_slots(Ctx &c, const int32_t *slot, int64_t n, const double *w, double *buf, const int *run);
 int debug_pipe_stamps(uint64_t *out, int npairs);  // diagnostic build only (CPK_PIPE_STAMPS)
 int64_t debug_blk_cycles(uint64_t *out, int64_t n);  // likewise: [4][1 << 17] per-block cycles
 // Kps row blocks of the rows [row0, nrows) (A.blk with a boundary at row0)
@@ -316,10 +321,12 @@ void launch_sep_exchange(Ctx &c, const DSep &S, const double *w, const double *x
 // redundant separator solve into wT (= w + nsub); rank 0 writes (add: accumulates) y at the T dofs
 // hslot / hbuf (optional): also pack y's Kp halo at the T dofs (PackArgs, backward)
 // tkr_* (optional, Precond::tkr): first form the T rows' refinement residual (launch_tkr_resid's
-// arithmetic, inside the prefix kernel when that path runs)
+// arithmetic, inside the prefix kernel when that path runs) from y's T values tkr_yT (default: wT,
+// which this solve overwrites last)
 void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active,
                       const int32_t *hslot = nullptr, double *hbuf = nullptr, const int32_t *tkr_ptr = nullptr,
-                      const int32_t *tkr_col = nullptr, const double *tkr_val = nullptr);
+                      const int32_t *tkr_col = nullptr, const double *tkr_val = nullptr,
+                      const double *tkr_yT = nullptr);
 // the T rows' refinement residual after the refinement's separator exchange, on every rank:
 // S.rbuf[tf_src[t]] (the T input +-x sent by rank 0) -= Kp row t * y, y from wT (T columns) and
 // the exchange's extra slots (subtree columns); each row summed in Kp's column order from 0.0
@@ -496,6 +503,16 @@ struct Precond {
     DBuf<int32_t> hslot2, tkr_ptr, tkr_col;
     DBuf<double> tkr_val;
     bool tkr = false;
+    // distributed, one forced refinement step, in schedule order: the first
+    // solve keeps its solution in schedule order (w, T values in w[nsub..]); the residual of the
+    // rank's subtree rows runs on Kp's local rows permuted into schedule order (dKpsl: columns are
+    // schedule positions, T columns nsub + t, so both read w), fused into the refinement solve's
+    // forward sweep; hslot2s: hslot2 keyed by schedule position; xs (nsub) the signed input
+    DMat dKpsl;
+    DBuf<int32_t> hslot2s;
+    bool dsched = false;
+    void dist_sched_apply(const double *x, int64_t neg_from, double *y, const int *run, const double *piggy_src);
+    PackArgs fwd_pack(const double *xt, int64_t xt_neg, const double *piggy_src) const;
     bool steps1_forced() const { return nitref == 1 && force_itref != 0 && !(residual_update != 0 && handle); }
     // algorithmic HBM bytes of one apply
     double apply_bytes() const;

@@ -903,7 +903,8 @@ void launch_tkr_resid(Ctx &c, const DSep &S, const int32_t *ptr, const int32_t *
 
 void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active,
                       const int32_t *hslot, double *hbuf, const int32_t *tkr_ptr, const int32_t *tkr_col,
-                      const double *tkr_val) {
+                      const double *tkr_val, const double *tkr_yT) {
+    if (!tkr_yT) tkr_yT = wT;
     if (S.nT == 0) return;
     static const bool lds_attr = [] {
         return hipFuncSetAttribute((const void *)tsolve_steps_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -914,7 +915,7 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
     auto fits = [&](size_t b) { return b && (b <= 64 * 1024 || lds_attr); };
     const bool grec = S.tsolve_global || !fits(S.lds);  // engine option: records in HBM
     const size_t lds = grec ? S.lds_g : S.lds;
-    const TkrArgs tkr{tkr_ptr, tkr_col, tkr_val, wT};  // wT: still y's T values (this solve writes it last)
+    const TkrArgs tkr{tkr_ptr, tkr_col, tkr_val, tkr_yT};  // y's T values (wT itself: this solve writes it last)
     if (S.nrec > 0 && fits(lds)) {
         hipLaunchKernelGGL(tprefix_kernel, dim3((unsigned)((S.nT + 3) / 4)), dim3(256), 0, c.stream, (int)S.nT,
                            S.tk_ptr.p, S.tk_col.p, S.tk_val.p, S.tr_ptr.p, S.tr_col.p, S.tr_val.p, S.tr_slot.p,
@@ -932,7 +933,7 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
         CPK_HIP(hipGetLastError());
         return;
     }
-    if (tkr_ptr) launch_tkr_resid(c, S, tkr_ptr, tkr_col, tkr_val, wT, run, active);  // the one-pass kernel reads rbuf
+    if (tkr_ptr) launch_tkr_resid(c, S, tkr_ptr, tkr_col, tkr_val, tkr_yT, run, active);  // the one-pass kernel reads rbuf
     hipLaunchKernelGGL(tsolve_kernel, dim3(1), dim3(256), (size_t)S.nT * sizeof(double), c.stream, (int)S.nlev,
                        (int)S.nT, S.lev_ptr.p, S.lev_rows.p, S.tf_ptr.p, S.tf_col.p, S.tf_val.p, S.tf_src.p,
                        S.tb_ptr.p, S.tb_col.p, S.tb_val.p, S.DT.p, S.rbuf.p, S.tdof.p, (int)S.ntdof, wT, y,
@@ -1495,8 +1496,10 @@ __device__ __forceinline__ void upper_block(
                     const double o = ADD ? (ys ? ys[r0 + i] : out[sp[j]]) + z : z;
                     out[sp[j]] = o;
                     pack_put(pk, sp[j], o);
-                } else if (ADD) {
-                    ys[r0 + i] = ys[r0 + i] + z;
+                } else {  // the solution stays in schedule order: packed by schedule row
+                    const double o = ADD ? ys[r0 + i] + z : z;
+                    if (ADD) ys[r0 + i] = o;
+                    pack_put(pk, r0 + i, o);
                 }
             } else {
                 pack_put(pk, r0 + i, z);
@@ -1983,8 +1986,10 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
                         const double o = ADD ? xg[j] + z : z;
                         out[dst[j]] = o;
                         pack_put(pk, dst[j], o);
-                    } else if (ADD) {
-                        ys[r0 + i] = xg[j] + z;
+                    } else {  // the solution stays in schedule order: packed by schedule row
+                        const double o = ADD ? xg[j] + z : z;
+                        if (ADD) ys[r0 + i] = o;
+                        pack_put(pk, r0 + i, o);
                     }
                 } else {
                     pack_put(pk, r0 + i, z);
@@ -2045,7 +2050,7 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true, kRes>), dim3((unsigned)grid),
                            blk, lds, c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p,
                            F.D.p, F.perm.p, xin, neg_from, w, out, run, active, 1, ys, 1, xs,
-                           (const int16_t *)F.fcol16.p, *ra, am, ap, PackArgs{});
+                           (const int16_t *)F.fcol16.p, *ra, am, ap, pk ? *pk : PackArgs{});
     else if (loc)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true>), dim3((unsigned)grid), blk,
                            lds, c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
@@ -2084,8 +2089,8 @@ static bool pipe_round0(Ctx &c, const DFactor &F, bool bwd, bool add, const doub
 
 // the fused-residual round-0 instantiations (launch_sptrsv_fwd_resid)
 static bool pipe_round0_resid(Ctx &c, const DFactor &F, double *r, const int *run, const ResArgs &ra,
-                              int64_t *plan_grid = nullptr) {
-#define CPK_PR(...) pipe_round<__VA_ARGS__>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra, plan_grid)
+                              int64_t *plan_grid = nullptr, const PackArgs *pk = nullptr, bool *pk_used = nullptr) {
+#define CPK_PR(...) pipe_round<__VA_ARGS__>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra, plan_grid, pk, pk_used)
     return CPK_PR(64, 3, 9) || CPK_PR(64, 4, 12) || CPK_PR(128, 2, 6) || CPK_PR(64, 6, 18);
 #undef CPK_PR
 }
@@ -2222,7 +2227,7 @@ static bool fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
                     const int *active, int sched_in, double *xs = nullptr, int64_t rfirst = 0, FwdIn *defer = nullptr,
                     const PackArgs *pk = nullptr) {
     int64_t R = (int64_t)F.round_ptr.size() - 1;
-    bool packed = pk != nullptr && rfirst == 0;  // every round through a packing kernel
+    bool packed = pk != nullptr;  // every round launched here through a packing kernel
     if (defer && fuse_last_ok(F)) {  // the last round runs with the backward sweep
         *defer = FwdIn{xin, neg_from, sched_in, xs, true, R - 1};
         R -= 1;
@@ -2251,7 +2256,7 @@ static bool fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
         }
     }
     CPK_HIP(hipGetLastError());
-    return packed && R > 0;
+    return packed && (R > 0 || rfirst > 0);
 }
 
 bool launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_from, double *w, const int *run,
@@ -2287,8 +2292,10 @@ int debug_pipe_stamps(uint64_t *out, int npairs) {
 #endif
 }
 
-bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const double *xs, const double *y, double *r, const int *run, FwdIn *defer) {
+bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const double *xs, const double *y, double *r,
+                             const int *run, FwdIn *defer, const PackArgs *pk, bool *packed) {
     if (defer) defer->valid = false;
+    if (packed) *packed = false;
     const bool off = F.no_fused_resid;  // A/B switch: separate residual SpMV
     if (off || !F.pipelined || F.round0_rows < 0 || F.fcol16.n == 0 || F.round_ptr.size() < 2 ||
         Kps.halo())
@@ -2296,8 +2303,10 @@ bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const do
     // round 0: r of its rows formed in the sweep (nothing is launched unless a configuration
     // matches); the rows above round 0 by the round-0 kernel's workgroups after their blocks
     const ResArgs ra{Kps.ptr.p, Kps.col.p, Kps.val.p, y, xs, F.round0_rows, F.N};
-    if (!pipe_round0_resid(c, F, r, run, ra)) return false;
-    fwd_all(c, F, r, INT64_MAX, r, run, nullptr, 1, nullptr, 1, defer);
+    bool used = false;
+    if (!pipe_round0_resid(c, F, r, run, ra, nullptr, pk, &used)) return false;
+    const bool rest = fwd_all(c, F, r, INT64_MAX, r, run, nullptr, 1, nullptr, 1, defer, pk);
+    if (packed) *packed = pk != nullptr && used && rest;
     return true;
 }
 
@@ -2305,7 +2314,7 @@ bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
                        const int *active, double *ys, const FwdIn *last, const PackArgs *pk) {
     if (!out && add && !ys) throw Error(CPK_ERR_ARGS, "internal: accumulating backward sweep without a base");
     int64_t R = (int64_t)F.round_ptr.size() - 1;
-    bool packed = pk != nullptr && out != nullptr && !(last && last->valid);
+    bool packed = pk != nullptr && !(last && last->valid);
     const PackArgs none{};
     if (last && last->valid) {  // the deferred last round, forward and backward (sptrsv_last_kernel)
         launch_last(c, F, *last, w, out, add, run, active, ys);
@@ -2336,6 +2345,22 @@ bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
 }
 
 // ---- small helpers ---------------------------------------------------------------------------
+__global__ void pack_slots_kernel(const int32_t *__restrict__ slot, int64_t n, const double *__restrict__ w,
+                                  double *__restrict__ buf, const int *run) {
+    if (run && *run == 0) return;
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t s = slot[q];
+        if (s >= 0) buf[s] = w[q];
+    }
+}
+
+void launch_pack_slots(Ctx &c, const int32_t *slot, int64_t n, const double *w, double *buf, const int *run) {
+    if (n <= 0) return;
+    const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, 2048);
+    hipLaunchKernelGGL(pack_slots_kernel, dim3(grid), dim3(kBlock), 0, c.stream, slot, n, w, buf, run);
+    CPK_HIP(hipGetLastError());
+}
+
 __global__ void sub_state_kernel(const double *__restrict__ x, int64_t neg_from, const double *__restrict__ g,
                                  int64_t N, double *__restrict__ t, const int *run) {
     if (run && *run == 0) return;

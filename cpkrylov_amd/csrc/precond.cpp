@@ -308,10 +308,12 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
         const HCsr &K = an.Kp;
         std::vector<int32_t> tof((size_t)an.N, -1);  // dof -> T index
         for (int64_t t = 0; t < rp.nT; t++) tof[an.F0.perm[ts.T[t]]] = (int32_t)t;
+        const bool want_tkr = !c.opts.no_tkr && rp.kt > 0 && rp.nT > 0;
+        const bool want_sched = !c.opts.no_sched_resid && (rp.nT == 0 || want_tkr);
         // Kp(i, j) != 0 joins an ancestor and a descendant, so outside T a row couples only with
         // its own rank's rows: checked over the whole matrix (the same verdict on every rank)
-        std::atomic<bool> coupled{!c.opts.no_tkr && rp.kt > 0 && rp.nT > 0};
-        if (coupled)
+        std::atomic<bool> coupled{want_tkr || want_sched};
+        if (coupled && c.nranks > 1)
             parallel_for(K.nrows, [&](int64_t lo, int64_t hi) {
                 for (int64_t d = lo; d < hi && coupled.load(std::memory_order_relaxed); d++)
                     if (tof[d] < 0)
@@ -320,7 +322,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
                             if (tof[g] < 0 && dm->owner[g] != dm->owner[d]) coupled = false;
                         }
             }, 1 << 16);
-        const bool ok = coupled;
+        const bool ok = want_tkr && coupled;
         std::vector<std::vector<int32_t>> need((size_t)c.nranks);
         for (int64_t t = 0; t < rp.nT && ok; t++) {
             const int32_t d = an.F0.perm[ts.T[t]];
@@ -376,6 +378,53 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
             make_dmat(kl, pc->dKpl);
             pc->dKpl.nloc = nloc;  // columns >= nloc: wT
             pc->tkr = true;
+        }
+        if (want_sched && coupled && (rp.nT == 0 || pc->tkr)) {
+            // the subtree rows' Kp rows in schedule order, entries in Kp's order (so each row sum
+            // is the residual SpMV's); columns: schedule positions, T dofs nsub + t
+            const int64_t nsub = rp.nsub;
+            const std::vector<int32_t> mine = dm->dofs(c.rank);
+            std::vector<int32_t> spos(mine.size(), -1), lrow((size_t)nsub);
+            for (int64_t q = 0; q < nsub; q++) {
+                lrow[q] = rp.Fsub.perm[S.order[q]];
+                spos[(size_t)lrow[q]] = (int32_t)q;
+            }
+            HCsr ks;
+            ks.nrows = nsub, ks.ncols = nsub + rp.nT;
+            ks.ptr.assign((size_t)nsub + 1, 0);
+            for (int64_t q = 0; q < nsub; q++) {
+                const int32_t d = mine[(size_t)lrow[q]];
+                ks.ptr[q + 1] = ks.ptr[q] + (K.ptr[d + 1] - K.ptr[d]);
+            }
+            ks.ind.resize((size_t)ks.ptr[nsub]);
+            ks.val.resize((size_t)ks.ptr[nsub]);
+            std::atomic<bool> bad{false};
+            parallel_for(nsub, [&](int64_t lo, int64_t hi) {
+                for (int64_t q = lo; q < hi; q++) {
+                    const int32_t d = mine[(size_t)lrow[q]];
+                    int64_t t = ks.ptr[q];
+                    for (int64_t p = K.ptr[d]; p < K.ptr[d + 1]; p++, t++) {
+                        const int32_t g = K.ind[p];
+                        const int32_t col = tof[g] >= 0 ? (int32_t)(nsub + tof[g]) : spos[(size_t)dm->lidx[g]];
+                        if (col < 0) bad = true;
+                        ks.ind[t] = col;
+                        ks.val[t] = devnum ? (double)(p + 1) : K.val[p];
+                    }
+                }
+            }, 1 << 14);
+            if (bad) throw Error(CPK_ERR_FACTOR, "internal: a subtree row's Kp row leaves its rank");
+            make_dmat(ks, pc->dKpsl);
+            if (pc->tkr) {
+                std::vector<int32_t> h2((size_t)std::max<int64_t>(nsub, 1), -1);
+                for (int64_t q = 0; q < nsub; q++) h2[q] = hslot2[(size_t)lrow[q]];
+                pc->hslot2s.upload(h2);
+            }
+            pc->xs.alloc((size_t)std::max<int64_t>(nsub, 1));
+            pc->dsched = true;
+            // the refinement residual fused into the round-0 forward sweep (launch_sptrsv_fwd_resid)
+            pc->fused_resid = pc->dF.round0_rows >= 0 && pc->dF.fcol16.n > 0;
+            // no separator: the last round's forward and backward meet in one launch, as on one GPU
+            pc->dF.fuse_last = !c.opts.no_fuse_last && rp.nT == 0;
         }
     }
     sub.lap("dist: refinement without the Kp halo");
@@ -436,7 +485,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
         add(pc->dF.fval, 0), add(pc->dF.bval, 0), add(pc->dF.D, 1);
         add(T.tf_val, 0), add(T.tb_val, 0), add(T.DT, 1), add(T.tk_val, 0), add(T.tr_val, 0), add(T.rec_v, 0);
         add(pc->dKp.val, 2);
-        add(pc->dKpl.val, 2), add(pc->tkr_val, 2);
+        add(pc->dKpl.val, 2), add(pc->tkr_val, 2), add(pc->dKpsl.val, 2);
         dldl_setup(pc->dl, an.sym, an.F0, {}, {}, {});
         pc->kpg.upload(an.Kp.val);
         dldl_numeric(c, pc->dl, pc->kpg.p, pc->dl.Lx.p, pc->dl.D.p);
@@ -451,7 +500,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     pc->dofmap = dm;
     an.F = Factor();
     pc->w.alloc((size_t)std::max<int64_t>(pc->nsub + T.nT, 1));
-    pc->r.alloc((size_t)std::max<int64_t>(pc->N, 1));
+    pc->r.alloc((size_t)std::max<int64_t>(std::max<int64_t>(pc->N, pc->nsub + T.nT), 1));  // dsched: a work vector
     pc->active.alloc(1);
     c.ensure_partials(std::max<size_t>(pc->dKp.nblk * 2, 4096));
     CPK_HIP(hipDeviceSynchronize());
@@ -603,12 +652,7 @@ bool Precond::ldl_solve(const double *xin, int64_t neg_from, double *y, bool add
     // from them after the exchange), not the refinement input's
     const double *xt = stage == 2 ? xT : xin;
     const int64_t xt_neg = stage == 2 ? xT_neg : neg_from;
-    PackArgs fp;
-    if (sep.tslot.n) {
-        fp.slot = sep.tslot.p, fp.buf = sep.sbuf.p, fp.tdof = sep.tdof.p, fp.ntdof = (int)sep.ntdof;
-        fp.nsend = (int)sep.nsend, fp.kt_data = (int)sep.kt_data, fp.x = xt, fp.neg_from = xt_neg;
-        fp.piggy = piggy_src;
-    }
+    const PackArgs fp = fwd_pack(xt, xt_neg, piggy_src);
     const bool fpacked = launch_sptrsv_fwd(c, dF, xin, neg_from, w.p, run, act, false, nullptr, nullptr,
                                            sep.tslot.n ? &fp : nullptr);
     launch_sep_exchange(c, sep, w.p, xt, xt_neg, piggy_src, fpacked);
@@ -619,6 +663,54 @@ bool Precond::ldl_solve(const double *xin, int64_t neg_from, double *y, bool add
     if (hpack) bp.slot = hslot.p, bp.buf = dKp.sbuf.p;
     if (stage == 1) bp.slot = hslot2.p, bp.buf = sep.sbuf.p;  // y of the rows T's Kp rows read
     return launch_sptrsv_bwd(c, dF, w.p, y, add, run, act, nullptr, nullptr, (hpack || stage == 1) ? &bp : nullptr);
+}
+
+// the forward sweep's separator payload: its rows' values by tslot, rank 0's T inputs +-xt[tdof]
+// and the piggyback values (tpack_kernel's work, in the write-back)
+PackArgs Precond::fwd_pack(const double *xt, int64_t xt_neg, const double *piggy_src) const {
+    PackArgs fp;
+    if (sep.tslot.n) {
+        fp.slot = sep.tslot.p, fp.buf = sep.sbuf.p, fp.tdof = sep.tdof.p, fp.ntdof = (int)sep.ntdof;
+        fp.nsend = (int)sep.nsend, fp.kt_data = (int)sep.kt_data, fp.x = xt, fp.neg_from = xt_neg;
+        fp.piggy = piggy_src;
+    }
+    return fp;
+}
+
+// y = M*x with one forced refinement step, distributed, in schedule order:
+// the single-GPU apply's kernels plus a separator exchange and solve inside each LDL solve.
+//   solve 1: forward sweep (captures the signed input xs, packs the payload), exchange, separator
+//            solve (rank 0: y at the T dofs), backward sweep kept in schedule order in w (packs the
+//            subtree values T's Kp rows read into the payload's extra slots, hslot2s);
+//   solve 2: r = xs - Kpsl*w fused into the forward sweep (w holds the subtree rows and T), the
+//            exchange, the separator solve forming the T rows' residual x_T - Kp_T*y itself and
+//            accumulating rank 0's T dofs, and the backward sweep writing y = P*(w + dy).
+// Every row sums in the order of the single-GPU path: bit-identical to it and to the oracle.
+void Precond::dist_sched_apply(const double *x, int64_t neg_from, double *y, const int *run,
+                               const double *piggy_src) {
+    Ctx &c = *ctx;
+    const bool pk = sep.tslot.n > 0;
+    FwdIn last;  // no separator (sep.nT == 0): the last round fused as on one GPU
+    const PackArgs fp1 = fwd_pack(x, neg_from, piggy_src);
+    const bool f1 = launch_sptrsv_fwd(c, dF, x, neg_from, w.p, run, nullptr, false, xs.p, &last, pk ? &fp1 : nullptr);
+    launch_sep_exchange(c, sep, w.p, x, neg_from, piggy_src, f1);
+    launch_sep_solve(c, sep, w.p + nsub, y, false, run, nullptr);
+    PackArgs bp;
+    if (hslot2s.n) bp.slot = hslot2s.p, bp.buf = sep.sbuf.p;
+    const bool b1 = launch_sptrsv_bwd(c, dF, w.p, nullptr, false, run, nullptr, nullptr, &last, hslot2s.n ? &bp : nullptr);
+    if (hslot2s.n && !b1) launch_pack_slots(c, hslot2s.p, nsub, w.p, sep.sbuf.p, run);
+    // solve 2: rank 0 sends the apply's own T inputs (the T rows' residual is formed from them)
+    const PackArgs fp2 = fwd_pack(x, neg_from, nullptr);
+    bool f2 = false;
+    FwdIn last2;
+    if (!(fused_resid && launch_sptrsv_fwd_resid(c, dF, dKpsl, xs.p, w.p, r.p, run, &last2, pk ? &fp2 : nullptr, &f2))) {
+        launch_spmv_resid_sched(c, dKpsl, nullptr, xs.p, 0, w.p, r.p, run);  // r = x - op.A*y (subtree rows)
+        f2 = launch_sptrsv_fwd(c, dF, r.p, N, r.p, run, nullptr, true, nullptr, &last2, pk ? &fp2 : nullptr);
+    }
+    launch_sep_exchange(c, sep, r.p, x, neg_from, nullptr, f2);
+    launch_sep_solve(c, sep, r.p + nsub, y, true, run, nullptr, nullptr, nullptr, tkr ? tkr_ptr.p : nullptr, tkr_col.p,
+                     tkr_val.p, w.p + nsub);
+    launch_sptrsv_bwd(c, dF, r.p, y, true, run, nullptr, w.p, &last2);  // y = P*(ys + dy)
 }
 
 void Precond::set_handle(bool on) {
@@ -648,6 +740,9 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
         launch_sptrsv_fwd(c, dF, x, neg_from, w.p, run, nullptr, false, xs.n ? xs.p : nullptr, &last);
         have_xs = xs.n > 0;
         launch_sptrsv_bwd(c, dF, w.p, nullptr, false, run, nullptr, nullptr, &last);
+    } else if (dist && dsched && steps1_forced()) {
+        dist_sched_apply(x, neg_from, y, run, piggy_src);
+        return;
     } else if (dist && tkr && steps1_forced()) {
         // distributed, one forced refinement step, no Kp halo exchange (Precond::tkr): y = LDL*x
         // packs the y values the T rows' residual needs into the separator payload; the local
@@ -707,13 +802,14 @@ double Precond::apply_bytes() const {
     const double bwd = 12 * l + 4 * (Nn + 1) + 16 * Nn + 4 * Nn + 8 * Nn + 8 * Nn;
     const double kp = 12 * (double)dKp.nnz + 4 * (Nn + 1) + 8 * Nn /*y*/ + 8 * Nn /*x*/ + 8 * Nn /*r*/;
     const int64_t steps = nitref > 0 ? (int64_t)nitref : 0;
-    if (steps && force_itref != 0 && sched_path() && !(residual_update != 0 && handle)) {
+    const DMat &Ks = dist ? dKpsl : dKps;  // distributed: the rank's subtree rows (dist_sched_apply)
+    if (steps && force_itref != 0 && (sched_path() || (dsched && steps1_forced())) && !(residual_update != 0 && handle)) {
         // schedule-order path: the first backward sweep keeps its solution (no perm, no
         // scatter); the residual gathers x through perm; the refinement forward sweeps read it
         // contiguously (no perm); each refinement backward sweep reads ys contiguously and only
         // the last scatters
         const double bwd_keep = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn;
-        const double kps = 12 * (double)dKps.nnz + 4 * (Nn + 1) + 8 * Nn /*y*/ +
+        const double kps = 12 * (double)Ks.nnz + 4 * (Nn + 1) + 8 * Nn /*y*/ +
                            (xs.n ? 8 * Nn /*xs*/ : 12 * Nn /*x(perm)*/) + 8 * Nn /*r*/;
         const double fwd_s = 12 * l - 2 * (double)dF.nnz16 + 4 * (Nn + 1) + 16 * Nn;
         const double bwd_acc = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn + 8 * Nn /*ys*/;

@@ -2062,14 +2062,14 @@ void reg_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, con
 
 void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *out) {
     const int64_t N = M.N;
+    const int64_t NW = std::max<int64_t>(std::max<int64_t>(N, M.nsub + M.sep.nT), 1);  // distributed work vectors
     reps = std::max(reps, 1);
     DBuf<double> x, y, z;
-    x.alloc(N), y.alloc(N), z.alloc(N);
-    CPK_HIP(hipMemsetAsync(y.p, 0, N * sizeof(double), c.stream));
-    launch_set_concat(c, x.p, nullptr, 0, N);  // zeros
-    std::vector<double> h(N);
-    for (int64_t i = 0; i < N; i++) h[i] = 1.0 + 1e-3 * (double)(i % 1000);
-    CPK_HIP(hipMemcpy(x.p, h.data(), N * sizeof(double), hipMemcpyHostToDevice));
+    x.alloc(NW), y.alloc(NW), z.alloc(NW);
+    CPK_HIP(hipMemsetAsync(y.p, 0, NW * sizeof(double), c.stream));
+    std::vector<double> h(NW);
+    for (int64_t i = 0; i < NW; i++) h[i] = 1.0 + 1e-3 * (double)(i % 1000);
+    CPK_HIP(hipMemcpy(x.p, h.data(), NW * sizeof(double), hipMemcpyHostToDevice));
     auto timeit = [&](const std::function<void()> &f) {
         f();  // warm
         CPK_HIP(hipEventRecord(c.ev0, c.stream));
@@ -2127,14 +2127,16 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
         out->fwd_bytes -= fl, out->bwd_bytes += fl;
     }
     out->fwd_resid_ms = out->fwd_resid_bytes = 0;
-    if (M.sched_path() && M.xs.n && M.fused_resid && launch_sptrsv_fwd_resid(c, M.dF, M.dKps, x.p, y.p, z.p, nullptr)) {
-        out->fwd_resid_ms = timeit([&]() {
-            launch_sptrsv_fwd_resid(c, M.dF, M.dKps, x.p, y.p, z.p, nullptr);
-        });
+    // the fused refinement input: one GPU on Kps, distributed (schedule order) on the rank's Kpsl
+    const DMat &Ks = M.dist ? M.dKpsl : M.dKps;
+    if ((M.sched_path() || M.dsched) && M.xs.n && M.fused_resid &&
+        launch_sptrsv_fwd_resid(c, M.dF, Ks, x.p, y.p, z.p, nullptr)) {
+        out->fwd_resid_ms = timeit([&]() { launch_sptrsv_fwd_resid(c, M.dF, Ks, x.p, y.p, z.p, nullptr); });
         // Kps, y, xs (the residual's reads) + the factor and w (the sweep's); r never goes to HBM
         // for round 0 (the tail rows' r write and read are < 1 % and not counted)
-        out->fwd_resid_bytes = 12.0 * M.dKps.nnz + 4.0 * (Nn + 1) + 8.0 * Nn /*y*/ + 8.0 * Nn /*xs*/ + 12.0 * l -
-                               2.0 * (double)M.dF.nnz16 + 4.0 * (Nn + 1) + 8.0 * Nn /*w*/;
+        const double Nr = (double)M.dF.N;
+        out->fwd_resid_bytes = 12.0 * Ks.nnz + 4.0 * (Nr + 1) + 8.0 * Nr /*y*/ + 8.0 * Nr /*xs*/ + 12.0 * l -
+                               2.0 * (double)M.dF.nnz16 + 4.0 * (Nr + 1) + 8.0 * Nr /*w*/;
     }
 }
 

@@ -81,13 +81,16 @@ def test_dist_apply_bitexact(name, P, props):
         assert np.all(d[:nl] < S["n"]) and np.all(d[nl:] >= S["n"])
 
 
-@pytest.mark.parametrize("P", [2, 3, 4])
+@pytest.mark.parametrize("P", [1, 2, 3, 4])
 @pytest.mark.parametrize("name", ["cvxqp1_m", "synthetic20k"])
 def test_dist_refinement_without_kp_halo(name, P):
     """One forced refinement step (the example options) without the Kp halo exchange: every
     rank's local rows read T's solution from its own separator solve, the T rows' residual is
-    formed after the refinement's separator exchange (engine option no_tkr restores the halo
-    exchange).  A sequence of applies, each bit for bit the oracle's and the halo path's."""
+    formed after the refinement's separator exchange.  Three paths: the default keeps the first
+    solve's solution in schedule order and fuses the subtree rows' residual into the refinement
+    solve's forward sweep (Precond::dist_sched_apply); engine option no_sched_resid runs the
+    residual as a local SpMV in the original order; no_tkr restores the Kp halo exchange.  A
+    sequence of applies, each bit for bit the oracle's on every path (P = 1: no separator)."""
     import cpkrylov_amd as cpk
     S = _system(name)
     rng = np.random.default_rng(41)
@@ -96,11 +99,17 @@ def test_dist_refinement_without_kp_halo(name, P):
     def work(ctx, r):
         M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
         M.nitref, M.force_itref = 1, True
-        return [M * z for z in zs], M.export_factors() if r == 0 else None, M.sep_info()["tkr"]
+        return [M * z for z in zs], M.export_factors() if r == 0 else None, M.sep_info()
 
-    for opts in (None, dict(no_tkr=True)):
+    for opts in (None, dict(no_fused_resid=True), dict(no_sched_resid=True), dict(no_tkr=True)):
         res = _run_ranks(P, work, opts)
-        assert all(t == (0 if opts else 1) for _, _, t in res), opts
+        for _, _, info in res:
+            sep = info["nT"] > 0
+            assert info["sched"] == (0 if opts and ("no_sched_resid" in opts or ("no_tkr" in opts and sep)) else 1), (opts, info)
+            assert info["tkr"] == (1 if sep and not (opts and "no_tkr" in opts) else 0), (opts, info)
+            if info["sched"]:
+                assert info["fused"] == (0 if opts and "no_fused_resid" in opts else 1), (opts, info)
+            assert sep == (P > 1)
         L, D, perm = res[0][1]
         Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=(L, D, perm))
         Mo.set(nitref=1.0, force_itref=1.0)
@@ -198,10 +207,18 @@ def test_rccl_one_rank_graph_capture():
     x1, s1, f1 = cpk.reg_cpkrylov(cpk.cpminres, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts)
     ctx = cpk.Context(device=0, rank=0, nranks=1, unique_id=cpk.get_unique_id())
     try:
+        assert ctx.info()["comm"] == "rccl" and ctx.info()["comm_ranks"] == 1
         x2, s2, f2 = cpk.reg_cpkrylov(cpk.cpminres, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts, ctx=ctx)
         assert s2["niters"] == s1["niters"] and f2 == f1
         assert np.array_equal(s2["residHistory"], s1["residHistory"])
         assert np.array_equal(x2, x1)
+        # the 1-rank apply runs the single-GPU kernel sequence (schedule order, fused residual)
+        info = s2["M"].sep_info()
+        assert info["sched"] == 1 and info["fused"] == 1 and info["nT"] == 0, info
+        z = np.random.default_rng(5).standard_normal(Pd["n"] + Pd["m"])
+        s2["M"].nitref, s1["M"].nitref = 1, 1
+        s2["M"].force_itref, s1["M"].force_itref = True, True
+        assert np.array_equal(s2["M"] * z, s1["M"] * z)
         del s2
     finally:
         ctx.close()
