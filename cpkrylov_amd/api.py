@@ -313,9 +313,10 @@ class opLDL2:
 
     def sep_info(self):
         """Diagnostic: the distributed separator solve's staging (cpk_pc_sep_info)."""
-        v = (C.c_int64 * 10)()
+        v = (C.c_int64 * 12)()
         check(lib.cpk_pc_sep_info(self.h, v))
-        return dict(zip(("dist", "nT", "nlev", "nrec", "lds", "lds_g", "kt", "tkr", "sched", "fused"), list(v)))
+        return dict(zip(("dist", "nT", "nlev", "nrec", "lds", "lds_g", "kt", "tkr", "sched", "fused", "tsweep",
+                         "tsweep_rounds"), list(v)))
 
     def sweep_info(self):
         """Diagnostic: the sweep schedule as launched (cpk_pc_sweep_info)."""

@@ -618,8 +618,9 @@ int cpk_pc_sep_info(cpk_pc M, int64_t *info) {
     need(M && info, "NULL argument");
     const Precond &p = *M->p;
     const DSep &T = p.sep;
-    const int64_t v[10] = {p.dist ? 1 : 0, T.nT, T.nlev, T.nrec, (int64_t)T.lds, (int64_t)T.lds_g, T.kt, p.tkr ? 1 : 0,
-                           p.dsched ? 1 : 0, (p.dsched && p.fused_resid && !p.dF.no_fused_resid) ? 1 : 0};
+    const int64_t v[12] = {p.dist ? 1 : 0, T.nT, T.nlev, T.nrec, (int64_t)T.lds, (int64_t)T.lds_g, T.kt, p.tkr ? 1 : 0,
+                           p.dsched ? 1 : 0, (p.dsched && p.fused_resid && !p.dF.no_fused_resid) ? 1 : 0,
+                           T.tsweep ? 1 : 0, T.tsweep ? (int64_t)T.tsw.round_ptr.size() - 1 : 0};
     std::memcpy(info, v, sizeof v);
     API_END
 }

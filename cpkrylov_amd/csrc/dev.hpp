@@ -105,6 +105,7 @@ struct EngineOpts {
     bool no_fused_resid = false;  // no_fused_resid:     refinement residual as its own SpMV
     int r0_xcd_chunk = 16;        // r0_xcd_chunk:       K > 0: runs of K consecutive round-0 blocks share an XCD
     bool tsolve_global = false;   // tsolve_global:      separator records read from HBM
+    bool tsolve_sweep = false;    // tsolve_sweep:       separator solved by the block sweeps (the path of a large T)
     bool no_piggy = false;        // no_piggy:           cpminres alpha by its own allreduce
     bool no_halo_merge = false;   // no_halo_merge:      cpminres beta by its own allreduce
     bool no_graph = false;        // no_graph:           no hipGraph capture of iterations
@@ -195,6 +196,7 @@ struct DFactor {
     // engine options of the preconditioner's context when it was built (launch-time paths)
     bool no_fused_resid = false;
     bool fuse_last = false;  // single GPU, no entries outside the factor: the last round fwd + bwd in one launch
+    bool skip0 = true;       // round 0's level-0 rows have no forward entries (false: a separator's T sweep)
     int64_t round0_rows = -1;  // round 0 is the rows [0, round0_rows) (-1: not a leading row range)
     std::vector<int32_t> hmeta;  // host copy of meta
     // round-0 blocks assigned to the persistent launch's workgroups by modelled cost (plan_round0),
@@ -404,8 +406,8 @@ constexpr int64_t kKrylovSpare = 2;
 struct DSep {
     int64_t nT = 0, kt = 0, nlev = 0, nsend = 0, ntdof = 0;
     int64_t kt_data = 0;  // payload values of the plan; [kt_data, kt) are the piggyback slots
-    DBuf<int32_t> tf_ptr, tf_col, tf_src, tb_ptr, tb_col, lev_ptr, lev_rows, send, tdof;
-    DBuf<double> tf_val, tb_val, DT, sbuf, rbuf;
+    DBuf<int32_t> tf_src, send, tdof;  // each T row's input position in the payload; tpack's rows; rank 0's T dofs
+    DBuf<double> DT, sbuf, rbuf;
     // stepped solve (tprefix_kernel + tsolve_steps_kernel): forward rows split into their
     // leading payload terms (tk_*) and the rest; the level solve is nsf forward and nsb backward
     // steps (steps[s] = waves | barrier flag) of records rec_v / rec_m (kernels.hip);
@@ -417,12 +419,23 @@ struct DSep {
     DBuf<uint32_t> rec_m;
     int64_t nsf = 0, nsb = 0, nrec = 0;
     size_t lds = 0;    // LDS bytes of the stepped solve with its records staged, 0 = too large
-    size_t lds_g = 0;  // LDS bytes with the records left in HBM; 0 (or no records): one-pass kernel
+    size_t lds_g = 0;  // LDS bytes with the records left in HBM; 0 (or no records): the T sweep
     bool tsolve_global = false;  // engine option at construction
+    // T sweep (dsep_sweep_setup): T's rows as a factor of their own, solved by the block sweep
+    // kernels over the combined vector rbuf = [payload (P * kt); T in T's schedule order] -- the
+    // separator solve of a T too large for one workgroup (no row or step limit)
+    bool tsweep = false;
+    int64_t tsw_base = 0;  // P * kt: where T's rows start in rbuf
+    DFactor tsw;
+    DBuf<int32_t> tsw_q;   // T row t -> its schedule position (rbuf[tsw_base + tsw_q[t]])
 };
 struct RankPlan;
 // Split the forward rows of T and build the steps of the separator level solve.
 void dsep_stage(DSep &T, const RankPlan &rp);
+// Build the T sweep: T's rows scheduled into blocks and rounds (build_schedule) and laid out as
+// a DFactor over the combined vector [payload (P * kt); T]; forced by the engine option
+// tsolve_sweep, else used when the stepped solve does not fit one workgroup.
+void dsep_sweep_setup(Ctx &c, DSep &T, const RankPlan &rp, int P);
 struct DofMap;
 
 struct Precond {

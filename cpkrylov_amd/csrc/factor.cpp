@@ -334,7 +334,7 @@ static void height_levels(const Factor &f, LdlSymbolic *sym) {
 }
 
 Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1, int64_t SUB0,
-                        const std::vector<int64_t> *extra_bwd) {
+                        const std::vector<int64_t> *extra_bwd, const std::vector<int64_t> *extra_fwd) {
     if (SUB0 <= 0 || SUB0 > CAP0) SUB0 = CAP0;
     const int64_t N = f.N;
     SubClock clk;
@@ -349,7 +349,8 @@ Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, i
     }, 1 << 18);
     parallel_for(N, [&](int64_t lo, int64_t hi) {
         for (int64_t v = lo; v < hi; v++)
-            ent[v] = (int32_t)std::max<int64_t>(nfwd[v], f.Lp[v + 1] - f.Lp[v] + (extra_bwd ? (*extra_bwd)[v] : 0));
+            ent[v] = (int32_t)std::max<int64_t>(nfwd[v] + (extra_fwd ? (*extra_fwd)[v] : 0),
+                                                f.Lp[v + 1] - f.Lp[v] + (extra_bwd ? (*extra_bwd)[v] : 0));
     });
     const int64_t u0 = std::max<int64_t>(1, CAP0 / std::max<int64_t>(R0, 1));
     const int64_t u1 = std::max<int64_t>(1, CAP1 / std::max<int64_t>(R1, 1));

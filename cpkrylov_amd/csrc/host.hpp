@@ -139,9 +139,10 @@ struct Schedule {
 // Round 0 peels subtrees of weight <= SUB0 (default CAP0) and packs them into blocks of CAP0:
 // a block's level count is that of its tallest subtree, so packing several short subtrees
 // per block cuts the barrier-separated level passes per row.
-// extra_bwd[v]: backward entries of row v outside the factor (distributed separators)
+// extra_bwd[v] / extra_fwd[v]: backward / forward entries of row v outside the factor (the
+// distributed separators' backward terms into T; T's own forward terms on the exchanged payload)
 Schedule build_schedule(const Factor &f, int64_t R0, int64_t CAP0, int64_t R1, int64_t CAP1, int64_t SUB0 = 0,
-                        const std::vector<int64_t> *extra_bwd = nullptr);
+                        const std::vector<int64_t> *extra_bwd = nullptr, const std::vector<int64_t> *extra_fwd = nullptr);
 // Apply the schedule's relabel to the factor (values unchanged, exact data movement).
 // src (optional): src[t] = index into f.Li / f.Lx of the relabelled factor's entry t.
 Factor relabel(const Factor &f, const Schedule &s, std::vector<int32_t> *src = nullptr);

@@ -453,57 +453,15 @@ void launch_spmv_resid_norm(Ctx &c, const DMat &A, const double *xin, int64_t ne
 }
 
 // ---- separator solve of the distributed apply ----------------------------
-// One workgroup solves the (replicated) separator rows T: forward by levels from the
-// allgathered payload (subtree values of every rank + the T inputs published by rank 0), then
-// backward by levels in reverse, all out of LDS.  Each row subtracts its terms in the exported
-// factor's order, exactly as the single-GPU sweep does.  The results go to w[nsub + t] (read
-// by the local backward sweep as outside-block values) and, on rank 0, to the T dofs of y.
-__global__ __launch_bounds__(256) void tsolve_kernel(
-    int nlev, int nT, const int32_t *__restrict__ lev_ptr, const int32_t *__restrict__ lev_rows,
-    const int32_t *__restrict__ tf_ptr, const int32_t *__restrict__ tf_col, const double *__restrict__ tf_val,
-    const int32_t *__restrict__ tf_src, const int32_t *__restrict__ tb_ptr, const int32_t *__restrict__ tb_col,
-    const double *__restrict__ tb_val, const double *__restrict__ DT, const double *__restrict__ rbuf,
-    const int32_t *__restrict__ tdof, int ntdof, double *wT, double *y, int add, const int *run, const int *active,
-    const int32_t *__restrict__ hslot, double *hbuf) {
-    extern __shared__ double wt[];
-    if (skip(run, active)) return;
-    const int tid = threadIdx.x;
-    for (int l = 0; l < nlev; l++) {
-        for (int q = lev_ptr[l] + tid; q < lev_ptr[l + 1]; q += blockDim.x) {
-            const int t = lev_rows[q];
-            double acc = rbuf[tf_src[t]];
-            for (int e = tf_ptr[t]; e < tf_ptr[t + 1]; e++) {
-                const int c = tf_col[e];
-                const double xv = c >= 0 ? rbuf[c] : wt[-c - 1];
-                acc -= tf_val[e] * xv;
-            }
-            wt[t] = acc;
-        }
-        __syncthreads();
-    }
-    for (int l = nlev - 1; l >= 0; l--) {
-        for (int q = lev_ptr[l] + tid; q < lev_ptr[l + 1]; q += blockDim.x) {
-            const int t = lev_rows[q];
-            double acc = wt[t] / DT[t];
-            for (int e = tb_ptr[t]; e < tb_ptr[t + 1]; e++) acc -= tb_val[e] * wt[tb_col[e]];
-            wt[t] = acc;
-        }
-        __syncthreads();
-    }
-    for (int t = tid; t < nT; t += blockDim.x) {
-        wT[t] = wt[t];
-        if (t < ntdof) {
-            const int32_t d = tdof[t];
-            const double o = add ? y[d] + wt[t] : wt[t];
-            y[d] = o;
-            if (hslot && hslot[d] >= 0) hbuf[hslot[d]] = o;  // the Kp halo of y (PackArgs)
-        }
-    }
-}
-
-// Stepped separator solve: the same arithmetic in the same order, restructured for latency.
-// The one-pass kernel above walks each term with two dependent global loads; at S10 / 8 ranks
-// T has 593 rows, 13 levels and rows of up to 49 payload terms, and it took ~160 us.  Here:
+// Every rank solves the (replicated) separator rows T redundantly: forward from the allgathered
+// payload (subtree values of every rank + the T inputs published by rank 0), then backward, each
+// row subtracting its terms in the exported factor's order, exactly as the single-GPU sweep does.
+// The results go to wT = w[nsub + t] (read by the local backward sweep as outside-block values)
+// and, on rank 0, to the T dofs of y.  Two paths: the stepped solve of one workgroup below
+// (T fits its LDS and step table), and the T sweep (dsep_sweep_setup) for any other T.
+// Stepped separator solve, restructured for latency.  A one-pass kernel (r01-r03) walked each
+// term with two dependent global loads; at S10 / 8 ranks T has 593 rows, 13 levels and rows of up
+// to 49 payload terms, and it took ~160 us.  Here:
 //  (1) tprefix_kernel, one wave per row across the chip: each forward row subtracts its LEADING
 //      payload terms (coalesced loads, one gather, the subtractions in order on one lane) into
 //      pre[t], and the payload terms of the rest of the row are pre-multiplied into their
@@ -852,6 +810,98 @@ void dsep_stage(DSep &T, const RankPlan &rp) {
     T.lds_g = 8 * (size_t)((nT + 2) & ~1) <= kTsolveMaxLds ? 8 * (size_t)((nT + 2) & ~1) : 0;
 }
 
+// The T sweep.  T's rows are a factor of their own: L_T's columns are the backward rows tb_*
+// (the rows below t, in T's pivot order), so its elimination tree is parent(t) = min tb_col,
+// and build_schedule cuts it into blocks and rounds like a rank's subtrees, with each row's
+// payload terms as extra forward entries.  The layout is a DFactor over the combined vector
+// rbuf = [payload of every rank (P * kt); T rows in schedule order]: a forward entry on payload
+// position p reads rbuf[p] (outside every block: pre-multiplied at staging, as any reference to
+// an earlier round), one on T row t' reads rbuf[base + q(t')], a T row's input is rbuf[tf_src[t]]
+// (perm), and the backward rows read the T region only.  Each row keeps tf_* / tb_* order -- the
+// exported factor's -- so the block kernels give the stepped solve's bits; nothing limits T's
+// size or its number of levels.
+void dsep_sweep_setup(Ctx &c, DSep &T, const RankPlan &rp, int P) {
+    const int64_t nT = T.nT, base = (int64_t)P * T.kt, NT = base + nT;
+    T.tsweep = false;
+    if (nT <= 0) return;
+    if (NT > (int64_t)INT32_MAX / 2) throw Error(CPK_ERR_UNSUPPORTED, "separator payload too large");
+    // L_T (CSC: column t holds the rows below it) and the etree
+    Factor f;
+    f.N = nT;
+    f.Lp.assign((size_t)nT + 1, 0);
+    f.parent.assign((size_t)nT, -1);
+    std::vector<int64_t> xf((size_t)nT, 0);
+    for (int64_t t = 0; t < nT; t++) {
+        for (int64_t e = rp.tb_ptr[t]; e < rp.tb_ptr[t + 1]; e++) {
+            const int32_t i = rp.tb_col[e];
+            f.Li.push_back(i);
+            if (f.parent[t] < 0 || i < f.parent[t]) f.parent[t] = i;
+        }
+        f.Lp[t + 1] = (int64_t)f.Li.size();
+        for (int64_t e = rp.tf_ptr[t]; e < rp.tf_ptr[t + 1]; e++) xf[t] += rp.tf_col[e] >= 0;
+    }
+    const SweepConfig sw = dist_sweep_default();
+    Schedule S = build_schedule(f, sw.rows[0], sw.cap[0], sw.rows[1], sw.cap[1], sw.sub0, nullptr, &xf);
+    std::vector<int32_t> q((size_t)nT);
+    for (int64_t k = 0; k < nT; k++) q[S.order[k]] = (int32_t)k;
+    DFactor &d = T.tsw;
+    for (int i = 0; i < 2; i++) d.sweep_rows[i] = sw.rows[i], d.sweep_cap[i] = sw.cap[i], d.sweep_threads[i] = sw.threads[i];
+    d.pipelined = true, d.no_upper = false, d.no_col16 = true, d.fuse_last = false, d.skip0 = false;
+    d.N = NT;
+    std::vector<uint32_t> fptr((size_t)NT + 1, 0), bptr((size_t)NT + 1, 0);
+    std::vector<int32_t> fcol, bcol, perm((size_t)NT, 0);
+    std::vector<double> fval, bval, D((size_t)NT, 0.0);  // payload rows: never solved
+    for (int64_t k = 0; k < nT; k++) {  // rows in schedule order
+        const int32_t t = S.order[k];
+        for (int64_t e = rp.tf_ptr[t]; e < rp.tf_ptr[t + 1]; e++) {
+            const int32_t cc = rp.tf_col[e];
+            fcol.push_back(cc >= 0 ? cc : (int32_t)(base + q[(size_t)(-cc - 1)]));
+            fval.push_back(rp.tf_val[e]);
+        }
+        for (int64_t e = rp.tb_ptr[t]; e < rp.tb_ptr[t + 1]; e++) {
+            bcol.push_back((int32_t)(base + q[(size_t)rp.tb_col[e]]));
+            bval.push_back(rp.tb_val[e]);
+        }
+        fptr[base + k + 1] = (uint32_t)fcol.size();
+        bptr[base + k + 1] = (uint32_t)bcol.size();
+        perm[base + k] = rp.tf_src[t];
+        D[base + k] = rp.DT[t];
+    }
+    for (int64_t r = 0; r < base; r++) fptr[r + 1] = 0, bptr[r + 1] = 0;  // payload rows: no entries
+    d.nnz = (int64_t)fcol.size();
+    fcol.resize(fcol.size() + kFactorPadEntries, 0), bcol.resize(bcol.size() + kFactorPadEntries, (int32_t)base);
+    fval.resize(fval.size() + kFactorPadEntries, 0.0), bval.resize(bval.size() + kFactorPadEntries, 0.0);
+    d.nblk = (int64_t)S.blk_row.size() - 1;
+    d.nlvl = (int64_t)S.lvl_row.size() - 1;
+    std::vector<int32_t> bl(S.blk_lvl.begin(), S.blk_lvl.end()), lr(S.lvl_row.size());
+    for (size_t i = 0; i < lr.size(); i++) lr[i] = (int32_t)(base + S.lvl_row[i]);
+    std::vector<int32_t> meta((size_t)d.nblk * 8);
+    d.round_fits.assign(S.round_ptr.size() - 1, 1);
+    for (int64_t b = 0; b < d.nblk; b++) {
+        const int64_t r0 = base + S.lvl_row[S.blk_lvl[b]], r1 = base + S.lvl_row[S.blk_lvl[b + 1]];
+        int32_t *m = &meta[(size_t)b * 8];
+        m[0] = (int32_t)r0, m[1] = (int32_t)r1, m[2] = (int32_t)S.blk_lvl[b], m[3] = (int32_t)S.blk_lvl[b + 1];
+        m[4] = (int32_t)fptr[r0], m[5] = (int32_t)fptr[r1], m[6] = (int32_t)bptr[r0], m[7] = (int32_t)bptr[r1];
+    }
+    for (size_t r = 0; r < d.round_fits.size(); r++)
+        for (int64_t b = S.round_ptr[r]; b < S.round_ptr[r + 1]; b++) {
+            const int32_t *m = &meta[(size_t)b * 8];
+            if (m[1] - m[0] > d.sweep_rows[1] || m[5] - m[4] > d.sweep_cap[1] || m[7] - m[6] > d.sweep_cap[1])
+                d.round_fits[r] = 0;
+        }
+    d.fptr.upload(fptr), d.fcol.upload(fcol), d.fval.upload(fval);
+    d.bptr.upload(bptr), d.bcol.upload(bcol), d.bval.upload(bval);
+    d.D.upload(D), d.perm.upload(perm);
+    d.blk_lvl.upload(bl), d.lvl_row.upload(lr), d.meta.upload(meta);
+    d.hmeta = meta;
+    d.round_ptr = S.round_ptr;
+    d.round0_rows = -1;
+    plan_round0(c, d, nullptr);
+    T.tsw_q.upload(q);
+    T.tsw_base = base;
+    T.tsweep = true;
+}
+
 // payload: w of this rank's rows that separator rows read, then (rank 0) the T inputs +-x[tdof]
 // (and, with piggy, kSepPiggy values of a solver's into the spare slots [kt_data, kt))
 __global__ void tpack_kernel(const double *__restrict__ w, const int32_t *__restrict__ send, int nsend,
@@ -901,6 +951,23 @@ void launch_tkr_resid(Ctx &c, const DSep &S, const int32_t *ptr, const int32_t *
     CPK_HIP(hipGetLastError());
 }
 
+// the T sweep's epilogue: wT in T order, rank 0's T dofs of y (and their Kp halo slots)
+__global__ void tsep_out_kernel(int nT, const int32_t *__restrict__ q, const double *__restrict__ wsw,
+                                const int32_t *__restrict__ tdof, int ntdof, double *wT, double *y, int add,
+                                const int *run, const int *active, const int32_t *__restrict__ hslot, double *hbuf) {
+    if (skip(run, active)) return;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nT; t += gridDim.x * blockDim.x) {
+        const double v = wsw[q[t]];
+        wT[t] = v;
+        if (t < ntdof) {
+            const int32_t d = tdof[t];
+            const double o = add ? y[d] + v : v;
+            y[d] = o;
+            if (hslot && hslot[d] >= 0) hbuf[hslot[d]] = o;
+        }
+    }
+}
+
 void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active,
                       const int32_t *hslot, double *hbuf, const int32_t *tkr_ptr, const int32_t *tkr_col,
                       const double *tkr_val, const double *tkr_yT) {
@@ -916,7 +983,7 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
     const bool grec = S.tsolve_global || !fits(S.lds);  // engine option: records in HBM
     const size_t lds = grec ? S.lds_g : S.lds;
     const TkrArgs tkr{tkr_ptr, tkr_col, tkr_val, tkr_yT};  // y's T values (wT itself: this solve writes it last)
-    if (S.nrec > 0 && fits(lds)) {
+    if (!S.tsweep && S.nrec > 0 && fits(lds)) {
         hipLaunchKernelGGL(tprefix_kernel, dim3((unsigned)((S.nT + 3) / 4)), dim3(256), 0, c.stream, (int)S.nT,
                            S.tk_ptr.p, S.tk_col.p, S.tk_val.p, S.tr_ptr.p, S.tr_col.p, S.tr_val.p, S.tr_slot.p,
                            S.tf_src.p, S.rbuf.p, S.pre.p, S.rec_v.p, run, active, tkr);
@@ -933,11 +1000,16 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
         CPK_HIP(hipGetLastError());
         return;
     }
-    if (tkr_ptr) launch_tkr_resid(c, S, tkr_ptr, tkr_col, tkr_val, tkr_yT, run, active);  // the one-pass kernel reads rbuf
-    hipLaunchKernelGGL(tsolve_kernel, dim3(1), dim3(256), (size_t)S.nT * sizeof(double), c.stream, (int)S.nlev,
-                       (int)S.nT, S.lev_ptr.p, S.lev_rows.p, S.tf_ptr.p, S.tf_col.p, S.tf_val.p, S.tf_src.p,
-                       S.tb_ptr.p, S.tb_col.p, S.tb_val.p, S.DT.p, S.rbuf.p, S.tdof.p, (int)S.ntdof, wT, y,
-                       add ? 1 : 0, run, active, hslot, hbuf);
+    if (!S.tsweep) throw Error(CPK_ERR_UNSUPPORTED, "internal: separator solve without a path");
+    // the T sweep: [payload; T] in rbuf; forward (input rbuf[tf_src[t]], the T rows' residual
+    // formed first when tkr), backward, then wT and rank 0's T dofs
+    if (tkr_ptr) launch_tkr_resid(c, S, tkr_ptr, tkr_col, tkr_val, tkr_yT, run, active);
+    launch_sptrsv_fwd(c, S.tsw, S.rbuf.p, INT64_MAX, S.rbuf.p, run, active);
+    launch_sptrsv_bwd(c, S.tsw, S.rbuf.p, nullptr, false, run, active);
+    const int grid = (int)std::min<int64_t>((S.nT + 255) / 256, 1024);
+    hipLaunchKernelGGL(tsep_out_kernel, dim3(grid), dim3(256), 0, c.stream, (int)S.nT, S.tsw_q.p,
+                       (const double *)(S.rbuf.p + S.tsw_base), S.tdof.p, (int)S.ntdof, wT, y, add ? 1 : 0, run, active,
+                       hslot, hbuf);
     CPK_HIP(hipGetLastError());
 }
 
@@ -2049,27 +2121,27 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
     if (ra)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true, kRes>), dim3((unsigned)grid),
                            blk, lds, c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p,
-                           F.D.p, F.perm.p, xin, neg_from, w, out, run, active, 1, ys, 1, xs,
+                           F.D.p, F.perm.p, xin, neg_from, w, out, run, active, 1, ys, F.skip0 ? 1 : 0, xs,
                            (const int16_t *)F.fcol16.p, *ra, am, ap, pk ? *pk : PackArgs{});
     else if (loc)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true>), dim3((unsigned)grid), blk,
                            lds, c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, 1, xs,
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.skip0 ? 1 : 0, xs,
                            (const int16_t *)F.fcol16.p, ResArgs{}, am, ap, pk ? *pk : PackArgs{});
     else if (!bwd)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, 1, xs,
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.skip0 ? 1 : 0, xs,
                            (const int16_t *)nullptr, ResArgs{}, am, ap, pk ? *pk : PackArgs{});
     else if (add)
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, true, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, 1, xs,
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.skip0 ? 1 : 0, xs,
                            (const int16_t *)nullptr, ResArgs{}, am, ap, pk ? *pk : PackArgs{});
     else
         hipLaunchKernelGGL((sptrsv_pipe_kernel<TPB, RPT, EPT, true, false, SPLIT>), dim3((unsigned)grid), blk, lds,
                            c.stream, F.round_ptr[0], nb, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, 1, xs,
+                           F.perm.p, xin, neg_from, w, out, run, active, sched_in, ys, F.skip0 ? 1 : 0, xs,
                            (const int16_t *)nullptr, ResArgs{}, am, ap, pk ? *pk : PackArgs{});
     return true;
 }
@@ -2207,7 +2279,7 @@ static void fwd_round(Ctx &c, const DFactor &F, int64_t r, const double *xin, in
     if (!nb) return;
     hipLaunchKernelGGL((sptrsv_fwd_kernel<TPB>), dim3((unsigned)nb), dim3(TPB),
                        sweep_lds_bytes(F.sweep_rows[i], F.sweep_cap[i]), c.stream, b0, F.sweep_rows[i],
-                       F.sweep_cap[i], r == 0 ? 1 : 0, F.blk_lvl.p, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.perm.p,
+                       F.sweep_cap[i], (r == 0 && F.skip0) ? 1 : 0, F.blk_lvl.p, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.perm.p,
                        xin, neg_from, w, run, active, sched_in, xs);
 }
 

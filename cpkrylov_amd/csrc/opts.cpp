@@ -59,6 +59,7 @@ const BoolOpt kBool[] = {
     {"no_sched_resid", &EngineOpts::no_sched_resid},
     {"no_fused_resid", &EngineOpts::no_fused_resid},
     {"tsolve_global", &EngineOpts::tsolve_global},
+    {"tsolve_sweep", &EngineOpts::tsolve_sweep},
     {"no_piggy", &EngineOpts::no_piggy},
     {"no_halo_merge", &EngineOpts::no_halo_merge},
     {"no_graph", &EngineOpts::no_graph},

@@ -251,8 +251,6 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     sub.lap("dist: dof map + rank plan");
     pc->n = dm->n_loc[c.rank], pc->m = dm->m_loc[c.rank], pc->N = pc->n + pc->m;
     pc->nsub = rp.nsub;
-    if (rp.nT * (int64_t)sizeof(double) > 64 * 1024)
-        throw Error(CPK_ERR_UNSUPPORTED, "separator set too large for the one-workgroup separator solve");
     // local sweeps: schedule + relabel of this rank's subtrees, rows summed in exported order
     std::vector<int64_t> nextra(rp.nsub);
     for (int64_t j = 0; j < rp.nsub; j++) nextra[j] = (int64_t)rp.extra[j].size();
@@ -432,15 +430,13 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     T.tsolve_global = c.opts.tsolve_global;
     T.kt_data = kt1 > 0 ? kt1 - kSepPiggy : 0;
     if (pc->tkr) pc->hslot2.upload(hslot2), pc->tkr_ptr.upload(tkr_ptr), pc->tkr_col.upload(tkr_col), pc->tkr_val.upload(tkr_val);
-    auto i32 = [](const std::vector<int64_t> &v) { return std::vector<int32_t>(v.begin(), v.end()); };
-    T.tf_ptr.upload(i32(rp.tf_ptr)), T.tf_col.upload(rp.tf_col), T.tf_val.upload(rp.tf_val);
-    T.tf_src.upload(rp.tf_src), T.tb_ptr.upload(i32(rp.tb_ptr)), T.tb_col.upload(rp.tb_col);
-    T.tb_val.upload(rp.tb_val), T.DT.upload(rp.DT), T.lev_ptr.upload(rp.tlev_ptr), T.lev_rows.upload(rp.tlev_rows);
-    T.tdof.upload(rp.tdof);
+    T.tf_src.upload(rp.tf_src), T.DT.upload(rp.DT), T.tdof.upload(rp.tdof);
     dsep_stage(T, rp);
+    // a T the stepped solve cannot hold (LDS, step table) goes through the block sweeps
+    if (T.nT > 0 && (c.opts.tsolve_sweep || T.nrec == 0 || (T.lds == 0 && T.lds_g == 0))) dsep_sweep_setup(c, T, rp, c.nranks);
     T.sbuf.alloc((size_t)std::max<int64_t>(T.kt, 1));
     T.sbuf.zero(c.stream);
-    T.rbuf.alloc((size_t)std::max<int64_t>(T.kt * c.nranks, 1));
+    T.rbuf.alloc((size_t)std::max<int64_t>(T.kt * c.nranks + (T.tsweep ? T.nT : 0), 1));
     sub.lap("dist: separator solve data");
     // refinement residual rows of Kp with their halo
     std::vector<int32_t> kp_send;
@@ -483,7 +479,8 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
             pc->vmaps.push_back(std::move(m));
         };
         add(pc->dF.fval, 0), add(pc->dF.bval, 0), add(pc->dF.D, 1);
-        add(T.tf_val, 0), add(T.tb_val, 0), add(T.DT, 1), add(T.tk_val, 0), add(T.tr_val, 0), add(T.rec_v, 0);
+        add(T.DT, 1), add(T.tk_val, 0), add(T.tr_val, 0), add(T.rec_v, 0);
+        add(T.tsw.fval, 0), add(T.tsw.bval, 0), add(T.tsw.D, 1);
         add(pc->dKp.val, 2);
         add(pc->dKpl.val, 2), add(pc->tkr_val, 2), add(pc->dKpsl.val, 2);
         dldl_setup(pc->dl, an.sym, an.F0, {}, {}, {});

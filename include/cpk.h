@@ -201,10 +201,11 @@ int cpk_pc_get_info(cpk_pc M, cpk_pc_info *info);
 /* Local slice of a (distributed) preconditioner: n_loc x-part and m_loc y-part dofs; dofs[i] =
  * global index of local entry i (n_loc + m_loc entries).  One GPU: the identity. */
 /* Diagnostic (not in the reference): the separator solve of a distributed preconditioner,
- * info[10] = {distributed, separator rows, levels, step records, LDS bytes with the records
+ * info[12] = {distributed, separator rows, levels, step records, LDS bytes with the records
  * staged (0: they do not fit), LDS bytes with the records left in HBM, payload per rank,
  * refinement residual without the Kp halo exchange, refinement in schedule order, its residual
- * fused into the forward sweep}. */
+ * fused into the forward sweep, separator solved by the block sweeps (T sweep), the T sweep's
+ * rounds}. */
 int cpk_pc_sep_info(cpk_pc M, int64_t *info);
 /* Diagnostic (not in the reference): the sweep schedule as launched, info[8] = {rounds, round-0
  * blocks, blocks above round 0, grid of the cost-balanced round-0 assignment of the forward /

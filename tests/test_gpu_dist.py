@@ -304,11 +304,12 @@ def test_dist_minres_fused_update_bitexact(P):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["tsolve_global"])
+@pytest.mark.parametrize("path", ["tsolve_global", "tsolve_sweep"])
 @pytest.mark.parametrize("P", [2, 4])
 def test_dist_apply_separator_fallbacks_bitexact(P, path):
-    """The separator solve's fallback (records left in HBM for a separator too large for LDS)
-    gives the same bits as the staged solve and the oracle."""
+    """The separator solve's other paths -- records left in HBM (a separator too large for LDS),
+    and T solved by the block sweeps (the path of a T no workgroup holds) -- give the same bits
+    as the staged solve and the oracle."""
     import cpkrylov_amd as cpk
     S = _system("synthetic20k")
     z = np.random.default_rng(7).standard_normal(S["n"] + S["m"])
@@ -324,6 +325,38 @@ def test_dist_apply_separator_fallbacks_bitexact(P, path):
     Mo.set(nitref=1.0, force_itref=1.0)
     yo = Mo @ z
     for y, _ in res:
+        assert np.array_equal(y, yo), np.max(np.abs(y - yo))
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_dist_apply_large_separator_bitexact(P):
+    """A separator larger than one workgroup can hold: S10's generator at 1M dofs with SURVEY
+    8d's +-64 coupling window and a tight split tolerance gives |T| = 10 000 rows (> 8192, the
+    old one-workgroup cap, and more steps than the stepped solve's table), so T is solved by the
+    block sweeps (dsep_sweep_setup).  Every rank's M*z -- plain, and with the forced refinement
+    step in schedule order -- equals the oracle's bit for bit."""
+    import cpkrylov_amd as cpk
+    S = saddle_system(N=1_000_000, window=64, seed=21)
+    z = np.random.default_rng(13).standard_normal(S["n"] + S["m"])
+
+    def work(ctx, r):
+        M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+        M.nitref = 0
+        y0 = M * z
+        M.nitref, M.force_itref = 1, True
+        return y0, M * z, M.sep_info(), M.export_factors() if r == 0 else None
+
+    res = _run_ranks(P, work, {"split_tol": "0.0005"})
+    info = res[0][2]
+    assert info["nT"] > 8192 and info["tsweep"] == 1 and info["sched"] == 1, info
+    L, D, perm = res[0][3]
+    Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=(L, D, perm))
+    Mo.set(nitref=0.0)
+    y0o = Mo @ z
+    Mo.set(nitref=1.0, force_itref=1.0)
+    yo = Mo @ z
+    for y0, y, _, _ in res:
+        assert np.array_equal(y0, y0o), np.max(np.abs(y0 - y0o))
         assert np.array_equal(y, yo), np.max(np.abs(y - yo))
 
 
