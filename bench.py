@@ -52,6 +52,8 @@ def parse(argv=None):
                     help="s10: symmetric 10M cpminres (the headline metric); s50: nonsymmetric 3x3-block "
                          "50M cpdqgmres(40) (SURVEY.md section 8d config 5)")
     ap.add_argument("--size", type=int, default=None, help="total dofs N (default 10M for s10, 50M for s50)")
+    ap.add_argument("--window", type=int, default=4,
+                    help="s10: the B coupling window (+-W columns; SURVEY.md 8d sketches 64, the headline system uses 4)")
     ap.add_argument("--method", default=None)
     ap.add_argument("--itmax", type=int, default=None, help="s50: iterations per step (default 120)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample")
@@ -154,7 +156,7 @@ def main(argv=None):
     from cpkrylov_amd.synthetic import nonsym_system, saddle_system
 
     t_setup = time.perf_counter()
-    S = nonsym_system(N=args.size) if args.config == "s50" else saddle_system(N=args.size)
+    S = nonsym_system(N=args.size) if args.config == "s50" else saddle_system(N=args.size, window=args.window)
     n, m, N = S["n"], S["m"], S["N"]
     # N > 1 (or --dist): one distributed solve over all ranks (strong scaling), RCCL collectives
     # and halo exchanges inside the solver; every rank holds its row block
@@ -301,8 +303,9 @@ def main(argv=None):
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": (f"S10 synthetic symmetric saddle-point system, cp{args.method} to convergence "
-                                    "(cpk_exprog1 options), step = one method call" if args.config == "s10" else
+            "config": {"workload": (f"S10 synthetic symmetric saddle-point system{'' if args.window == 4 else f' (B window +-{args.window})'}, "
+                                    f"cp{args.method} to convergence (cpk_exprog1 options), step = one method call"
+                                    if args.config == "s10" else
                                     f"S50 synthetic nonsymmetric 3x3-block saddle-point system, cp{args.method}"
                                     f"(mem 40), step = one method call TRUNCATED at {args.opts['itmax']} iterations "
                                     "(cpk_exprog1 tolerances; convergence takes 611-1039 iterations, rounding-"
@@ -312,7 +315,7 @@ def main(argv=None):
                        "parallelism": f"rowblock{world}" if distributed else "single",
                        "rccl_ranks": cinfo["comm_ranks"] if cinfo["comm"] == "rccl" else 0,
                        "sweep": ctx.get_option("sweep"),
-                       "seed": S["seed"],
+                       "seed": S["seed"], "window": S["window"],
                        "rows_local_rank0": N_loc,
                        **({"rhs_perturb": args.rhs_perturb, "perturb_seed": args.perturb_seed}
                           if args.rhs_perturb else {})},
@@ -438,7 +441,7 @@ def pmc_probe(args):
     import cpkrylov_amd as cpk
     from cpkrylov_amd import _lib
     from cpkrylov_amd.synthetic import nonsym_system, saddle_system
-    S = nonsym_system(N=args.size) if args.config == "s50" else saddle_system(N=args.size)
+    S = nonsym_system(N=args.size) if args.config == "s50" else saddle_system(N=args.size, window=args.window)
     ctx = cpk.Context(device=0)
     A, Cm = cpk.Matrix(S["Q"], ctx), cpk.Matrix(S["C"], ctx)
     M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
@@ -470,7 +473,8 @@ def pmc_traffic(args):
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(tmp, ctr)
             cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
-                   sys.executable, os.path.abspath(__file__), "--pmc-probe", "--size", str(args.size)]
+                   sys.executable, os.path.abspath(__file__), "--pmc-probe", "--size", str(args.size),
+                   "--window", str(args.window)]
             try:
                 r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
             except subprocess.TimeoutExpired:
