@@ -12,7 +12,7 @@ S = saddle_system(int(os.environ.get("N", "10000000")))
 ctx = cpk.Context(device=0)
 A, Cm = cpk.Matrix(S["Q"], ctx), cpk.Matrix(S["C"], ctx)
 for cfg in sys.argv[1:]:
-    os.environ["CPK_SWEEP"] = cfg
+    ctx.set_option("sweep", cfg)  # engine options live in the context (read when M is built)
     M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
     M.nitref, M.force_itref = 1, True
     p = _lib.Profile()
