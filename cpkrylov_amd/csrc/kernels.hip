@@ -1161,11 +1161,7 @@ __device__ __forceinline__ void sweep_levels(SweepLds &S, int nl, bool skip_firs
 #ifndef CPK_LEVEL_OWN
 #define CPK_LEVEL_OWN 2
 #endif
-// CPK_LEVEL_PIPE (A/B builds): 1 the one-wave round-0 level loops load a level's static operands
-// while the previous level runs (levels_grouped_fwd, levels_owned_bwd_pipe), 0 they do not
-#ifndef CPK_LEVEL_PIPE
-#define CPK_LEVEL_PIPE 1
-#endif
+
 template <int TPB, int RPT, bool BWD, int CH>
 __device__ __forceinline__ void levels_owned(SweepLds &S, int nl, int nr, bool skip_first, int tid) {
     static_assert(CH <= kSweepPad, "chunk wider than the padding");
@@ -1203,83 +1199,6 @@ __device__ __forceinline__ void levels_owned(SweepLds &S, int nl, int nr, bool s
         }
         if (CPK_LEVEL_OWN >= 2 && TPB == kWave) asm volatile("" ::: "memory");
         else __syncthreads();
-    }
-}
-
-// The backward levels_owned of a one-wave block, pipelined (CPK_LEVEL_PIPE): the level bounds sit
-// in a register (readlane), and the first entry chunk of the lane's next row to solve -- its
-// rows are solved from the highest down, one level at a time -- is loaded while the current row
-// gathers and subtracts.  A row costs its gathers, its chain and its store.  Rows of one level
-// are independent, so taking a lane's rows of a level highest first changes nothing: each row
-// subtracts its terms in the same order, bit for bit.
-template <int RPT, int CH>
-__device__ __forceinline__ void levels_owned_bwd_pipe(SweepLds &S, int nl, int nr, int lane) {
-    static_assert(CH <= kSweepPad, "chunk wider than the padding");
-    uint32_t pe[RPT];
-    double acc[RPT];
-#pragma unroll
-    for (int j = 0; j < RPT; j++) {
-        const int k = lane + j * kWave;
-        pe[j] = 0u, acc[j] = 0.0;
-        if (k < nr) pe[j] = (uint32_t)(uint16_t)S.p[k] | ((uint32_t)(uint16_t)S.p[k + 1] << 16), acc[j] = S.w[k];
-    }
-    const int lvr = lane <= nl ? (int)S.lv[lane] : 0;
-    int jn = -1;  // the lane's next row to solve: the highest owned one
-#pragma unroll
-    for (int j = 0; j < RPT; j++)
-        if (lane + j * kWave < nr) jn = j;
-    auto pe_of = [&](int j) {
-        uint32_t r = pe[0];
-#pragma unroll
-        for (int i = 1; i < RPT; i++) r = j == i ? pe[i] : r;
-        return r;
-    };
-    auto acc_of = [&](int j) {
-        double r = acc[0];
-#pragma unroll
-        for (int i = 1; i < RPT; i++) r = j == i ? acc[i] : r;
-        return r;
-    };
-    int pc[CH];
-    double pv[CH];
-    {
-        const int e0 = jn >= 0 ? (int)(pe_of(jn) & 0xffffu) : 0;
-#pragma unroll
-        for (int i = 0; i < CH; i++) pc[i] = S.c[e0 + i], pv[i] = S.v[e0 + i];
-    }
-    for (int l = nl - 1; l >= 0; l--) {
-        const int a = __builtin_amdgcn_readlane(lvr, l);
-        while (jn >= 0 && lane + jn * kWave >= a) {  // the lane's rows of this level, highest first
-            const uint32_t q = pe_of(jn);
-            const int e0 = (int)(q & 0xffffu), e1 = (int)(q >> 16), k = lane + jn * kWave;
-            double x[CH];
-#pragma unroll
-            for (int i = 0; i < CH; i++) x[i] = S.w[pc[i]];
-            // the next row's first chunk, in flight during this row's chain
-            const int e0n = jn > 0 ? (int)(pe_of(jn - 1) & 0xffffu) : 0;
-            int nc[CH];
-            double nv[CH];
-#pragma unroll
-            for (int i = 0; i < CH; i++) nc[i] = S.c[e0n + i], nv[i] = S.v[e0n + i];
-            double ac = acc_of(jn);
-#pragma unroll
-            for (int i = 0; i < CH; i++) ac -= (e0 + i < e1) ? pv[i] * x[i] : 0.0;
-            for (int e = e0 + CH; e < e1; e += CH) {
-                int c[CH];
-                double v[CH], y[CH];
-#pragma unroll
-                for (int i = 0; i < CH; i++) c[i] = S.c[e + i], v[i] = S.v[e + i];
-#pragma unroll
-                for (int i = 0; i < CH; i++) y[i] = S.w[c[i]];
-#pragma unroll
-                for (int i = 0; i < CH; i++) ac -= (e + i < e1) ? v[i] * y[i] : 0.0;
-            }
-            S.w[k] = ac;
-            jn--;
-#pragma unroll
-            for (int i = 0; i < CH; i++) pc[i] = nc[i], pv[i] = nv[i];
-        }
-        asm volatile("" ::: "memory");  // one wave: LDS in issue order
     }
 }
 
@@ -1357,81 +1276,9 @@ __device__ __forceinline__ void levels_grouped(SweepLds &S, int nl, bool skip_fi
         asm volatile("" ::: "memory");  // one wave: LDS in issue order (levels_owned)
     }
 }
-// Forward levels of the persistent round-0 kernel, pipelined across levels (CPK_LEVEL_PIPE).  The
-// grouped loop above spends four dependent LDS round trips per level before its chain: the
-// level bounds, the rows' entry bounds and inputs, the first entries, then their gathers.  Only
-// the gathers depend on earlier levels (a level writes its own rows only), so here the level
-// bounds sit in a register (lane i holds lv[i], read by readlane) and a level's bounds, inputs
-// and first (column, value) pair are loaded while the previous level gathers and runs its chain:
-// a level costs the gather, the chain and the store.  Every level is grouped (G = 16 / 8 / 4 / 2 / 1
-// lanes per row for <= 4 / 8 / 16 / 32 / 64 rows), each row's products subtracted in the row's
-// order by its first lane: the arithmetic of levels_grouped, bit for bit.  Blocks with more than
-// 63 levels or a level of more than 64 rows take levels_grouped.
-struct LevelSlot {
-    int k, e0, e1, c, lg;
-    double acc, v;
-    bool row;
-};
-__device__ __forceinline__ void level_slot(const SweepLds &S, int lvr, int l, int lane, LevelSlot &s) {
-    const int a = __builtin_amdgcn_readlane(lvr, l), z = __builtin_amdgcn_readlane(lvr, l + 1), nr = z - a;
-    s.lg = nr <= 4 ? 4 : (nr <= 8 ? 3 : (nr <= 16 ? 2 : (nr <= 32 ? 1 : 0)));
-    const int g = lane >> s.lg, j = lane & ((1 << s.lg) - 1);
-    s.row = g < nr;
-    s.k = a + (s.row ? g : 0);
-    s.e0 = S.p[s.k];
-    s.e1 = s.row ? (int)S.p[s.k + 1] : s.e0;
-    s.acc = S.w[s.k];
-    const int e = s.e0 + j, ec = e < s.e1 ? e : s.e0;  // clamped: a valid entry of the block
-    s.c = S.c[ec];
-    s.v = S.v[ec];
-}
 template <int CH>
 __device__ __forceinline__ void levels_grouped_fwd(SweepLds &S, int nl, bool skip_first, int lane) {
-    if (!CPK_LEVEL_PIPE || nl > 63) {
-        levels_grouped<CH, false, false>(S, nl, skip_first, lane);
-        return;
-    }
-    int li = skip_first ? 1 : 0;
-    if (li >= nl) return;
-    const int lvr = lane <= nl ? (int)S.lv[lane] : 0;
-    int maxr = 0;
-    for (int l = li; l < nl; l++) maxr = max(maxr, __builtin_amdgcn_readlane(lvr, l + 1) - __builtin_amdgcn_readlane(lvr, l));
-    if (maxr > 64) {
-        levels_grouped<CH, false, false>(S, nl, skip_first, lane);
-        return;
-    }
-    LevelSlot cur;
-    level_slot(S, lvr, li, lane, cur);
-    for (;;) {
-        const double xg = S.w[cur.c];  // the first chunk's gather (the previous level's stores are in)
-        const bool more = li + 1 < nl;
-        LevelSlot nx;
-        if (more) level_slot(S, lvr, li + 1, lane, nx);  // static data and inputs of the next level's rows
-        const int G = 1 << cur.lg, j = lane & (G - 1);
-        double x = cur.e0 + j < cur.e1 ? cur.v * xg : 0.0;
-        double acc = cur.acc;
-        acc -= x;
-        for (int s = 1; s < G; s++) {
-            x = row_next_lane(x);
-            acc -= x;
-        }
-        for (int c0 = G; __any(cur.e0 + c0 < cur.e1); c0 += G) {  // rows longer than their group
-            const int e = cur.e0 + c0 + j;
-            const int ec = e < cur.e1 ? e : cur.e0;
-            const double xv = S.v[ec] * S.w[S.c[ec]];
-            x = e < cur.e1 ? xv : 0.0;
-            acc -= x;
-            for (int s = 1; s < G; s++) {
-                x = row_next_lane(x);
-                acc -= x;
-            }
-        }
-        if (cur.row && j == 0) S.w[cur.k] = acc;
-        asm volatile("" ::: "memory");  // one wave: LDS in issue order (levels_owned)
-        if (!more) break;
-        li++;
-        cur = nx;
-    }
+    levels_grouped<CH, false, false>(S, nl, skip_first, lane);
 }
 
 // Backward write-back of row k (schedule order) with value z:
@@ -2198,8 +2045,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
         // skip0: level 0 holds only rows without entries (the G pivots are in the blocks)
         // lane-owned rows for the backward sweep only: A/B at S10 (profiles/r03_level_ab_v2.txt),
         // backward 193.9 -> 186.7 us, but forward 211 -> 232 us and the fused forward 270 -> 286
-        if (CPK_LEVEL_PIPE && SPLIT == 1 && BWD && TPB == kWave && nl <= 63) levels_owned_bwd_pipe<RPT, CPK_PIPE_CH>(S, nl, nr, tid);
-        else if (CPK_LEVEL_OWN && SPLIT == 1 && BWD) levels_owned<TPB, RPT, BWD, CPK_PIPE_CH>(S, nl, nr, skip0 != 0, tid);
+        if (CPK_LEVEL_OWN && SPLIT == 1 && BWD) levels_owned<TPB, RPT, BWD, CPK_PIPE_CH>(S, nl, nr, skip0 != 0, tid);
         else if (CPK_LEVEL_GROUP && SPLIT == 1 && TPB == kWave && !BWD) levels_grouped_fwd<CPK_PIPE_CH>(S, nl, skip0 != 0, tid);
         else sweep_levels<TPB, BWD, false, CPK_PIPE_CH, false, true>(S, nl, skip0 != 0, tid);
 #pragma unroll

@@ -270,3 +270,33 @@ def test_s50_band():
 @pytest.mark.timeout(900)
 def test_s50_eight_ranks():
     _eight_ranks("s50")
+
+
+GOLDEN_S50 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "s50_serial_golden.npz")
+
+
+@pytest.mark.timeout(900)
+def test_s50_serial_golden():
+    """The 1-GPU S50 run against the SERIAL oracle (tests/golden/make_s50_golden.py, run once on
+    the CPU with the product's pivot order: niters, the history, a sample of x) within that
+    reference's own band -- the largest deviation of the same solve with its inner products
+    partitioned over 2, 4 and 8 threads -- with no safety factor."""
+    if S50_N != 50_000_000 or S50_ITMAX != 120 or not os.path.exists(GOLDEN_S50):
+        pytest.skip("the serial S50 fixture is for N = 50M, 120 iterations")
+    import hashlib
+    g = np.load(GOLDEN_S50)
+    if "s50" not in _ONE_GPU:
+        _one_gpu("s50", False)
+    x, stats, flag, perm = _ONE_GPU["s50"]
+    assert hashlib.sha256(np.ascontiguousarray(perm, np.int32).tobytes()).digest() == bytes(g["perm_sha256"])
+    assert stats["niters"] == int(g["niters"]) and bool(flag["solved"]) == bool(g["solved"])
+    h, ho = stats["residHistory"], g["hist"]
+    assert len(h) == len(ho)
+    dev = _hist_dev(h, ho, ho[0])
+    step = int(g["x_sample_step"])
+    xs, xo = x[::step], g["x_sample"]
+    dx = float(np.linalg.norm(xs - xo) / np.linalg.norm(xo))
+    _log(f"s50 vs serial: hist dev {dev:.3e} (band {float(g['band_hist']):.3e}, legs {g['band_legs']}) "
+         f"x(sample) dev {dx:.3e} (band {float(g['band_x_sample']):.3e})")
+    assert dev <= float(g["band_hist"]), (dev, float(g["band_hist"]))
+    assert dx <= float(g["band_x_sample"]), (dx, float(g["band_x_sample"]))
