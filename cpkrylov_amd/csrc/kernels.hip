@@ -1814,10 +1814,7 @@ template <int TPB, int RPT, int EPT, bool BWD, bool ADD, int SPLIT = 1, bool LOC
 #ifndef CPK_PIPE_WAVES
 #define CPK_PIPE_WAVES 4  // waves per SIMD the round-0 kernel's registers allow (4: 128 VGPRs)
 #endif
-#ifndef CPK_PIPE_WAVES_SMALL
-#define CPK_PIPE_WAVES_SMALL 5  // the same for 128-row blocks (<64, 2, 6>: a 5.6 KB LDS image)
-#endif
-__global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPLIT == 1 ? (TPB == 64 && RPT == 2 ? CPK_PIPE_WAVES_SMALL : CPK_PIPE_WAVES) : 1))) void sptrsv_pipe_kernel(
+__global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPLIT == 1 ? CPK_PIPE_WAVES : 1))) void sptrsv_pipe_kernel(
     int64_t blk0, int64_t nblk, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin,
@@ -2158,7 +2155,7 @@ static bool pipe_round0(Ctx &c, const DFactor &F, bool bwd, bool add, const doub
     if (!F.pipelined || F.round_ptr.size() < 2) return false;
 #define CPK_PR(...) pipe_round<__VA_ARGS__>(c, F, bwd, add, xin, neg_from, w, out, run, active, sched_in, ys, xs, nullptr, plan_grid, pk, pk_used)
     return CPK_PR(32, 6, 18, 2) || CPK_PR(32, 4, 12, 2) || CPK_PR(32, 8, 24, 2) || CPK_PR(128, 2, 6) ||
-           CPK_PR(64, 3, 9) || CPK_PR(64, 2, 6) || CPK_PR(64, 4, 12) || CPK_PR(64, 6, 18) || CPK_PR(64, 8, 24) || CPK_PR(128, 1, 4) ||
+           CPK_PR(64, 3, 9) || CPK_PR(64, 4, 12) || CPK_PR(64, 6, 18) || CPK_PR(64, 8, 24) || CPK_PR(128, 1, 4) ||
            CPK_PR(256, 1, 3);
 #undef CPK_PR
 }
@@ -2167,7 +2164,7 @@ static bool pipe_round0(Ctx &c, const DFactor &F, bool bwd, bool add, const doub
 static bool pipe_round0_resid(Ctx &c, const DFactor &F, double *r, const int *run, const ResArgs &ra,
                               int64_t *plan_grid = nullptr, const PackArgs *pk = nullptr, bool *pk_used = nullptr) {
 #define CPK_PR(...) pipe_round<__VA_ARGS__>(c, F, false, false, r, INT64_MAX, r, nullptr, run, nullptr, 1, nullptr, nullptr, &ra, plan_grid, pk, pk_used)
-    return CPK_PR(64, 3, 9) || CPK_PR(64, 2, 6) || CPK_PR(64, 4, 12) || CPK_PR(128, 2, 6) || CPK_PR(64, 6, 18);
+    return CPK_PR(64, 3, 9) || CPK_PR(64, 4, 12) || CPK_PR(128, 2, 6) || CPK_PR(64, 6, 18);
 #undef CPK_PR
 }
 
