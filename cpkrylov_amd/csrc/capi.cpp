@@ -230,7 +230,7 @@ int cpk_ctx_get_info(cpk_ctx ctx, int64_t *info) {
 int cpk_ctx_get_options(cpk_ctx ctx, char *buf, size_t cap) {
     API_BEGIN
     need(ctx && buf && cap > 0, "NULL argument");
-    const std::string v = engine_opts_string(ctx->c.opts, ctx->c.dist());
+    const std::string v = engine_opts_string(ctx->c.opts, ctx->c.dist() && ctx->c.nranks > 1);
     need(v.size() < cap, "buffer too small");
     std::memcpy(buf, v.c_str(), v.size() + 1);
     API_END
@@ -288,7 +288,7 @@ int cpk_ctx_set_option(cpk_ctx ctx, const char *name, const char *value) {
 int cpk_ctx_get_option(cpk_ctx ctx, const char *name, char *buf, size_t cap) {
     API_BEGIN
     need(ctx && name && buf && cap > 0, "NULL argument");
-    const std::string v = get_engine_option(ctx->c.opts, name, ctx->c.dist());
+    const std::string v = get_engine_option(ctx->c.opts, name, ctx->c.dist() && ctx->c.nranks > 1);
     need(v.size() < cap, "buffer too small");
     std::memcpy(buf, v.c_str(), v.size() + 1);
     API_END

@@ -81,10 +81,12 @@ struct SweepConfig {
     int rows[2] = {192, 512}, cap[2] = {576, 3072}, threads[2] = {64, 256};
     int sub0 = 480;  // round-0 subtree cap (0: cap[0])
 };
-// The distributed preconditioner's default (each rank schedules only its own subtrees): the
-// single-GPU default's lower round-0 subtrees give a rank's 1.25 M rows at S10 / P = 8 a third
-// sweep round, 0.337 against 0.311-0.321 ms per iteration (profiles/r03_dist_timing_v41.log), so
-// a distributed context keeps the round-0 blocks uncapped with 512-thread upper blocks.
+// The distributed preconditioner's default for P > 1 (each rank schedules only its own
+// subtrees): the single-GPU default's lower round-0 subtrees give a rank's 1.25 M rows at S10 /
+// P = 8 a third sweep round, 0.337 against 0.311-0.321 ms per iteration
+// (profiles/r03_dist_timing_v41.log), so such a rank keeps the round-0 blocks uncapped with
+// 512-thread upper blocks.  A 1-rank communicator holds the whole system: the single-GPU default
+// (profiles/r04_dist_v3.txt: 815 it/s with the distributed default against 892 on one GPU).
 SweepConfig dist_sweep_default();
 
 // Engine options of a context (opts.cpp; cpk_ctx_set_option).  None changes a result: they

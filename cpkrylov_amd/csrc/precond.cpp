@@ -254,7 +254,9 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     // local sweeps: schedule + relabel of this rank's subtrees, rows summed in exported order
     std::vector<int64_t> nextra(rp.nsub);
     for (int64_t j = 0; j < rp.nsub; j++) nextra[j] = (int64_t)rp.extra[j].size();
-    const SweepConfig sw = effective_sweep(c.opts, true);  // the distributed path's (dist_sweep_default)
+    // the rank's subtrees of a P > 1 split take the distributed default (dist_sweep_default); one
+    // rank holds the whole system and takes the single-GPU one
+    const SweepConfig sw = effective_sweep(c.opts, c.nranks > 1);
     Schedule S = build_schedule(rp.Fsub, sw.rows[0], sw.cap[0], sw.rows[1], sw.cap[1], sw.sub0, &nextra);
     for (int i = 0; i < 2; i++)
         pc->dF.sweep_rows[i] = sw.rows[i], pc->dF.sweep_cap[i] = sw.cap[i], pc->dF.sweep_threads[i] = sw.threads[i];
