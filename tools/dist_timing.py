@@ -5,7 +5,7 @@ peers: collectives are no-ops, so the numbers are meaningless but the kernels ar
 rank's share of the P-way solve.
 Prints, per (P, rank): the local rows, the construction time of the rank's preconditioner
 (ptime, and a refactorization with the same values), kernel timings (cpk_profile_kernels), the
-wall time per iteration of a 20-iteration solve (collective latency NOT included), the process's
+wall time per iteration of an ITMAX-iteration solve (collective latency NOT included), the process's
 peak host RSS and the device memory the rank's objects hold.
 CONFIG=s10 (default): S10, cpminres.  CONFIG=s50: S50 (nonsymmetric 3x3 block, 50M dofs),
 cpdqgmres(40), with the Krylov A as the placement hint -- SURVEY.md section 8d config 5.
@@ -30,7 +30,10 @@ CONFIG = os.environ.get("CONFIG", "s10")
 if CONFIG == "s50":
     S = nonsym_system(int(os.environ.get("N", "50000000")))
     METHOD, MOPTS = 5, dict(mem=40, restart=40)
+    # the bench line's truncated run: the 40-vector window fills over the first 40 iterations
+    ITMAX = int(os.environ.get("ITMAX", "120"))
 else:
+    ITMAX = int(os.environ.get("ITMAX", "20"))
     S = saddle_system(int(os.environ.get("N", "10000000")), window=int(os.environ.get("WINDOW", "4")))
     METHOD, MOPTS = 2, {}
 runs = [(int(a.split(":")[0]), int(a.split(":")[1])) for a in sys.argv[1:]] or [(1, 0), (2, 0), (4, 0), (8, 0), (8, 7)]
@@ -51,15 +54,15 @@ for P, r, sw in runs:
     dofs, n_loc = M.local_dofs()
     p = _lib.Profile()
     _lib.check(_lib.lib.cpk_profile_kernels(ctx.h, A.h, Cm.h, M.h, 20, C.byref(p)))
-    # a fixed 20-iteration solve (tolerance 0): wall time per iteration of the rank's kernels
+    # a fixed ITMAX-iteration solve (tolerance 0): wall time per iteration of the rank's kernels
     dev = torch.device("cuda", 0)
     b1 = torch.from_numpy(np.ascontiguousarray(S["rhs"][dofs[:n_loc]])).to(dev)
     xy = torch.empty(max(len(dofs), 1), dtype=torch.float64, device=dev)
-    opts = _lib.make_opts(dict(atol=0.0, rtol=0.0, itmax=20, print=False, nitref=1, force_itref=True, **MOPTS))
+    opts = _lib.make_opts(dict(atol=0.0, rtol=0.0, itmax=ITMAX, print=False, nitref=1, force_itref=True, **MOPTS))
     st = _lib.Stats()
-    hist = np.zeros(64)
+    hist = np.zeros(ITMAX + 64)
     st.hist = hist.ctypes.data_as(C.POINTER(C.c_double))
-    st.hist_cap = 64
+    st.hist_cap = ITMAX + 64
     per_it = None
     err = None
     try:
