@@ -60,7 +60,10 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-reps", type=int, default=20)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE passes")
-    ap.add_argument("--dist", action="store_true", help="run the distributed path even on one GPU (1-rank RCCL)")
+    ap.add_argument("--dist", action="store_true",
+                    help="one GPU through a 1-rank RCCL communicator (a torchrun world of one: the single-GPU path)")
+    ap.add_argument("--dist1", action="store_true",
+                    help="with --dist: engine option dist1, the distributed kernels at one rank (diagnostic)")
     ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--rhs-perturb", type=float, default=0.0,
                     help="scale the rhs by (1 + eps*u), u uniform in [-1, 1] (sensitivity runs; never the bench line)")
@@ -160,7 +163,7 @@ def main(argv=None):
     n, m, N = S["n"], S["m"], S["N"]
     # N > 1 (or --dist): one distributed solve over all ranks (strong scaling), RCCL collectives
     # and halo exchanges inside the solver; every rank holds its row block
-    distributed = world > 1 or args.dist
+    distributed = world > 1 or args.dist or args.dist1
     dev = torch.device("cuda", local)
     if distributed:
         # every rank must finish its setup before any rank enters a collective: a rank that fails
@@ -172,7 +175,8 @@ def main(argv=None):
             if dist:
                 dist.broadcast_object_list(uid, src=0)
             with _quiet_stdout():
-                ctx = cpk.Context(device=local, rank=rank, nranks=world, unique_id=uid[0])
+                ctx = cpk.Context(device=local, rank=rank, nranks=world, unique_id=uid[0],
+                                  options={"dist1": 1} if args.dist1 else None)
             cinfo = ctx.info()
             if cinfo["comm"] != "rccl" or cinfo["comm_ranks"] != world:
                 raise RuntimeError(f"the RCCL communicator holds {cinfo['comm_ranks']} rank(s), expected {world}")
@@ -312,7 +316,7 @@ def main(argv=None):
                                     "dependent, DESIGN.md sec. 6), parity checked on the same truncated run"),
                        "N": N, "n": n, "m": m, "nnz_kp": M.info["nnz_kp"], "nnz_l": M.info["nnz_l"],
                        "sweep_launches": M.info["nrounds"], "elim_tree_depth": M.info["depth"],
-                       "parallelism": f"rowblock{world}" if distributed else "single",
+                       "parallelism": f"rowblock{world}" if cinfo["distributed"] else "single",
                        "rccl_ranks": cinfo["comm_ranks"] if cinfo["comm"] == "rccl" else 0,
                        "sweep": ctx.get_option("sweep"),
                        "seed": S["seed"], "window": S["window"],

@@ -49,6 +49,8 @@ struct cpk_mat_s {
     // cached in the Precond itself (Precond::dist_ops), keyed by the matrices' generations: they
     // die with the preconditioner, and a new preconditioner never sees an old one's rows
     const DMat &krylov_op(cpk_mat_s *C, Precond &M) {
+        if (M.dist != ctx->c.dist())
+            throw Error(CPK_ERR_ARGS, "engine option dist1 changed after the preconditioner was built");
         if (!M.dist) return blkdiag_with(C);
         auto &slot = M.dist_ops[{'K', gen, C->gen}];
         if (!slot) {
@@ -198,7 +200,7 @@ int cpk_ctx_create(int device, int rank, int nranks, const unsigned char *unique
     need(out != nullptr, "out is NULL");
     need(nranks == 1 || unique_id != nullptr, "unique_id required when nranks > 1");
     auto ctx = ctx_base(device, rank, nranks);
-    if (unique_id) {  // a 1-rank communicator runs the distributed path too
+    if (unique_id) {  // a 1-rank communicator: the single-GPU path unless engine option dist1
         ctx->comm.reset(make_rccl_comm(nranks, rank, unique_id));
         ctx->c.comm = ctx->comm.get();
     }

@@ -115,6 +115,8 @@ struct EngineOpts {
     bool no_tkr = false;          // no_tkr:             distributed refinement residual through the Kp halo
     bool no_minres_fuse = false;  // no_minres_fuse:     cpminres update as its own pass (normalise + w, x)
     bool dist_graph = true;       // dist_graph:         capture collectives in the graphs
+    bool dist1 = false;           // dist1:              a 1-rank communicator runs the distributed path
+                                  //                     (diagnostic; set before building operators)
     int batch = 0;                // batch:              fixed iterations per graph (0: adaptive)
     bool profile_fwd_sched = false;     // profile_fwd_sched: diagnostic, the profiled forward reads its input in schedule order
 };
@@ -141,7 +143,11 @@ struct Ctx {
     DBuf<unsigned> counter;  // arrival tickets
     DBuf<double> red;        // distributed mode: local sums awaiting the allreduce
     Comm *comm = nullptr;    // owned by the C-ABI context object
-    bool dist() const { return comm != nullptr; }  // also a 1-rank communicator (tests)
+    // the distributed path: a communicator of more than one rank.  A 1-rank communicator has
+    // nothing to exchange and runs the single-GPU path (the same bits) unless engine option
+    // dist1 asks for the distributed kernels (tests; DESIGN.md section 7's 1-rank comparison).
+    // The timing stand-in (NullComm) declares nranks > 1.
+    bool dist() const { return comm != nullptr && (nranks > 1 || opts.dist1); }
     void ensure_partials(size_t count);
 };
 

@@ -67,6 +67,7 @@ const BoolOpt kBool[] = {
     {"no_tkr", &EngineOpts::no_tkr},
     {"no_minres_fuse", &EngineOpts::no_minres_fuse},
     {"dist_graph", &EngineOpts::dist_graph},
+    {"dist1", &EngineOpts::dist1},
     {"profile_fwd_sched", &EngineOpts::profile_fwd_sched},
 };
 

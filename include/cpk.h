@@ -105,8 +105,9 @@ int cpk_abi_version(void);
 /* Fill `id` (128 bytes) with an RCCL unique id on rank 0; broadcast it to the other ranks. */
 int cpk_get_unique_id(unsigned char id[128]);
 /* device < 0: use the current device.  nranks == 1 and unique_id == NULL: no communicator.
- * With a unique_id the context runs the distributed path (RCCL) even for nranks == 1;
- * nranks > 1 requires a unique_id. */
+ * nranks > 1 requires a unique_id and runs the distributed path over RCCL.  A 1-rank RCCL
+ * communicator (a torchrun world of one) has nothing to exchange: it runs the single-GPU path
+ * unless engine option dist1 is set before the operators are built. */
 int cpk_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id, cpk_ctx *out);
 /* Diagnostic timing stand-in (no reference counterpart): rank `rank` of an nranks-way
  * distributed context WITHOUT peers.  Every collective is a no-op (an allgather copies the
@@ -134,8 +135,9 @@ int cpk_ctx_create_sim(int device, cpk_simgroup group, int rank, int nranks, cpk
  * once at creation; a change applies to preconditioners and solves created afterwards.
  * Names: sweep ("rows,cap,threads[,rows,cap,threads[,sub0]]"; unset, each path has its own
  * default: a distributed context reports and uses the distributed one), split_tol, host_factor,
- * no_pipe, no_upper, no_col16, no_sched_resid, no_fused_resid, r0_xcd_chunk, tsolve_global,
+ * no_pipe, no_upper, no_col16, no_sched_resid, no_fused_resid, r0_xcd_chunk, tsolve_global, tsolve_sweep,
  * no_piggy, no_halo_merge, no_graph, no_fuse_last, no_tkr, no_minres_fuse, dist_graph, batch,
+ * dist1 (a 1-rank communicator runs the distributed kernels; set before building operators),
  * profile_fwd_sched (diagnostic), sweep_set ("0" returns sweep to the per-path default).
  * Booleans as "0"/"1".  A distributed preconditioner allgathers a hash of its plan and of every
  * option at creation and fails (CPK_ERR_ARGS) on every rank unless all ranks agree. */

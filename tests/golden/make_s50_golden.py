@@ -9,12 +9,13 @@ host analysis is deterministic for any thread count), and records
     niters and the solved flag;
   * x's norm and a fixed sample of x (every XSTEP-th entry);
   * the serial reference's own band: the largest deviation from it of the same solve with the
-    inner products partitioned over 2, 4 and 8 OpenMP threads (each a different summation order
-    of every dot product -- the only thing a parallel implementation changes);
+    inner products partitioned over 2 to 8 OpenMP threads (each a different summation order of
+    every dot product -- the only thing a parallel implementation changes), per thread count;
   * a hash of the pivot order, so the test can check that the GPU ran the same order.
 
-Run (about an hour on 8 cores, ~45 GB of memory):  python tests/golden/make_s50_golden.py
-The output, tests/golden/s50_serial_golden.npz, is data only.
+Run (about 1.5 hours on 8 cores, ~45 GB of memory):  python tests/golden/make_s50_golden.py
+`--legs 3,5,6,7` adds thread counts to an existing fixture (the committed one was made with
+2, 4, 8 and extended so).  The output, tests/golden/s50_serial_golden.npz, is data only.
 """
 import hashlib
 import os
@@ -54,31 +55,59 @@ def solve(S, perm, threads):
         O.set_threads(1)
 
 
+def legs_of(S, perm, h, x, threads):
+    """per thread count: (history deviation / h0, x-sample deviation)"""
+    sample = np.arange(0, S["N"], XSTEP)
+    out = {}
+    for T in threads:
+        xt, stt = solve(S, perm, T)
+        ht = np.asarray(stt["residHistory"])
+        L = min(len(ht), len(h))
+        assert len(ht) == len(h), (T, len(ht), len(h))
+        out[T] = (float(np.max(np.abs(ht[:L] - h[:L])) / h[0]),
+                  float(np.linalg.norm(xt[sample] - x[sample]) / np.linalg.norm(x[sample])))
+        log(f"threads={T}: hist {out[T][0]:.3e} x(sample) {out[T][1]:.3e}")
+    return out
+
+
 def main():
+    extend = None
+    if len(sys.argv) > 2 and sys.argv[1] == "--legs":
+        extend = [int(t) for t in sys.argv[2].split(",")]
     t = time.perf_counter()
     S = nonsym_system(N=N)
     log(f"S50 generated, N={S['N']} ({time.perf_counter() - t:.0f} s)")
     perm = np.ascontiguousarray(cpk.analyze(S["G"], S["B"], -S["C"])["perm"], np.int32)
     log("product pivot order from the host analysis")
+    sample = np.arange(0, S["N"], XSTEP)
+    if extend:
+        g = dict(np.load(OUT))
+        assert bytes(g["perm_sha256"]) == hashlib.sha256(perm.tobytes()).digest()
+        # the serial x at the sample and the serial history are in the fixture; the legs need the
+        # full serial x, so the serial solve runs again (deterministic: checked against the fixture)
+        x, st = solve(S, perm, 1)
+        assert np.array_equal(np.asarray(st["residHistory"]), g["hist"]) and np.array_equal(x[sample], g["x_sample"])
+        new = legs_of(S, perm, g["hist"], x, extend)
+        legs = dict(zip((int(v) for v in g.get("band_threads", [2, 4, 8])), (float(v) for v in g["band_legs"])))
+        legs.update({T: v[0] for T, v in new.items()})
+        ths = sorted(legs)
+        g["band_threads"] = np.array(ths)
+        g["band_legs"] = np.array([legs[T] for T in ths])
+        g["band_hist"] = np.float64(max(legs.values()))
+        g["band_x_sample"] = np.float64(max([float(g["band_x_sample"])] + [v[1] for v in new.values()]))
+        np.savez_compressed(OUT, **g)
+        log(f"extended {OUT}: legs {dict(zip(ths, g['band_legs']))}")
+        return
     x, st = solve(S, perm, 1)
     h = np.asarray(st["residHistory"])
-    sample = np.arange(0, S["N"], XSTEP)
-    band_h, band_x = 0.0, 0.0
-    legs = {}
-    for T in (2, 4, 8):
-        xt, stt = solve(S, perm, T)
-        ht = np.asarray(stt["residHistory"])
-        L = min(len(ht), len(h))
-        legs[T] = float(np.max(np.abs(ht[:L] - h[:L])) / h[0])
-        band_h = max(band_h, legs[T])
-        band_x = max(band_x, float(np.linalg.norm(xt[sample] - x[sample]) / np.linalg.norm(x[sample])))
-        assert stt["niters"] == st["niters"], (T, stt["niters"], st["niters"])
-    log(f"band over 2/4/8 threads: hist {band_h:.3e} ({legs}) x(sample) {band_x:.3e}")
+    ths = [2, 3, 4, 5, 6, 7, 8]
+    legs = legs_of(S, perm, h, x, ths)
     np.savez_compressed(OUT, N=np.int64(S["N"]), itmax=np.int64(ITMAX), niters=np.int64(st["niters"]),
                         solved=np.int64(st["solved"]), hist=h, x_norm=np.float64(np.linalg.norm(x)),
-                        x_sample_step=np.int64(XSTEP), x_sample=x[sample], band_hist=np.float64(band_h),
-                        band_x_sample=np.float64(band_x),
-                        band_legs=np.array([legs[2], legs[4], legs[8]]),
+                        x_sample_step=np.int64(XSTEP), x_sample=x[sample],
+                        band_hist=np.float64(max(v[0] for v in legs.values())),
+                        band_x_sample=np.float64(max(v[1] for v in legs.values())),
+                        band_threads=np.array(ths), band_legs=np.array([legs[T][0] for T in ths]),
                         perm_sha256=np.frombuffer(hashlib.sha256(perm.tobytes()).digest(), np.uint8))
     log(f"wrote {OUT}")
 

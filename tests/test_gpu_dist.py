@@ -27,12 +27,15 @@ SAFETY = 10.0
 
 def _run_ranks(P, fn, options=None):
     """fn(ctx, rank) on P simulated ranks; returns the list of results.  options: engine options
-    of every rank's context (a dict), or a function rank -> dict."""
+    of every rank's context (a dict), or a function rank -> dict.  P = 1 sets dist1 (a 1-rank
+    communicator otherwise runs the single-GPU path)."""
     import cpkrylov_amd as cpk
     g = cpk.SimGroup(P)
 
     def one(r):
         opt = options(r) if callable(options) else options
+        if P == 1:
+            opt = dict(opt or {}, dist1=1)
         ctx = cpk.Context(device=0, rank=r, nranks=P, simgroup=g, options=opt)
         try:
             return fn(ctx, r)
@@ -199,31 +202,40 @@ def test_dist_device_vectors_synthetic():
 
 
 def test_rccl_one_rank_graph_capture():
-    """The RCCL transport and hipGraph capture of its collectives, on the one GPU available:
-    a 1-rank communicator runs the distributed path (allreduce epilogues captured in the
-    iteration graph).  With one rank every sum is the local one, so the answer is bit-identical
-    to the single-GPU path."""
+    """The RCCL transport and hipGraph capture of its collectives, on the one GPU available.  A
+    1-rank communicator runs the single-GPU path by default (nothing to exchange); with engine
+    option dist1 it runs the distributed path (allreduce epilogues captured in the iteration
+    graph).  With one rank every sum is the local one: both are bit-identical to the single-GPU
+    path."""
     import cpkrylov_amd as cpk
     Pd = F.load("cvxqp1_m")
     opts = dict(F.EXPROG_OPTS)
     x1, s1, f1 = cpk.reg_cpkrylov(cpk.cpminres, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts)
-    ctx = cpk.Context(device=0, rank=0, nranks=1, unique_id=cpk.get_unique_id())
-    try:
-        assert ctx.info()["comm"] == "rccl" and ctx.info()["comm_ranks"] == 1
-        x2, s2, f2 = cpk.reg_cpkrylov(cpk.cpminres, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts, ctx=ctx)
-        assert s2["niters"] == s1["niters"] and f2 == f1
-        assert np.array_equal(s2["residHistory"], s1["residHistory"])
-        assert np.array_equal(x2, x1)
-        # the 1-rank apply runs the single-GPU kernel sequence (schedule order, fused residual)
-        info = s2["M"].sep_info()
-        assert info["sched"] == 1 and info["fused"] == 1 and info["nT"] == 0, info
-        z = np.random.default_rng(5).standard_normal(Pd["n"] + Pd["m"])
-        s2["M"].nitref, s1["M"].nitref = 1, 1
-        s2["M"].force_itref, s1["M"].force_itref = True, True
-        assert np.array_equal(s2["M"] * z, s1["M"] * z)
-        del s2
-    finally:
-        ctx.close()
+    z = np.random.default_rng(5).standard_normal(Pd["n"] + Pd["m"])
+    s1["M"].nitref, s1["M"].force_itref = 1, True
+    y1 = s1["M"] * z
+    for dist1 in (False, True):
+        ctx = cpk.Context(device=0, rank=0, nranks=1, unique_id=cpk.get_unique_id(),
+                          options={"dist1": 1} if dist1 else None)
+        try:
+            info = ctx.info()
+            assert info["comm"] == "rccl" and info["comm_ranks"] == 1 and info["distributed"] == dist1, info
+            x2, s2, f2 = cpk.reg_cpkrylov(cpk.cpminres, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts, ctx=ctx)
+            assert s2["niters"] == s1["niters"] and f2 == f1
+            assert np.array_equal(s2["residHistory"], s1["residHistory"])
+            assert np.array_equal(x2, x1)
+            # either way the apply runs the single-GPU kernel sequence (schedule order, fused residual)
+            sep = s2["M"].sep_info()
+            assert sep["dist"] == int(dist1) and sep["sched"] == 1 and sep["fused"] == 1 and sep["nT"] == 0, sep
+            s2["M"].nitref, s2["M"].force_itref = 1, True
+            assert np.array_equal(s2["M"] * z, y1)
+            # dist1 decides the path when the operators are built: flipping it afterwards is refused
+            ctx.set_option("dist1", "0" if dist1 else "1")
+            with pytest.raises(cpk.CpkError, match="dist1"):
+                cpk.cpminres(Pd["rhs"][:Pd["n"]], Pd["Q"], Pd["C"], s2["M"], opts)
+            del s2
+        finally:
+            ctx.close()
 
 
 @pytest.mark.parametrize("P", [8])
