@@ -224,9 +224,12 @@ def test_rccl_one_rank_graph_capture():
             assert s2["niters"] == s1["niters"] and f2 == f1
             assert np.array_equal(s2["residHistory"], s1["residHistory"])
             assert np.array_equal(x2, x1)
-            # either way the apply runs the single-GPU kernel sequence (schedule order, fused residual)
+            # dist1: the distributed apply runs the single-GPU kernel sequence (schedule order,
+            # fused residual); without it the preconditioner is the single-GPU one
             sep = s2["M"].sep_info()
-            assert sep["dist"] == int(dist1) and sep["sched"] == 1 and sep["fused"] == 1 and sep["nT"] == 0, sep
+            assert sep["dist"] == int(dist1), sep
+            if dist1:
+                assert sep["sched"] == 1 and sep["fused"] == 1 and sep["nT"] == 0, sep
             s2["M"].nitref, s2["M"].force_itref = 1, True
             assert np.array_equal(s2["M"] * z, y1)
             # dist1 decides the path when the operators are built: flipping it afterwards is refused
