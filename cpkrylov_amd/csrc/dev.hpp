@@ -103,6 +103,8 @@ struct EngineOpts {
     bool no_pipe = false;         // no_pipe:            round 0 one workgroup per block
     bool no_upper = false;        // no_upper:           upper rounds through the generic kernels
     bool no_col16 = false;        // no_col16:           round-0 forward columns as int32
+    bool no_dataflow = false;     // no_dataflow:        upper rounds always on the level loop
+    bool all_dataflow = false;    // all_dataflow:       upper rounds always on the dataflow loop (tests)
     bool no_sched_resid = false;  // no_sched_resid:     refinement residual in original order
     bool no_fused_resid = false;  // no_fused_resid:     refinement residual as its own SpMV
     int r0_xcd_chunk = 16;        // r0_xcd_chunk:       K > 0: runs of K consecutive round-0 blocks share an XCD
@@ -201,6 +203,7 @@ struct DFactor {
     bool pipelined = true;  // round 0 through the persistent pipelined kernel (set before make_dfactor)
     bool no_upper = false;  // upper rounds through the generic kernels (set before make_dfactor)
     bool no_col16 = false;  // no int16 round-0 forward columns (set before make_dfactor)
+    int dataflow = 0;       // upper-round level loops: 0 the host model per block, 1 never, 2 always
     // engine options of the preconditioner's context when it was built (launch-time paths)
     bool no_fused_resid = false;
     bool fuse_last = false;  // single GPU, no entries outside the factor: the last round fwd + bwd in one launch
@@ -410,6 +413,9 @@ Analysis analyze(const HCsr &A11, const HCsr &B, const HCsr &C22, const EngineOp
 constexpr int64_t kSepPiggy = 2;  // spare payload slots per rank in the separator exchange
 // spare slots per rank in the Krylov operator's halo exchange: the Lanczos beta partials ride
 // there with the next vector's halo (solvers.hip, cpminres)
+// block record flags (DFactor::meta, the l1 field): the dataflow level loop per direction for
+// an upper-round block (mark_dataflow, kernels.hip); every reader of l1 masks them off
+constexpr int32_t kMetaDfFwd = 1 << 30, kMetaDfBwd = 1 << 29, kMetaL1Mask = (1 << 29) - 1;
 constexpr int64_t kKrylovSpare = 2;
 struct DSep {
     int64_t nT = 0, kt = 0, nlev = 0, nsend = 0, ntdof = 0;

@@ -61,6 +61,152 @@ void make_dmat(const HCsr &a, DMat &d) {
 // by descending key of the row.  key[q] is the pre-relabel index of relabelled row q (so a
 // relabelled factor still sums in the exported factor's order); extra[q] are backward entries
 // of row q that refer to rows outside this factor (distributed separators).
+// entries per LDS round trip in the upper-round level loop, per direction: the forward rows
+// carry tens of in-block terms, the backward ones few (stamps build, profiles/r03_upper_ch_v17.txt:
+// 8 vs 4 per chunk, forward levels -7 % / -11 % in rounds 1 / 2, backward +14 % / +17 %)
+#ifndef CPK_UPPER_CH_FWD
+#define CPK_UPPER_CH_FWD 8
+#endif
+#ifndef CPK_UPPER_CH_BWD
+#define CPK_UPPER_CH_BWD 4
+#endif
+// the dataflow level loop (levels_dataflow) where mark_dataflow picks it; terms per iteration;
+// the modelled cost of one of its trips relative to a level-loop trip (more LDS reads and
+// instructions per iteration; calibrated on S10 and the +-64 window variant)
+constexpr double kDataflowTripCost = 2.0;
+#ifndef CPK_UPPER_DATAFLOW
+#define CPK_UPPER_DATAFLOW 1
+#endif
+#ifndef CPK_DF_CH
+#define CPK_DF_CH 8
+#endif
+// Level loop or dataflow loop (levels_dataflow) for an upper-round block's levels, chosen per
+// block and direction on the host from a model of each loop's dependent LDS round trips:
+//   level loop (sweep_levels, one wave): per level and pass of 64 rows, one trip for the rows'
+//     bounds and one pair per chunk of CPK_UPPER_CH terms of the level's longest row;
+//   dataflow loop: its lock-step schedule simulated exactly (a row's terms taken CPK_DF_CH at a
+//     time once their columns were finished in an earlier iteration), a pair of trips per
+//     iteration plus one per row switch.
+// The dataflow loop wins on dense chains (a separator clique: a level per row, tens of terms
+// each) and loses on wide shallow blocks, where a lane's rows wait on each other in sequence.
+// The choice is bits 30 (forward) / 29 (backward) of the block record's l1 (kernels mask them).
+namespace {
+int64_t level_trips(const std::vector<int32_t> &lvl_bounds, const std::vector<int> &nterm, int ch) {
+    int64_t trips = 0;
+    for (size_t l = 0; l + 1 < lvl_bounds.size(); l++) {
+        for (int a = lvl_bounds[l]; a < lvl_bounds[l + 1]; a += kWave) {
+            int mx = 0;
+            for (int k = a; k < std::min(a + kWave, (int)lvl_bounds[l + 1]); k++) mx = std::max(mx, nterm[k]);
+            trips += 1 + 2 * ((mx + ch - 1) / ch);
+        }
+    }
+    return trips;
+}
+// terms[k]: the row's loop terms (after the folded outside prefix), -1 for an outside term;
+// order[i]: the i-th row solved (lane i % 64); returns trips, or `stop` once it exceeds it
+int64_t dataflow_trips(const std::vector<std::vector<int>> &terms, bool bwd, int ch, int64_t stop) {
+    const int nr = (int)terms.size();
+    std::vector<int64_t> done(nr, INT64_MAX);
+    struct Lane { int i, e; };
+    std::vector<Lane> L(kWave);
+    for (int l = 0; l < kWave; l++) L[l] = {l, 0};
+    auto row = [&](int i) { return bwd ? nr - 1 - i : i; };
+    int64_t trips = 1;
+    for (int64_t it = 0;; it++) {
+        bool any = false;
+        int switches = 0;
+        for (int l = 0; l < kWave; l++) {
+            Lane &z = L[l];
+            if (z.i >= nr) continue;
+            any = true;
+            const std::vector<int> &t = terms[row(z.i)];
+            for (int j = 0; j < ch && z.e < (int)t.size(); j++) {
+                const int c = t[z.e];
+                if (c >= 0 && done[c] >= it) break;
+                z.e++;
+            }
+            int sw = 0;
+            while (z.i < nr && z.e >= (int)terms[row(z.i)].size()) {
+                done[row(z.i)] = it;
+                z.i += kWave, z.e = 0, sw++;
+            }
+            switches = std::max(switches, sw);
+        }
+        if (!any) return trips;
+        trips += 2 + switches;
+        if (trips > stop) return trips;
+    }
+}
+}  // namespace
+
+void mark_dataflow(std::vector<int32_t> &meta, const std::vector<int64_t> &round_ptr, const std::vector<uint32_t> &fptr,
+                   const std::vector<int32_t> &fcol, const std::vector<uint32_t> &bptr, const std::vector<int32_t> &bcol,
+                   int mode) {
+    if (!CPK_UPPER_DATAFLOW || round_ptr.size() < 3 || mode == 1) return;
+    const int64_t b0 = round_ptr[1], b1 = round_ptr.back();  // the upper rounds
+    // CPK_DF_ALPHA (diagnostic, tools/gpu_steps.sh A/B runs): the trip cost the model uses
+    static const double alpha = getenv("CPK_DF_ALPHA") ? atof(getenv("CPK_DF_ALPHA")) : kDataflowTripCost;
+    std::vector<float> ratio((size_t)(b1 - b0) * 2, 0.f);
+    parallel_for(b1 - b0, [&](int64_t lo, int64_t hi) {
+        std::vector<int32_t> lb;
+        std::vector<int> nterm;
+        std::vector<std::vector<int>> terms;
+        for (int64_t b = b0 + lo; b < b0 + hi; b++) {
+            int32_t *m = &meta[(size_t)b * 8];
+            const int r0 = m[0], r1 = m[1], nr = r1 - r0;
+            for (int dir = 0; dir < 2; dir++) {
+                const std::vector<uint32_t> &ptr = dir ? bptr : fptr;
+                const std::vector<int32_t> &col = dir ? bcol : fcol;
+                terms.assign((size_t)nr, {});
+                nterm.assign((size_t)nr, 0);
+                for (int k = 0; k < nr; k++) {
+                    uint32_t e = ptr[r0 + k];
+                    const uint32_t e1 = ptr[r0 + k + 1];
+                    while (e < e1 && !(col[e] >= r0 && col[e] < r1)) e++;  // fold_prefix's leading outside terms
+                    for (; e < e1; e++) terms[k].push_back(col[e] >= r0 && col[e] < r1 ? col[e] - r0 : -1);
+                    nterm[k] = (int)terms[k].size();
+                }
+                // level bounds of the block (rows are contiguous by level): from the row dependencies
+                // the kernel's level array describes -- recomputed here as the longest path
+                std::vector<int> lev((size_t)nr, 0);
+                int nlev = 0;
+                for (int q = 0; q < nr; q++) {
+                    const int k = dir ? nr - 1 - q : q;
+                    for (int c : terms[k]) if (c >= 0) lev[k] = std::max(lev[k], lev[c] + 1);
+                    nlev = std::max(nlev, lev[k] + 1);
+                }
+                // rows per level (the kernel walks each level's rows in passes of 64)
+                std::vector<int> cnt((size_t)nlev, 0), mx((size_t)nlev, 0);
+                lb.assign((size_t)nlev + 1, 0);
+                std::vector<int> byl((size_t)nr);
+                for (int k = 0; k < nr; k++) cnt[lev[k]]++;
+                for (int l = 0; l < nlev; l++) lb[l + 1] = lb[l] + cnt[l];
+                {
+                    std::vector<int> pos(lb.begin(), lb.end() - 1);
+                    for (int k = 0; k < nr; k++) byl[pos[lev[k]]++] = nterm[k];
+                }
+                const int64_t lt = level_trips(lb, byl, dir ? CPK_UPPER_CH_BWD : CPK_UPPER_CH_FWD);
+                const int64_t dt = dataflow_trips(terms, dir == 1, CPK_DF_CH, (int64_t)(4 * lt) + 8);
+                ratio[(size_t)(b - b0) * 2 + dir] = (float)lt / (float)std::max<int64_t>(dt, 1);
+                if (mode == 2 || alpha * (double)dt < (double)lt) m[3] |= dir ? kMetaDfBwd : kMetaDfFwd;
+            }
+        }
+    }, 4);
+    if (getenv("CPK_DEBUG_DATAFLOW")) {  // diagnostic: blocks per direction on the dataflow loop
+        int64_t nf = 0, nb = 0;
+        for (int64_t b = b0; b < b1; b++) nf += (meta[(size_t)b * 8 + 3] & kMetaDfFwd) != 0, nb += (meta[(size_t)b * 8 + 3] & kMetaDfBwd) != 0;
+        fprintf(stderr, "dataflow: %lld upper blocks, forward %lld, backward %lld (trip cost %.2f)\n", (long long)(b1 - b0),
+                (long long)nf, (long long)nb, alpha);
+        for (int dir = 0; dir < 2; dir++) {  // level-loop trips / dataflow trips, quantiles
+            std::vector<float> q;
+            for (int64_t b = 0; b < b1 - b0; b++) q.push_back(ratio[(size_t)b * 2 + dir]);
+            std::sort(q.begin(), q.end());
+            fprintf(stderr, "  %s lt/dt: p10 %.2f p50 %.2f p90 %.2f max %.2f\n", dir ? "bwd" : "fwd", q[q.size() / 10],
+                    q[q.size() / 2], q[q.size() * 9 / 10], q.back());
+        }
+    }
+}
+
 constexpr int64_t kInsertionSortMax = 32;  // rows up to this long sort by insertion (keys are distinct)
 void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vector<int64_t> *key,
                   const std::vector<std::vector<BwdExtra>> *extra, std::vector<int32_t> *fsrc,
@@ -219,9 +365,10 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
         m[0] = (int32_t)r0, m[1] = (int32_t)r1, m[2] = (int32_t)l0, m[3] = (int32_t)l1;
         m[4] = (int32_t)fptr[r0], m[5] = (int32_t)fptr[r1], m[6] = (int32_t)bptr[r0], m[7] = (int32_t)bptr[r1];
     }
+    mark_dataflow(meta, s.round_ptr, fptr, fcol, bptr, bcol, d.dataflow);
     d.meta.upload(meta);
     d.hmeta = meta;
-    clk.lap("layout: uploads, block records");
+    clk.lap("layout: uploads, block records, level-loop choice");
     d.round0_rows = -1;
     if (s.round_ptr.size() >= 2) {  // round 0 a leading, contiguous row range?
         int64_t r = 0;
@@ -847,6 +994,7 @@ void dsep_sweep_setup(Ctx &c, DSep &T, const RankPlan &rp, int P) {
     DFactor &d = T.tsw;
     for (int i = 0; i < 2; i++) d.sweep_rows[i] = sw.rows[i], d.sweep_cap[i] = sw.cap[i], d.sweep_threads[i] = sw.threads[i];
     d.pipelined = true, d.no_upper = false, d.no_col16 = true, d.fuse_last = false, d.skip0 = false;
+    d.dataflow = c.opts.no_dataflow ? 1 : (c.opts.all_dataflow ? 2 : 0);
     d.N = NT;
     std::vector<uint32_t> fptr((size_t)NT + 1, 0), bptr((size_t)NT + 1, 0);
     std::vector<int32_t> fcol, bcol, perm((size_t)NT, 0);
@@ -883,6 +1031,7 @@ void dsep_sweep_setup(Ctx &c, DSep &T, const RankPlan &rp, int P) {
         m[0] = (int32_t)r0, m[1] = (int32_t)r1, m[2] = (int32_t)S.blk_lvl[b], m[3] = (int32_t)S.blk_lvl[b + 1];
         m[4] = (int32_t)fptr[r0], m[5] = (int32_t)fptr[r1], m[6] = (int32_t)bptr[r0], m[7] = (int32_t)bptr[r1];
     }
+    mark_dataflow(meta, S.round_ptr, fptr, fcol, bptr, bcol, d.dataflow);
     for (size_t r = 0; r < d.round_fits.size(); r++)
         for (int64_t b = S.round_ptr[r]; b < S.round_ptr[r + 1]; b++) {
             const int32_t *m = &meta[(size_t)b * 8];
@@ -1028,15 +1177,6 @@ void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, co
 // LDS image of a staged block (dynamic shared memory, sized per launch):
 //   double w[R + 1] | double v[CAP + 8] | int16 c[CAP + 8] | int16 p[R + 1] | int16 lv[R + 1] | int16 ps[R + 1]
 constexpr int kSweepPad = 8;
-// entries per LDS round trip in the upper-round level loop, per direction: the forward rows
-// carry tens of in-block terms, the backward ones few (stamps build, profiles/r03_upper_ch_v17.txt:
-// 8 vs 4 per chunk, forward levels -7 % / -11 % in rounds 1 / 2, backward +14 % / +17 %)
-#ifndef CPK_UPPER_CH_FWD
-#define CPK_UPPER_CH_FWD 8
-#endif
-#ifndef CPK_UPPER_CH_BWD
-#define CPK_UPPER_CH_BWD 4
-#endif
 #define CPK_UPPER_CH(bwd) ((bwd) ? CPK_UPPER_CH_BWD : CPK_UPPER_CH_FWD)
 #ifndef CPK_PIPE_CH
 #define CPK_PIPE_CH 2  // entries per LDS round trip in the round-0 level loop
@@ -1281,6 +1421,65 @@ __device__ __forceinline__ void levels_grouped_fwd(SweepLds &S, int nl, bool ski
     levels_grouped<CH, false, false>(S, nl, skip_first, lane);
 }
 
+// Dataflow level phase of the upper rounds (one wave, after fold_prefix; terms against the 1.0
+// slot R as in sweep_levels<..., ONE>).  The level loop waits, per level, for the slowest row of
+// the level, and a row of many in-block terms costs a chunk round trip pair per CH terms in
+// every level it sits on.  Here lane L owns the block's rows L, L + 64, ... (forward; backward
+// from the last row down), in the order the rows depend on each other, and each iteration it
+// takes the next CH terms of its current row, reads their columns' ready flags and values, and
+// subtracts the longest READY prefix of them in the row's order; a finished row publishes its
+// value and flag and the lane moves on.  No level structure is needed: a row starts on its
+// early terms while later ones are still being solved, so a chain of dense rows (a separator
+// clique) advances about one row per iteration instead of one level per row-length of chunks.
+// Same terms in the same order, not-taken ones subtract +0.0 (an exact no-op): bit-identical.
+// The flags live in the level-bound array (lv, R + 1 entries: rows < nr, and R ready), unused
+// here.  One wave, so LDS operations complete in issue order: a flag read after a store sees
+// it, and a flag is stored after its value.  Progress: the lowest unfinished row (highest,
+// backward) has every source done and is its lane's current row, so every iteration takes at
+// least one term or finishes a row; `ne + 2` iterations bound the loop (a hang is impossible
+// even on malformed input).
+template <bool BWD, int CH>
+__device__ __forceinline__ void levels_dataflow(SweepLds &S, int nr, int R, int ne, int lane) {
+    static_assert(CH <= kSweepPad, "chunk wider than the padding");
+    int16_t *rdy = S.lv;
+    for (int k = lane; k < nr; k += kWave) rdy[k] = 0;
+    if (lane == 0) rdy[R] = 1;
+    asm volatile("" ::: "memory");
+    int i = lane;  // the lane's current row, counted from the first row it solves
+    bool live = i < nr;
+    int k = 0, e = 0, e1 = 0;
+    double acc = 0.0;
+    if (live) k = BWD ? nr - 1 - i : i, e = S.ps[k], e1 = S.p[k + 1], acc = S.w[k];
+    for (int it = 0; it < ne + 2 && __any(live); it++) {
+        if (live) {
+            int c[CH];
+            double v[CH], x[CH];
+            int16_t f[CH];
+#pragma unroll
+            for (int j = 0; j < CH; j++) c[j] = S.c[e + j], v[j] = S.v[e + j];
+#pragma unroll
+            for (int j = 0; j < CH; j++) f[j] = rdy[c[j]], x[j] = S.w[c[j]];
+            int t = 0;
+#pragma unroll
+            for (int j = 0; j < CH; j++) {
+                const bool take = t == j && e + j < e1 && f[j] != 0;
+                acc -= take ? v[j] * x[j] : 0.0;
+                t += take;
+            }
+            e += t;
+            while (e >= e1) {  // row done (and every following row with no terms left)
+                S.w[k] = acc;
+                rdy[k] = 1;
+                i += kWave;
+                live = i < nr;
+                if (!live) break;
+                k = BWD ? nr - 1 - i : i, e = S.ps[k], e1 = S.p[k + 1], acc = S.w[k];
+            }
+        }
+        asm volatile("" ::: "memory");
+    }
+}
+
 // Backward write-back of row k (schedule order) with value z:
 //   out != null: out[perm[k]] = z, or (ADD) base + z with base = ys[k] when ys is given (the
 //                previous solution kept in schedule order), else out[perm[k]];
@@ -1496,7 +1695,7 @@ __device__ __forceinline__ void upper_block(
 #else
     (void)b;
 #endif
-    const int r0 = m.r0, r1 = m.r1, nr = r1 - r0, nl = m.l1 - m.l0;
+    const int r0 = m.r0, r1 = m.r1, nr = r1 - r0, nl = (m.l1 & kMetaL1Mask) - m.l0;
     const uint32_t e0 = BWD ? (uint32_t)m.be0 : (uint32_t)m.fe0;
     const int ne = BWD ? m.be1 - m.be0 : m.fe1 - m.fe0;
     const int tid = threadIdx.x;
@@ -1553,7 +1752,9 @@ __device__ __forceinline__ void upper_block(
     // (a single wave's LDS accesses complete in program order) the chain is LDS latency only;
     // narrow levels give each row a lane group (levels_grouped)
     if (tid < kWave) {
-        if (CPK_UPPER_GROUP(BWD)) levels_grouped<CPK_UPPER_CH(BWD), BWD, true>(S, nl, false, tid);
+        if (CPK_UPPER_DATAFLOW && (m.l1 & (BWD ? kMetaDfBwd : kMetaDfFwd)))
+            levels_dataflow<BWD, CPK_DF_CH>(S, nr, R, ne, tid);
+        else if (CPK_UPPER_GROUP(BWD)) levels_grouped<CPK_UPPER_CH(BWD), BWD, true>(S, nl, false, tid);
         else sweep_levels<kWave, BWD, true, CPK_UPPER_CH(BWD), true, true>(S, nl, false, tid);
     }
     __syncthreads();
@@ -1610,7 +1811,7 @@ __device__ __forceinline__ void last_block(
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
     int sched_in, double *xs, double *w, double *out, double *ys) {
     constexpr int R = RPU * TPB, CAP = EPU * TPB;
-    const int r0 = m.r0, r1 = m.r1, nr = r1 - r0, nl = m.l1 - m.l0;
+    const int r0 = m.r0, r1 = m.r1, nr = r1 - r0, nl = (m.l1 & kMetaL1Mask) - m.l0;
     const int nef = m.fe1 - m.fe0, neb = m.be1 - m.be0;
     const int tid = threadIdx.x;
     SweepLds S(smem, R, CAP);
@@ -1662,7 +1863,8 @@ __device__ __forceinline__ void last_block(
     __syncthreads();
     fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (CPK_UPPER_GROUP(false)) levels_grouped<CPK_UPPER_CH(false), false, true>(S, nl, false, tid);
+        if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd)) levels_dataflow<false, CPK_DF_CH>(S, nr, R, nef, tid);
+        else if (CPK_UPPER_GROUP(false)) levels_grouped<CPK_UPPER_CH(false), false, true>(S, nl, false, tid);
         else sweep_levels<kWave, false, true, CPK_UPPER_CH(false), true, true>(S, nl, false, tid);
     }
     __syncthreads();
@@ -1680,6 +1882,8 @@ __device__ __forceinline__ void last_block(
     }
     if (tid == 0) S.p[nr] = (int16_t)neb;
     if (tid < kSweepPad) S.c[neb + tid] = (int16_t)R;
+    if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd) && !(m.l1 & kMetaDfBwd))  // the forward flags took lv
+        for (int l = tid; l <= nl; l += TPB) S.lv[l] = (int16_t)(lvl_row[m.l0 + l] - r0);
 #pragma unroll
     for (int u = 0; u < EPU; u++) {
         const int e = tid + u * TPB;
@@ -1692,7 +1896,8 @@ __device__ __forceinline__ void last_block(
     __syncthreads();
     fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (CPK_UPPER_GROUP(true)) levels_grouped<CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
+        if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfBwd)) levels_dataflow<true, CPK_DF_CH>(S, nr, R, neb, tid);
+        else if (CPK_UPPER_GROUP(true)) levels_grouped<CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
         else sweep_levels<kWave, true, true, CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
     }
     __syncthreads();
@@ -1846,7 +2051,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     uint32_t kb0 = 0, kb1 = 0;
     int32_t kc[RES ? EPT : 1];  // columns only: the values load beside the y gathers
     auto issue = [&](const BlkMeta &m) {
-        const int nr = m.r1 - m.r0, nl = m.l1 - m.l0;
+        const int nr = m.r1 - m.r0, nl = (m.l1 & kMetaL1Mask) - m.l0;
         const uint32_t e0 = BWD ? (uint32_t)m.be0 : (uint32_t)m.fe0;
         const int ne = BWD ? m.be1 - m.be0 : m.fe1 - m.fe0;
         if (RES) {
@@ -1914,7 +2119,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
 #ifdef CPK_PIPE_STAMPS
         const uint64_t tb = (uint64_t)clock64();
 #endif
-        const int nr = cur.r1 - cur.r0, nl = cur.l1 - cur.l0;
+        const int nr = cur.r1 - cur.r0, nl = (cur.l1 & kMetaL1Mask) - cur.l0;
         const uint32_t e0 = BWD ? (uint32_t)cur.be0 : (uint32_t)cur.fe0;
         const int ne = BWD ? cur.be1 - cur.be0 : cur.fe1 - cur.fe0;
         const int r0 = cur.r0, r1 = cur.r1;

@@ -56,6 +56,8 @@ const BoolOpt kBool[] = {
     {"no_pipe", &EngineOpts::no_pipe},
     {"no_upper", &EngineOpts::no_upper},
     {"no_col16", &EngineOpts::no_col16},
+    {"no_dataflow", &EngineOpts::no_dataflow},
+    {"all_dataflow", &EngineOpts::all_dataflow},
     {"no_sched_resid", &EngineOpts::no_sched_resid},
     {"no_fused_resid", &EngineOpts::no_fused_resid},
     {"tsolve_global", &EngineOpts::tsolve_global},

@@ -321,12 +321,14 @@ def test_dist_minres_fused_update_bitexact(P):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["tsolve_global", "tsolve_sweep"])
+@pytest.mark.parametrize("path", ["tsolve_global", "tsolve_sweep", "tsolve_sweep,all_dataflow",
+                                  "tsolve_sweep,no_dataflow"])
 @pytest.mark.parametrize("P", [2, 4])
 def test_dist_apply_separator_fallbacks_bitexact(P, path):
     """The separator solve's other paths -- records left in HBM (a separator too large for LDS),
-    and T solved by the block sweeps (the path of a T no workgroup holds) -- give the same bits
-    as the staged solve and the oracle."""
+    and T solved by the block sweeps (the path of a T no workgroup holds; its upper rounds and
+    the ranks' own on either level loop) -- give the same bits as the staged solve and the
+    oracle."""
     import cpkrylov_amd as cpk
     S = _system("synthetic20k")
     z = np.random.default_rng(7).standard_normal(S["n"] + S["m"])
@@ -336,7 +338,7 @@ def test_dist_apply_separator_fallbacks_bitexact(P, path):
         M.nitref, M.force_itref = 1, True
         return M * z, M.export_factors() if r == 0 else None
 
-    res = _run_ranks(P, work, {path: 1})
+    res = _run_ranks(P, work, {k: 1 for k in path.split(",")})
     L, D, perm = res[0][1]
     Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=(L, D, perm))
     Mo.set(nitref=1.0, force_itref=1.0)

@@ -356,6 +356,48 @@ def test_precond_apply_fused_last_round(gpu_ctx, name, props):
         for y in ys:
             assert np.array_equal(y, yo)
 
+_W64 = {}
+
+
+@pytest.mark.parametrize("name", ["cvxqp1_m", "synthetic", "w64"])
+@pytest.mark.parametrize("props", [dict(nitref=0), dict(nitref=1, force_itref=True),
+                                   dict(nitref=2, force_itref=False, itref_tol=1e-30)])
+def test_precond_apply_dataflow_levels(gpu_ctx, name, props):
+    """The upper rounds' two level loops: the level-synchronous loop (engine option no_dataflow)
+    and the dataflow loop (levels_dataflow; all_dataflow forces it on every upper block), and the
+    default per-block choice of the host model -- with the default staging and small blocks
+    (many upper rounds, the fused last round among them), on a system whose separators are dense
+    chains (w64: the +-64 coupling window, where the model picks the dataflow loop).  Every way
+    the oracle's bits."""
+    import cpkrylov_amd as cpk
+    if name == "w64":
+        from cpkrylov_amd.synthetic import saddle_system
+        if "s" not in _W64:
+            _W64["s"] = saddle_system(N=60000, window=64, seed=5)
+        S = _W64["s"]
+        G, B, C = S["G"], S["B"], S["C"]
+    else:
+        G, B, C = _system_gbc(name)
+    z = np.random.default_rng(37).standard_normal(G.shape[0] + B.shape[0])
+    for sweep in ("", "64,192,64,128,512,512"):
+        ys = []
+        for mode in ({}, {"no_dataflow": 1}, {"all_dataflow": 1}):
+            opts = dict(mode)
+            if sweep:
+                opts["sweep"] = sweep
+            with cpk.engine_options(**opts):
+                M = cpk.opLDL2(G, B, -C)
+            for k, v in props.items():
+                setattr(M, k, v)
+            ys.append(M * z)
+        L, D, perm = M.export_factors()
+        Mo = O.LDL2(G, B, -C, factors=(L, D, perm))
+        Mo.set(**{k: float(v) for k, v in props.items()})
+        yo = Mo @ z
+        for y in ys:
+            assert np.array_equal(y, yo)
+
+
 @pytest.mark.parametrize("name,extra,batch", [("cvxqp1_m", {}, 0), ("cvxqp1_m", {}, 3), ("cvxqp1_m", {"itmax": 1}, 0),
                                               ("cvxqp1_m", {"itmax": 2}, 3), ("cvxqp1_m", {"itmax": 7}, 3),
                                               ("syn_symm20k", {}, 0)])
