@@ -70,6 +70,17 @@ void make_dmat(const HCsr &a, DMat &d) {
 #ifndef CPK_UPPER_CH_BWD
 #define CPK_UPPER_CH_BWD 4
 #endif
+// round 0 on the dataflow loop: 0 never, 1 both directions, 2 forward only (default), terms per
+// iteration.  A/B at S10 (profiles/r04_r0_dataflow_ab_v7.txt, two boxes): forward-only with 2
+// terms per iteration takes the round-0 forward sweep 188 -> 176-178 us and the fused residual
+// forward 260 -> 252-256 us (+1.3-1.5 % it/s); the backward loses 1-3 % on it (the owned-row
+// level loop stays), 4 terms spill
+#ifndef CPK_R0_DATAFLOW
+#define CPK_R0_DATAFLOW 2
+#endif
+#ifndef CPK_R0_DF_CH
+#define CPK_R0_DF_CH 2
+#endif
 // the dataflow level loop (levels_dataflow) where mark_dataflow picks it; terms per iteration;
 // the modelled cost of one of its trips relative to a level-loop trip (more LDS reads and
 // instructions per iteration; calibrated on S10 and the +-64 window variant)
@@ -1438,20 +1449,37 @@ __device__ __forceinline__ void levels_grouped_fwd(SweepLds &S, int nl, bool ski
 // backward) has every source done and is its lane's current row, so every iteration takes at
 // least one term or finishes a row; `ne + 2` iterations bound the loop (a hang is impossible
 // even on malformed input).
-template <bool BWD, int CH>
+// Rows with no terms left are ready from the start; a lane walks only its rows with terms, a
+// bit mask of them in a register (next row: lowest set bit), so a finished row hands over to the
+// next one without a loop.
+template <bool BWD, int CH, bool PS, int RPL>  // PS: rows start at ps[k] (after fold_prefix), else p[k];
+                                               // RPL: rows per lane (R / 64)
 __device__ __forceinline__ void levels_dataflow(SweepLds &S, int nr, int R, int ne, int lane) {
     static_assert(CH <= kSweepPad, "chunk wider than the padding");
+    static_assert(RPL <= 32, "row mask of 32 bits");
     int16_t *rdy = S.lv;
-    for (int k = lane; k < nr; k += kWave) rdy[k] = 0;
+    uint32_t mask = 0;  // bit j: row lane + 64 j has terms to take
+#pragma unroll
+    for (int j = 0; j < RPL; j++) {
+        const int i = lane + j * kWave;
+        if (i < nr) {
+            const int k = BWD ? nr - 1 - i : i;
+            const bool has = (PS ? S.ps[k] : S.p[k]) < S.p[k + 1];
+            rdy[k] = has ? 0 : 1;
+            mask |= (uint32_t)has << j;
+        }
+    }
     if (lane == 0) rdy[R] = 1;
     asm volatile("" ::: "memory");
-    int i = lane;  // the lane's current row, counted from the first row it solves
-    bool live = i < nr;
     int k = 0, e = 0, e1 = 0;
     double acc = 0.0;
-    if (live) k = BWD ? nr - 1 - i : i, e = S.ps[k], e1 = S.p[k + 1], acc = S.w[k];
-    for (int it = 0; it < ne + 2 && __any(live); it++) {
-        if (live) {
+    auto next_row = [&]() {
+        const int i = lane + (int)__builtin_ctz(mask) * kWave;
+        k = BWD ? nr - 1 - i : i, e = PS ? S.ps[k] : S.p[k], e1 = S.p[k + 1], acc = S.w[k];
+    };
+    if (mask) next_row();
+    for (int it = 0; it < ne + 2 && __any(mask != 0); it++) {
+        if (mask) {
             int c[CH];
             double v[CH], x[CH];
             int16_t f[CH];
@@ -1467,13 +1495,11 @@ __device__ __forceinline__ void levels_dataflow(SweepLds &S, int nr, int R, int 
                 t += take;
             }
             e += t;
-            while (e >= e1) {  // row done (and every following row with no terms left)
+            if (e >= e1) {  // row done: publish it, take the next row with terms
                 S.w[k] = acc;
                 rdy[k] = 1;
-                i += kWave;
-                live = i < nr;
-                if (!live) break;
-                k = BWD ? nr - 1 - i : i, e = S.ps[k], e1 = S.p[k + 1], acc = S.w[k];
+                mask &= mask - 1;
+                if (mask) next_row();
             }
         }
         asm volatile("" ::: "memory");
@@ -1753,7 +1779,7 @@ __device__ __forceinline__ void upper_block(
     // narrow levels give each row a lane group (levels_grouped)
     if (tid < kWave) {
         if (CPK_UPPER_DATAFLOW && (m.l1 & (BWD ? kMetaDfBwd : kMetaDfFwd)))
-            levels_dataflow<BWD, CPK_DF_CH>(S, nr, R, ne, tid);
+            levels_dataflow<BWD, CPK_DF_CH, true, R / kWave>(S, nr, R, ne, tid);
         else if (CPK_UPPER_GROUP(BWD)) levels_grouped<CPK_UPPER_CH(BWD), BWD, true>(S, nl, false, tid);
         else sweep_levels<kWave, BWD, true, CPK_UPPER_CH(BWD), true, true>(S, nl, false, tid);
     }
@@ -1863,7 +1889,7 @@ __device__ __forceinline__ void last_block(
     __syncthreads();
     fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd)) levels_dataflow<false, CPK_DF_CH>(S, nr, R, nef, tid);
+        if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd)) levels_dataflow<false, CPK_DF_CH, true, R / kWave>(S, nr, R, nef, tid);
         else if (CPK_UPPER_GROUP(false)) levels_grouped<CPK_UPPER_CH(false), false, true>(S, nl, false, tid);
         else sweep_levels<kWave, false, true, CPK_UPPER_CH(false), true, true>(S, nl, false, tid);
     }
@@ -1896,7 +1922,7 @@ __device__ __forceinline__ void last_block(
     __syncthreads();
     fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfBwd)) levels_dataflow<true, CPK_DF_CH>(S, nr, R, neb, tid);
+        if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfBwd)) levels_dataflow<true, CPK_DF_CH, true, R / kWave>(S, nr, R, neb, tid);
         else if (CPK_UPPER_GROUP(true)) levels_grouped<CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
         else sweep_levels<kWave, true, true, CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
     }
@@ -2250,7 +2276,9 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
         // skip0: level 0 holds only rows without entries (the G pivots are in the blocks)
         // lane-owned rows for the backward sweep only: A/B at S10 (profiles/r03_level_ab_v2.txt),
         // backward 193.9 -> 186.7 us, but forward 211 -> 232 us and the fused forward 270 -> 286
-        if (CPK_LEVEL_OWN && SPLIT == 1 && BWD) levels_owned<TPB, RPT, BWD, CPK_PIPE_CH>(S, nl, nr, skip0 != 0, tid);
+        if (CPK_R0_DATAFLOW && (CPK_R0_DATAFLOW == 1 || !BWD) && SPLIT == 1 && TPB == kWave)
+            levels_dataflow<BWD, CPK_R0_DF_CH, false, R / kWave>(S, nr, R, ne, tid);
+        else if (CPK_LEVEL_OWN && SPLIT == 1 && BWD) levels_owned<TPB, RPT, BWD, CPK_PIPE_CH>(S, nl, nr, skip0 != 0, tid);
         else if (CPK_LEVEL_GROUP && SPLIT == 1 && TPB == kWave && !BWD) levels_grouped_fwd<CPK_PIPE_CH>(S, nl, skip0 != 0, tid);
         else sweep_levels<TPB, BWD, false, CPK_PIPE_CH, false, true>(S, nl, skip0 != 0, tid);
 #pragma unroll
