@@ -70,13 +70,12 @@ void make_dmat(const HCsr &a, DMat &d) {
 #ifndef CPK_UPPER_CH_BWD
 #define CPK_UPPER_CH_BWD 4
 #endif
-// round 0 on the dataflow loop: 0 never, 1 both directions, 2 forward only (default), terms per
-// iteration.  A/B at S10 (profiles/r04_r0_dataflow_ab_v7.txt, two boxes): forward-only with 2
-// terms per iteration takes the round-0 forward sweep 188 -> 176-178 us and the fused residual
-// forward 260 -> 252-256 us (+1.3-1.5 % it/s); the backward loses 1-3 % on it (the owned-row
-// level loop stays), 4 terms spill
+// round 0 on the dataflow loop: 0 never, 1 both directions (default), 2 forward only; terms per
+// iteration.  A/B at S10 (profiles/r04_r0_dataflow_ab_v7.txt): 2 terms per iteration take the
+// round-0 forward sweep 188 -> 170-178 us and the fused residual forward 260 -> 251-256 us; the
+// backward 180-182 -> 177 us once a lane walks a mask of its rows (4 terms spill)
 #ifndef CPK_R0_DATAFLOW
-#define CPK_R0_DATAFLOW 2
+#define CPK_R0_DATAFLOW 1
 #endif
 #ifndef CPK_R0_DF_CH
 #define CPK_R0_DF_CH 2
@@ -2334,6 +2333,11 @@ static bool pipe_round(Ctx &c, const DFactor &F, bool bwd, bool add, const doubl
                          : loc ? (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT, true>
                                : (const void *)sptrsv_pipe_kernel<TPB, RPT, EPT, false, false, SPLIT>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, TPB * SPLIT, lds) != hipSuccess || occ < 1) occ = 1;
+    // at most CPK_PIPE_WAVES waves per SIMD, even when a variant's registers would allow more: the
+    // assignment's dispatch-slot speeds (plan_round0) are measured at four, and a fifth wave on
+    // some SIMDs only (the LDS caps a CU at 18 workgroups) made the forward sweep 15 % slower
+    // (a 96-VGPR build, r04o)
+    occ = std::min(occ, std::max(1, CPK_PIPE_WAVES * 4 * kWave / (TPB * SPLIT)));
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
