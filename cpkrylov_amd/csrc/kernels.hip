@@ -1486,13 +1486,14 @@ __device__ __forceinline__ void levels_dataflow(SweepLds &S, int nr, int R, int 
             for (int j = 0; j < CH; j++) c[j] = S.c[e + j], v[j] = S.v[e + j];
 #pragma unroll
             for (int j = 0; j < CH; j++) f[j] = rdy[c[j]], x[j] = S.w[c[j]];
-            int t = 0;
+            // ready bits of the chunk's terms, every flag used: no load is sunk into a branch, so
+            // all flag and value reads of an iteration are in flight together
+            uint32_t rb = 0;
 #pragma unroll
-            for (int j = 0; j < CH; j++) {
-                const bool take = t == j && e + j < e1 && f[j] != 0;
-                acc -= take ? v[j] * x[j] : 0.0;
-                t += take;
-            }
+            for (int j = 0; j < CH; j++) rb |= (uint32_t)((f[j] != 0) & (e + j < e1)) << j;
+            const int t = __builtin_ctz(~rb);  // the leading ready terms
+#pragma unroll
+            for (int j = 0; j < CH; j++) acc -= j < t ? v[j] * x[j] : 0.0;
             e += t;
             if (e >= e1) {  // row done: publish it, take the next row with terms
                 S.w[k] = acc;
