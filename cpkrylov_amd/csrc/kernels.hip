@@ -87,9 +87,15 @@ constexpr double kDataflowTripCost = 2.0;
 #ifndef CPK_UPPER_DATAFLOW
 #define CPK_UPPER_DATAFLOW 1
 #endif
-#ifndef CPK_DF_CH
-#define CPK_DF_CH 8
+// (per direction; the +-64 window, profiles/r04_dataflow_ch_ab_v10.txt: forward 8 / 4 / 2 terms
+// 0.767 / 0.732 / 0.900 ms per sweep, backward 0.690 / 0.574 / 0.536)
+#ifndef CPK_DF_CH_FWD
+#define CPK_DF_CH_FWD 4
 #endif
+#ifndef CPK_DF_CH_BWD
+#define CPK_DF_CH_BWD 2
+#endif
+#define CPK_DF_CH(bwd) ((bwd) ? CPK_DF_CH_BWD : CPK_DF_CH_FWD)
 // Level loop or dataflow loop (levels_dataflow) for an upper-round block's levels, chosen per
 // block and direction on the host from a model of each loop's dependent LDS round trips:
 //   level loop (sweep_levels, one wave): per level and pass of 64 rows, one trip for the rows'
@@ -196,7 +202,7 @@ void mark_dataflow(std::vector<int32_t> &meta, const std::vector<int64_t> &round
                     for (int k = 0; k < nr; k++) byl[pos[lev[k]]++] = nterm[k];
                 }
                 const int64_t lt = level_trips(lb, byl, dir ? CPK_UPPER_CH_BWD : CPK_UPPER_CH_FWD);
-                const int64_t dt = dataflow_trips(terms, dir == 1, CPK_DF_CH, (int64_t)(4 * lt) + 8);
+                const int64_t dt = dataflow_trips(terms, dir == 1, CPK_DF_CH(dir == 1), (int64_t)(4 * lt) + 8);
                 ratio[(size_t)(b - b0) * 2 + dir] = (float)lt / (float)std::max<int64_t>(dt, 1);
                 if (mode == 2 || alpha * (double)dt < (double)lt) m[3] |= dir ? kMetaDfBwd : kMetaDfFwd;
             }
@@ -1779,7 +1785,7 @@ __device__ __forceinline__ void upper_block(
     // narrow levels give each row a lane group (levels_grouped)
     if (tid < kWave) {
         if (CPK_UPPER_DATAFLOW && (m.l1 & (BWD ? kMetaDfBwd : kMetaDfFwd)))
-            levels_dataflow<BWD, CPK_DF_CH, true, R / kWave>(S, nr, R, ne, tid);
+            levels_dataflow<BWD, CPK_DF_CH(BWD), true, R / kWave>(S, nr, R, ne, tid);
         else if (CPK_UPPER_GROUP(BWD)) levels_grouped<CPK_UPPER_CH(BWD), BWD, true>(S, nl, false, tid);
         else sweep_levels<kWave, BWD, true, CPK_UPPER_CH(BWD), true, true>(S, nl, false, tid);
     }
@@ -1889,7 +1895,7 @@ __device__ __forceinline__ void last_block(
     __syncthreads();
     fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd)) levels_dataflow<false, CPK_DF_CH, true, R / kWave>(S, nr, R, nef, tid);
+        if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd)) levels_dataflow<false, CPK_DF_CH(false), true, R / kWave>(S, nr, R, nef, tid);
         else if (CPK_UPPER_GROUP(false)) levels_grouped<CPK_UPPER_CH(false), false, true>(S, nl, false, tid);
         else sweep_levels<kWave, false, true, CPK_UPPER_CH(false), true, true>(S, nl, false, tid);
     }
@@ -1922,7 +1928,7 @@ __device__ __forceinline__ void last_block(
     __syncthreads();
     fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfBwd)) levels_dataflow<true, CPK_DF_CH, true, R / kWave>(S, nr, R, neb, tid);
+        if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfBwd)) levels_dataflow<true, CPK_DF_CH(true), true, R / kWave>(S, nr, R, neb, tid);
         else if (CPK_UPPER_GROUP(true)) levels_grouped<CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
         else sweep_levels<kWave, true, true, CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
     }
