@@ -81,9 +81,11 @@ void make_dmat(const HCsr &a, DMat &d) {
 #define CPK_R0_DF_CH 2
 #endif
 // the dataflow level loop (levels_dataflow) where mark_dataflow picks it; terms per iteration;
-// the modelled cost of one of its trips relative to a level-loop trip (more LDS reads and
-// instructions per iteration; calibrated on S10 and the +-64 window variant)
-constexpr double kDataflowTripCost = 2.0;
+// the modelled cost of one of its trips relative to a level-loop trip: 2.0 for the first loop
+// (8 terms, a row-switch loop, short-circuit flag reads), 1.0 since the mask walk, the
+// branch-free ready prefix and 4 / 2 terms (profiles/r04_dataflow_alpha_ab_v11.txt: S10 +0.4 %,
+// P = 8 rank -1.2 %, the +-64 window 324 -> 357 it/s)
+constexpr double kDataflowTripCost = 1.0;
 #ifndef CPK_UPPER_DATAFLOW
 #define CPK_UPPER_DATAFLOW 1
 #endif
