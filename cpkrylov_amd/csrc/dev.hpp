@@ -209,6 +209,9 @@ struct DFactor {
     bool fuse_last = false;  // single GPU, no entries outside the factor: the last round fwd + bwd in one launch
     bool skip0 = true;       // round 0's level-0 rows have no forward entries (false: a separator's T sweep)
     int64_t round0_rows = -1;  // round 0 is the rows [0, round0_rows) (-1: not a leading row range)
+    // rows of round 0 whose backward value the pipelined kernel does not store back into w in a
+    // sweep launched with wdead (launch_sptrsv_bwd): the byte models drop them
+    int64_t bwd_dead_w_rows() const { return pipelined && round0_rows > 0 ? round0_rows : 0; }
     std::vector<int32_t> hmeta;  // host copy of meta
     // round-0 blocks assigned to the persistent launch's workgroups by modelled cost (plan_round0),
     // per kernel variant v (0 forward, 1 forward with the fused refinement residual, 2 backward):
@@ -287,8 +290,11 @@ bool launch_sptrsv_fwd(Ctx &c, const DFactor &F, const double *xin, int64_t neg_
 // add with ys: out = P * (ys + solution), ys the previous solution in schedule order
 // pk (optional, distributed): the output packed by the write-back, keyed by output index (out
 // given) or by schedule row (out == null); returns whether every round packed
+// wdead: nothing reads w after this sweep, so the pipelined round 0 (the sweep's last round)
+// does not store its rows back into it (it still writes out / ys)
 bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
-                       const int *active, double *ys = nullptr, const FwdIn *last = nullptr, const PackArgs *pk = nullptr);
+                       const int *active, double *ys = nullptr, const FwdIn *last = nullptr, const PackArgs *pk = nullptr,
+                       bool wdead = false);
 // r = xin(perm) - A*y with A = P'*Kp*P in schedule order (rows and columns), y in schedule
 // order (perm null: xin is the signed input already in schedule order, see launch_sptrsv_fwd);
 // order; each row sums its entries in Kp's column order, so r(k) equals row perm(k) of the

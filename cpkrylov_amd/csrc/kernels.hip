@@ -2063,8 +2063,9 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
     static_assert(SPLIT == 1 || TPB * SPLIT == 64, "split blocks must share one wave");
     static_assert(!LOC || !BWD, "block-local columns: forward round 0 only");
     static_assert(!RES || (LOC && SPLIT == 1), "fused residual: forward round 0 with block-local columns");
-    // perm is read for the forward gather (unless the input is in schedule order) and for the
-    // backward scatter (unless the solution stays in schedule order)
+    // sched_in: forward, the input is in schedule order; backward, w is dead after the sweep
+    // (launch_sptrsv_bwd's wdead).  perm is read for the forward gather (unless the input is in
+    // schedule order) and for the backward scatter (unless the solution stays in schedule order)
     const bool need_perm = BWD ? out != nullptr : !sched_in;
     constexpr int R = RPT * TPB, CAP = EPT * TPB;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2294,7 +2295,9 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
             const int i = tid + j * TPB;
             if (i < nr) {
                 const double z = S.w[i];
-                w[r0 + i] = z;
+                // round 0 is the backward sweep's last round; the caller says when nothing reads
+                // its w afterwards (backward: sched_in carries launch_sptrsv_bwd's wdead)
+                if (!BWD || !sched_in) w[r0 + i] = z;
                 if (BWD) {
                     if (out) {
                         const double o = ADD ? xg[j] + z : z;
@@ -2630,7 +2633,7 @@ bool launch_sptrsv_fwd_resid(Ctx &c, const DFactor &F, const DMat &Kps, const do
 }
 
 bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool add, const int *run,
-                       const int *active, double *ys, const FwdIn *last, const PackArgs *pk) {
+                       const int *active, double *ys, const FwdIn *last, const PackArgs *pk, bool wdead) {
     if (!out && add && !ys) throw Error(CPK_ERR_ARGS, "internal: accumulating backward sweep without a base");
     int64_t R = (int64_t)F.round_ptr.size() - 1;
     bool packed = pk != nullptr && !(last && last->valid);
@@ -2640,7 +2643,8 @@ bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
         R = last->from;
     }
     for (int64_t r = R - 1; r >= 0; r--) {
-        if (r == 0 && pipe_round0(c, F, true, add, nullptr, 0, w, out, run, active, 0, ys, nullptr, nullptr, pk)) continue;
+        if (r == 0 && pipe_round0(c, F, true, add, nullptr, 0, w, out, run, active, wdead ? 1 : 0, ys, nullptr, nullptr, pk))
+            continue;
         if (r > 0 && upper_round(c, F, r, true, add, nullptr, 0, w, out, run, active, 0, ys, nullptr, pk ? *pk : none))
             continue;
         packed = false;

@@ -711,7 +711,7 @@ void Precond::dist_sched_apply(const double *x, int64_t neg_from, double *y, con
     launch_sep_exchange(c, sep, r.p, x, neg_from, nullptr, f2);
     launch_sep_solve(c, sep, r.p + nsub, y, true, run, nullptr, nullptr, nullptr, tkr ? tkr_ptr.p : nullptr, tkr_col.p,
                      tkr_val.p, w.p + nsub);
-    launch_sptrsv_bwd(c, dF, r.p, y, true, run, nullptr, w.p, &last2);  // y = P*(ys + dy)
+    launch_sptrsv_bwd(c, dF, r.p, y, true, run, nullptr, w.p, &last2, nullptr, true);  // y = P*(ys + dy); r dead
 }
 
 void Precond::set_handle(bool on) {
@@ -771,7 +771,8 @@ void Precond::apply(const double *x, int64_t neg_from, double *y, const int *run
                 else launch_spmv_resid_sched(c, dKps, dF.perm.p, x, neg_from, w.p, r.p, run);
                 launch_sptrsv_fwd(c, dF, r.p, N, r.p, run, nullptr, true, nullptr, &last);
             }
-            launch_sptrsv_bwd(c, dF, r.p, s + 1 == steps ? y : nullptr, true, run, nullptr, w.p, &last);
+            // r is formed again by the next step's residual: its round-0 rows are not stored back
+            launch_sptrsv_bwd(c, dF, r.p, s + 1 == steps ? y : nullptr, true, run, nullptr, w.p, &last, nullptr, true);
         }
         return;
     }
@@ -813,7 +814,8 @@ double Precond::apply_bytes() const {
         const double kps = 12 * (double)Ks.nnz + 4 * (Nn + 1) + 8 * Nn /*y*/ +
                            (xs.n ? 8 * Nn /*xs*/ : 12 * Nn /*x(perm)*/) + 8 * Nn /*r*/;
         const double fwd_s = 12 * l - 2 * (double)dF.nnz16 + 4 * (Nn + 1) + 16 * Nn;
-        const double bwd_acc = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn + 8 * Nn /*ys*/;
+        const double dead = 8.0 * (double)dF.bwd_dead_w_rows();  // round 0's w, not stored back
+        const double bwd_acc = 12 * l + 4 * (Nn + 1) + 16 * Nn + 8 * Nn + 8 * Nn /*ys*/ - dead;
         double b = fwd + (xs.n ? 8 * Nn : 0.0) /*xs written*/ + bwd_keep + steps * (kps + fwd_s + bwd_acc) + (4 + 8) * Nn /*last: perm + scatter*/ +
                    (steps - 1) * 8.0 * Nn /*ys written back in place*/;
         // fused refinement input (launch_sptrsv_fwd_resid): r is neither written nor read back

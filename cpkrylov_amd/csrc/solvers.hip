@@ -2104,11 +2104,12 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
     out->fwd_bytes = 12.0 * l - 2.0 * (double)M.dF.nnz16 + 4.0 * (Nn + 1) + 4.0 * Nn /*perm*/ + 8.0 * Nn /*x*/ + 8.0 * Nn /*w*/;
     const double pair_ms = timeit([&]() {
         launch_sptrsv_fwd(c, M.dF, x.p, M.n, M.w.p, nullptr, nullptr, fsched, nullptr, &last);
-        launch_sptrsv_bwd(c, M.dF, M.w.p, z.p, false, nullptr, nullptr, nullptr, &last);
+        launch_sptrsv_bwd(c, M.dF, M.w.p, z.p, false, nullptr, nullptr, nullptr, &last, nullptr, true);
     });
     out->bwd_ms = pair_ms - out->fwd_ms;
-    out->bwd_bytes = 12.0 * l + 4.0 * (Nn + 1) + 4.0 * Nn + 8.0 * Nn /*D*/ + 8.0 * Nn /*w in*/ + 8.0 * Nn /*w out*/ +
-                     8.0 * Nn /*y*/;
+    // w out: the upper rounds' rows only (wdead: round 0, the last round, writes y and not w)
+    out->bwd_bytes = 12.0 * l + 4.0 * (Nn + 1) + 4.0 * Nn + 8.0 * Nn /*D*/ + 8.0 * Nn /*w in*/ +
+                     8.0 * (Nn - (double)M.dF.bwd_dead_w_rows()) /*w out*/ + 8.0 * Nn /*y*/;
     out->apply_ms = timeit([&]() { M.apply(x.p, M.n, z.p, nullptr); });
     out->apply_bytes = M.apply_bytes();
     out->fwd_launches = out->bwd_launches = (int64_t)M.dF.round_ptr.size() - 1;
