@@ -1705,7 +1705,7 @@ __device__ __forceinline__ void pack_inputs(const PackArgs &pk, int64_t e) {
 // fused residual, bwd, bwd accumulating][block] (tools/blk_cycles.py: the round-0 cost model),
 // then the upper rounds' phases [fwd, bwd][staging, fold, levels, write-back][block]
 // (tools/upper_cycles.py)
-constexpr int kBlkCycMax = 1 << 17;
+constexpr int kBlkCycMax = 1 << 20;  // round 0: keyed by the block's first level (BlkMeta::l0)
 __device__ uint64_t g_blk_cyc[12 * kBlkCycMax];
 #define CPK_UP_STAMP(k)                                                                          \
     do {                                                                                       \
@@ -2314,8 +2314,8 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
             }
         }
 #ifdef CPK_PIPE_STAMPS
-        if (SPLIT == 1 && tid == 0 && !asg && b < kBlkCycMax)
-            g_blk_cyc[(BWD ? (ADD ? 3 : 2) : (RES ? 1 : 0)) * kBlkCycMax + b] = (uint64_t)clock64() - tb;
+        if (SPLIT == 1 && tid == 0 && cur.l0 < kBlkCycMax)  // keyed by l0: valid under the assignment too
+            g_blk_cyc[(BWD ? (ADD ? 3 : 2) : (RES ? 1 : 0)) * kBlkCycMax + cur.l0] = (uint64_t)clock64() - tb;
 #endif
         if (bn >= bend) break;
         __syncthreads();

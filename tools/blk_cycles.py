@@ -36,10 +36,11 @@ M.nitref, M.force_itref = 1, True
 z = np.random.default_rng(1).standard_normal(M.n)
 for _ in range(3):
     _ = M * z
-buf = np.zeros(4 * 131072, np.uint64)
+KMAX = 1 << 20  # kBlkCycMax: round-0 cycles are keyed by the block's first level
+buf = np.zeros(4 * KMAX, np.uint64)
 got = C.c_int64(0)
 _lib.check(_lib.lib.cpk_debug_blk_cycles(buf.ctypes.data_as(C.POINTER(C.c_uint64)), buf.size, C.byref(got)))
-cyc = buf.reshape(4, 131072)[:, :nb].astype(np.float64)
+cyc = buf.reshape(4, KMAX)[:, bl[:nb]].astype(np.float64)
 np.savez(os.path.join(os.environ.get("OUT", "gpurun_out"), "blk_cycles.npz"), cyc=cyc, rows=rows, nl=nl, fe=fe, be=be,
          ke=ke)
 names = ["fwd", "fwd_resid", "bwd", "bwd_add"]
@@ -53,6 +54,11 @@ for v in range(4):
     coef, *_ = np.linalg.lstsq(X, y, rcond=None)
     pred = X @ coef
     r2 = 1 - np.sum((y - pred) ** 2) / np.sum((y - y.mean()) ** 2)
+    # the levels-only model the assignment uses (kR0Cost): its R^2 for comparison
+    c1, *_ = np.linalg.lstsq(X[:, :2], y, rcond=None)
+    r2l = 1 - np.sum((y - X[:, :2] @ c1) ** 2) / np.sum((y - y.mean()) ** 2)
+    print(json.dumps({"variant": names[v], "levels_only_coef": [round(float(c), 2) for c in c1],
+                      "levels_only_r2": round(float(r2l), 3)}), flush=True)
     print(json.dumps({"variant": names[v], "blocks": nb, "mean_cycles": round(float(y.mean()), 1),
                       "cv": round(float(y.std() / y.mean()), 3), "coef[1,nl,rows,ent(,kps)]": [round(float(c), 2) for c in coef],
                       "r2": round(float(r2), 3), "p99_resid_frac": round(float(np.percentile(np.abs(y - pred) / y.mean(), 99)), 3)}),
