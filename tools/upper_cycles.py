@@ -16,7 +16,7 @@ import cpkrylov_amd as cpk  # noqa: E402
 from cpkrylov_amd import _lib  # noqa: E402
 from cpkrylov_amd.synthetic import saddle_system  # noqa: E402
 
-KMAX = 1 << 17
+KMAX = 1 << 20  # kBlkCycMax (kernels.hip)
 S = saddle_system(int(os.environ.get("N", "10000000")))
 H = cpk.analyze(S["G"], S["B"], -S["C"])
 rp, bl, lr, order, L = H["round_ptr"], H["blk_lvl"], H["lvl_row"], H["order"], H["L"]
