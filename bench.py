@@ -266,6 +266,10 @@ def main(argv=None):
                                           "(upper rounds): one LDL' solve (forward + backward sweep, all rounds)",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "bytes_per_launch": sweep_bytes,
+                # y = LDL^-1 x with y the output: since r04 v13 round 0 no longer stores the dead
+                # work vector, which the byte model dropped (8 B per round-0 row); the fraction on
+                # the r03/r04-v12 model (the solve's bytes plus that store) keeps rounds comparable
+                "frac_prev_model": round(gbs(sweep_bytes + prof.bwd_dead_store_bytes, sweep_ms) / HBM_PEAK_GBS, 4),
                 "avg_ms": round(sweep_ms, 5), "launches": int(prof.fwd_launches) + int(prof.bwd_launches)}
     # the metric's "SpMV GB/s": the saddle-point SpMV inside every M*z (refinement residual)
     spmv_achieved = gbs(prof.resid_bytes, prof.resid_ms)

@@ -44,7 +44,7 @@ class Profile(C.Structure):
     _fields_ = [(k, C.c_double) for k in ("spmv_ms", "spmv_bytes", "resid_ms", "resid_bytes", "fwd_ms", "fwd_bytes",
                                           "bwd_ms", "bwd_bytes", "apply_ms", "apply_bytes")] + \
                [("fwd_launches", C.c_int64), ("bwd_launches", C.c_int64)] + \
-               [("fwd_resid_ms", C.c_double), ("fwd_resid_bytes", C.c_double)]
+               [("fwd_resid_ms", C.c_double), ("fwd_resid_bytes", C.c_double), ("bwd_dead_store_bytes", C.c_double)]
 
 
 P = C.POINTER

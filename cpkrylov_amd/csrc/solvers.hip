@@ -2110,6 +2110,7 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
     // w out: the upper rounds' rows only (wdead: round 0, the last round, writes y and not w)
     out->bwd_bytes = 12.0 * l + 4.0 * (Nn + 1) + 4.0 * Nn + 8.0 * Nn /*D*/ + 8.0 * Nn /*w in*/ +
                      8.0 * (Nn - (double)M.dF.bwd_dead_w_rows()) /*w out*/ + 8.0 * Nn /*y*/;
+    out->bwd_dead_store_bytes = 8.0 * (double)M.dF.bwd_dead_w_rows();
     out->apply_ms = timeit([&]() { M.apply(x.p, M.n, z.p, nullptr); });
     out->apply_bytes = M.apply_bytes();
     out->fwd_launches = out->bwd_launches = (int64_t)M.dF.round_ptr.size() - 1;

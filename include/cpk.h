@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CPK_ABI_VERSION 2
+#define CPK_ABI_VERSION 3
 
 typedef enum {
     CPK_OK = 0,
@@ -290,6 +290,9 @@ typedef struct {
     int64_t fwd_launches, bwd_launches;
     double fwd_resid_ms, fwd_resid_bytes;  /* refinement input fused into the forward sweep: r = x - Kp*y,
                                               then w = L \ P'r (0 when the apply does not fuse it) */
+    double bwd_dead_store_bytes;     /* (ABI 3) bytes of the work-vector store the profiled backward
+                                        sweep skips (round 0's w, dead after the sweep): not in
+                                        bwd_bytes; the r03 byte model counted them */
 } cpk_profile;
 int cpk_profile_kernels(cpk_ctx ctx, cpk_mat A, cpk_mat C, cpk_pc M, int reps, cpk_profile *out);
 

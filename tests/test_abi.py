@@ -22,7 +22,7 @@ def test_every_declared_symbol_is_exported():
 
 
 def test_abi_version():
-    assert _lib.lib.cpk_abi_version() == 2
+    assert _lib.lib.cpk_abi_version() == 3
 
 
 def test_symgivens_host_entry():
