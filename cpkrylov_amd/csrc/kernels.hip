@@ -77,9 +77,12 @@ void make_dmat(const HCsr &a, DMat &d) {
 #ifndef CPK_R0_DATAFLOW
 #define CPK_R0_DATAFLOW 1
 #endif
-#ifndef CPK_R0_DF_CH
-#define CPK_R0_DF_CH 2
+#ifndef CPK_R0_DF_CH_FWD
+#define CPK_R0_DF_CH_FWD 2
 #endif
+#ifndef CPK_R0_DF_CH_BWD
+#define CPK_R0_DF_CH_BWD 1  // backward rows of round 0 carry ~2 in-block terms: 1 per iteration
+#endif                      // (profiles/r04_r0_bwd_ch_ab_v15.txt: 3 / 4 terms slower, 1 forward slower)
 // the dataflow level loop (levels_dataflow) where mark_dataflow picks it; terms per iteration;
 // the modelled cost of one of its trips relative to a level-loop trip: 2.0 for the first loop
 // (8 terms, a row-switch loop, short-circuit flag reads), 1.0 since the mask walk, the
@@ -2286,7 +2289,7 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
         // lane-owned rows for the backward sweep only: A/B at S10 (profiles/r03_level_ab_v2.txt),
         // backward 193.9 -> 186.7 us, but forward 211 -> 232 us and the fused forward 270 -> 286
         if (CPK_R0_DATAFLOW && (CPK_R0_DATAFLOW == 1 || !BWD) && SPLIT == 1 && TPB == kWave)
-            levels_dataflow<BWD, CPK_R0_DF_CH, false, R / kWave>(S, nr, R, ne, tid);
+            levels_dataflow<BWD, BWD ? CPK_R0_DF_CH_BWD : CPK_R0_DF_CH_FWD, false, R / kWave>(S, nr, R, ne, tid);
         else if (CPK_LEVEL_OWN && SPLIT == 1 && BWD) levels_owned<TPB, RPT, BWD, CPK_PIPE_CH>(S, nl, nr, skip0 != 0, tid);
         else if (CPK_LEVEL_GROUP && SPLIT == 1 && TPB == kWave && !BWD) levels_grouped_fwd<CPK_PIPE_CH>(S, nl, skip0 != 0, tid);
         else sweep_levels<TPB, BWD, false, CPK_PIPE_CH, false, true>(S, nl, skip0 != 0, tid);
