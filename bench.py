@@ -65,6 +65,11 @@ def parse(argv=None):
     ap.add_argument("--dist1", action="store_true",
                     help="with --dist: engine option dist1, the distributed kernels at one rank (diagnostic)")
     ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-exact", action="store_true",
+                    help="skip the exact_dots block (the same solve with order-independent inner products, "
+                         "timed, and compared bit for bit with the oracle's exact mode)")
+    ap.add_argument("--no-w64", action="store_true",
+                    help="skip the w64 block (the S10 system with SURVEY 8d's +-64 B window, measured by a child run)")
     ap.add_argument("--rhs-perturb", type=float, default=0.0,
                     help="scale the rhs by (1 + eps*u), u uniform in [-1, 1] (sensitivity runs; never the bench line)")
     ap.add_argument("--perturb-seed", type=int, default=1)
@@ -290,6 +295,9 @@ def main(argv=None):
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not distributed:
         cpu, parity = cpu_baseline(S, b1.cpu().numpy(), M, args, hist_gpu, niters_last)
+    exact = None
+    if rank == 0 and world == 1 and not distributed and not args.no_exact:
+        exact = exact_block(ctx, S, M, step, st, hist, xy, b1, args, iters / dt)
     pmc = None
     if rank == 0 and world == 1 and not args.no_pmc and not distributed and args.config == "s10":
         pmc = pmc_traffic(args)
@@ -339,7 +347,10 @@ def main(argv=None):
             "cpu_baseline": cpu,
             "pmc": pmc,
             "parity": parity,
+            "exact_dots": exact,
         }
+        if world == 1 and not distributed and args.config == "s10" and args.window == 4 and not args.no_w64:
+            line["w64"] = w64_block(args)
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
@@ -437,6 +448,79 @@ def cpu_baseline(S, b1, M_gpu, args, hist_gpu, niters_gpu):
                             "the OpenMP leg and of two rhs perturbed by 1e-15 relative; tolerance = "
                             "max(1e-8, 10 x band) (tests/test_gpu_parity.py)"}
     return cpu, parity
+
+
+def exact_block(ctx, S, M, step, st, hist, xy, b1, args, value_default):
+    """The same method call with engine option exact_dots (every inner product the correctly
+    rounded exact sum of its TwoProd pairs, xacc.hpp): timed like the headline (its overhead is
+    the ratio), and compared BIT FOR BIT with the oracle's exact mode run on the product's own
+    factors -- niters, every history entry, x and y.  The oracle's OpenMP leg gives the serial
+    restatement's bits in this mode (tests/test_gpu_exact.py), so it runs on the granted cores."""
+    from oracle import oracle as O
+    ctx.set_option("exact_dots", 1)
+    try:
+        step()  # warm-up: the exact solver's graphs
+        ctx.synchronize()
+        reps = max(1, min(args.steps, 5))
+        t = time.perf_counter()
+        it = 0
+        for _ in range(reps):
+            it += step()
+        ctx.synchronize()
+        dt = time.perf_counter() - t
+        h_gpu = hist[:st.hist_len].copy()
+        xy_gpu = xy.cpu().numpy()
+        niters = int(st.niters)
+    finally:
+        ctx.set_option("exact_dots", 0)
+    L, D, perm = M.export_factors()
+    Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=(L, D, perm))
+    # residual_update off: the value object's dead SpMVs subtract zeros (SURVEY 8a-9a), same bits
+    Mo.set(nitref=args.opts["nitref"], itref_tol=args.opts["itref_tol"], force_itref=1.0, residual_update=0.0)
+    threads = host_cpu()["threads"]
+    O.set_threads(threads)
+    try:
+        t = time.perf_counter()
+        with O.exact():
+            x, y, so = O.method(args.method, b1.cpu().numpy(), S["Q"], S["C"], Mo, dict(args.opts, residual_update=False))
+        t_or = time.perf_counter() - t
+    finally:
+        O.set_threads(1)
+    ho = so["residHistory"]
+    xyo = np.concatenate([x, y])
+    same_h = len(ho) == len(h_gpu) and bool(np.array_equal(ho, h_gpu))
+    same_x = bool(np.array_equal(xyo, xy_gpu[:len(xyo)]))
+    v = it / dt
+    return {"value": round(v, 2), "unit": "iters/s", "ms_per_step": round(dt / reps * 1e3, 3),
+            "overhead_vs_default": round(value_default / v, 4) if v > 0 else None,
+            "parity": {"niters_gpu": niters, "niters_oracle": int(so["niters"]),
+                       "history_bitexact": same_h, "xy_bitexact": same_x,
+                       "pass": bool(niters == int(so["niters"]) and same_h and same_x),
+                       "oracle": f"oracle cp{args.method} in exact mode (orc_set_exact) on the product's exported "
+                                 f"factors, OpenMP {threads} threads ({t_or:.1f} s): the serial restatement's bits"}}
+
+
+def w64_block(args):
+    """SURVEY 8d's +-64 B window (nnz(L) ~ 40.9 M, elimination tree 255 deep): the same bench in
+    a child process (its own cpu_baseline sample, parity, PMC traffic), embedded as a block."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--window", "64", "--steps", str(args.steps), "--warmup",
+           str(args.warmup), "--cpu-seconds", str(min(args.cpu_seconds, 10.0)), "--no-w64"]
+    if args.no_pmc:
+        cmd.append("--no-pmc")
+    if args.no_cpu_baseline:
+        cmd.append("--no-cpu-baseline")
+    if args.no_exact:
+        cmd.append("--no-exact")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=420)
+    if r.returncode != 0:
+        return {"error": f"child exited {r.returncode}: {r.stderr[-400:]}"}
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    keep = ("value", "unit", "ms_per_step", "iters_per_step", "solved", "roofline", "spmv_roofline", "kernels",
+            "cpu_baseline", "pmc", "parity", "exact_dots", "setup_s")
+    out = {k: d.get(k) for k in keep}
+    out["config"] = d["config"]
+    return out
 
 
 PMC_REPS = 5

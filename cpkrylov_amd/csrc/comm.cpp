@@ -33,6 +33,9 @@ struct RcclComm : Comm {
     void allreduce_sum(double *buf, size_t n, hipStream_t s) override {
         nccl_check(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c, s), "ncclAllReduce");
     }
+    void allreduce_sum_i64(int64_t *buf, size_t n, hipStream_t s) override {
+        nccl_check(ncclAllReduce(buf, buf, n, ncclInt64, ncclSum, c, s), "ncclAllReduce");
+    }
     void allgather(const double *send, double *recv, size_t n, hipStream_t s) override {
         nccl_check(ncclAllGather(send, recv, n, ncclDouble, c, s), "ncclAllGather");
     }
@@ -75,6 +78,7 @@ struct NullComm : Comm {
     int rank, P;
     NullComm(int r, int p) : rank(r), P(p) {}
     void allreduce_sum(double *, size_t, hipStream_t) override {}
+    void allreduce_sum_i64(int64_t *, size_t, hipStream_t) override {}
     void allgather(const double *send, double *recv, size_t n, hipStream_t s) override {
         if (n) CPK_HIP(hipMemcpyAsync(recv + (size_t)rank * n, send, n * sizeof(double), hipMemcpyDeviceToDevice, s));
     }
@@ -128,6 +132,16 @@ struct SimComm : Comm {
         CPK_HIP(hipStreamSynchronize(s));
         g->barrier();
         launch_sum_slots(s, g->shared.p, g->P, n, buf);
+        CPK_HIP(hipStreamSynchronize(s));
+        g->barrier();
+    }
+    void allreduce_sum_i64(int64_t *buf, size_t n, hipStream_t s) override {
+        check(n);  // the shared buffer holds 8-byte words: the digits travel as their bits
+        int64_t *sh = reinterpret_cast<int64_t *>(g->shared.p);
+        CPK_HIP(hipMemcpyAsync(sh + rank * n, buf, n * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+        CPK_HIP(hipStreamSynchronize(s));
+        g->barrier();
+        launch_sum_slots_i64(s, sh, g->P, n, buf);
         CPK_HIP(hipStreamSynchronize(s));
         g->barrier();
     }

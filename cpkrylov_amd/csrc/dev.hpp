@@ -64,6 +64,8 @@ struct DBuf {
 struct Comm {
     virtual ~Comm() = default;
     virtual void allreduce_sum(double *buf, size_t n, hipStream_t s) = 0;
+    // integer sums (exact_dots: the superaccumulator digits of every rank, xacc.hpp)
+    virtual void allreduce_sum_i64(int64_t *buf, size_t n, hipStream_t s) = 0;
     virtual void allgather(const double *send, double *recv, size_t n, hipStream_t s) = 0;
     virtual bool capturable() const = 0;  // may be captured into a hipGraph
     virtual bool has_peers() const { return true; }  // false: the timing stand-in (no exchange)
@@ -119,6 +121,10 @@ struct EngineOpts {
     bool dist_graph = true;       // dist_graph:         capture collectives in the graphs
     bool dist1 = false;           // dist1:              a 1-rank communicator runs the distributed path
                                   //                     (diagnostic; set before building operators)
+    bool exact_dots = false;      // exact_dots:         every inner product the correctly rounded exact sum
+                                  //                     of its TwoProd pairs (xacc.hpp): order-independent,
+                                  //                     the oracle's orc_set_exact values bit for bit; the
+                                  //                     one option that changes results (last bits)
     int batch = 0;                // batch:              fixed iterations per graph (0: adaptive)
     bool profile_fwd_sched = false;     // profile_fwd_sched: diagnostic, the profiled forward reads its input in schedule order
 };
@@ -144,13 +150,20 @@ struct Ctx {
     DBuf<double> partials;   // per-workgroup partial sums of the grid reductions
     DBuf<unsigned> counter;  // arrival tickets
     DBuf<double> red;        // distributed mode: local sums awaiting the allreduce
+    // exact_dots: sub-accumulators of the exact reductions (zero between launches) and, in
+    // distributed mode, the digits awaiting the int64 allreduce (xacc.hpp)
+    DBuf<int64_t> xsub, xred;
     Comm *comm = nullptr;    // owned by the C-ABI context object
     // the distributed path: a communicator of more than one rank.  A 1-rank communicator has
     // nothing to exchange and runs the single-GPU path (the same bits) unless engine option
     // dist1 asks for the distributed kernels (tests; DESIGN.md section 7's 1-rank comparison).
     // The timing stand-in (NullComm) declares nranks > 1.
     bool dist() const { return comm != nullptr && (nranks > 1 || opts.dist1); }
+    bool exact() const { return opts.exact_dots; }
+    // reduction workspace for grids of up to `count` partial sums (and, in exact mode, the
+    // sub-accumulators of at least 4 sums); ensure_xacc: room for `nsums` exact sums per launch
     void ensure_partials(size_t count);
+    void ensure_xacc(size_t nsums);
 };
 
 // HBM-resident CSR with a row-block partition for the LDS-staged streaming SpMV.
@@ -329,6 +342,7 @@ void simgroup_destroy(SimGroup *g);
 Comm *make_sim_comm(SimGroup *g, int rank);
 Comm *make_null_comm(int rank, int nranks);  // diagnostic timing stand-in (cpk_ctx_create_null)
 void launch_sum_slots(hipStream_t s, const double *slots, int P, size_t n, double *out);
+void launch_sum_slots_i64(hipStream_t s, const int64_t *slots, int P, size_t n, int64_t *out);
 struct DSep;
 // pack this rank's separator payload (w rows read by T, rank 0: +-x at the T dofs), allgather
 // t = x_eff - g with x_eff[i] = (i >= neg_from ? -x[i] : x[i])  (the GHN residual update)
@@ -456,6 +470,9 @@ void dsep_stage(DSep &T, const RankPlan &rp);
 // a DFactor over the combined vector [payload (P * kt); T]; forced by the engine option
 // tsolve_sweep, else used when the stepped solve does not fit one workgroup.
 void dsep_sweep_setup(Ctx &c, DSep &T, const RankPlan &rp, int P);
+// the stepped separator solve can hold T on this device (kernels.hip; the same predicate at
+// setup and at launch)
+bool sep_steps_fit(const DSep &S);
 struct DofMap;
 
 struct Precond {

@@ -22,6 +22,10 @@ struct RedBuf {
     unsigned *counter;  // zero between launches (the last workgroup resets it)
     double *defer = nullptr;  // distributed mode: the last workgroup stores the local sums here
                               // instead of running the epilogue (it runs after the allreduce)
+    // exact mode (xacc.hpp, engine option exact_dots): the sums' sub-accumulators
+    // [kXSub][NV][kXW] (zero between launches), and the distributed mode's digit output [NV][kXW]
+    int64_t *xsub = nullptr;
+    int64_t *xdefer = nullptr;
 };
 
 __device__ __forceinline__ double wave_sum(double v) {

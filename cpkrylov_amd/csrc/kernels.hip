@@ -17,6 +17,7 @@
 #include "devutil.hpp"
 #include "dist.hpp"
 #include "spmv.hpp"
+#include "xacc.hpp"
 
 namespace cpk {
 
@@ -28,6 +29,33 @@ void Ctx::ensure_partials(size_t count) {
         counter.alloc(kTicketWords);
         CPK_HIP(hipMemset(counter.p, 0, counter.bytes()));
     }
+    if (exact()) ensure_xacc(4);
+}
+
+void Ctx::ensure_xacc(size_t nsums) {
+    if (xsub.n < (size_t)kXSub * kXW * nsums) {
+        xsub.alloc((size_t)kXSub * kXW * nsums);
+        CPK_HIP(hipMemset(xsub.p, 0, xsub.bytes()));  // the launches leave them zero
+    }
+    if (dist() && xred.n < (size_t)kXW * nsums) xred.alloc((size_t)kXW * nsums);
+}
+
+// the rounded global sums of the exact digits: out[j] = xround(dig[j]) on every rank
+__global__ void xround_kernel(int64_t *dig, int nv, double *out) {
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nv; j += gridDim.x * blockDim.x)
+        out[j] = xround(dig + (size_t)j * kXW);  // normalises the (allreduced, dead) digits in place
+}
+
+void allreduce_red(Ctx &c, int nv) {
+    if (!c.exact()) {
+        c.comm->allreduce_sum(c.red.p, (size_t)nv, c.stream);
+        return;
+    }
+    if ((size_t)nv > c.red.n || (size_t)nv * kXW > c.xred.n)
+        throw Error(CPK_ERR_UNSUPPORTED, "exact reduction wider than its buffers");
+    c.comm->allreduce_sum_i64(c.xred.p, (size_t)nv * kXW, c.stream);
+    hipLaunchKernelGGL(xround_kernel, dim3(1), dim3(256), 0, c.stream, c.xred.p, nv, c.red.p);
+    CPK_HIP(hipGetLastError());
 }
 
 // ---- device matrix layout -------------------------------------------------------------------
@@ -165,9 +193,7 @@ void mark_dataflow(std::vector<int32_t> &meta, const std::vector<int64_t> &round
                    int mode) {
     if (!CPK_UPPER_DATAFLOW || round_ptr.size() < 3 || mode == 1) return;
     const int64_t b0 = round_ptr[1], b1 = round_ptr.back();  // the upper rounds
-    // CPK_DF_ALPHA (diagnostic, tools/gpu_steps.sh A/B runs): the trip cost the model uses
-    static const double alpha = getenv("CPK_DF_ALPHA") ? atof(getenv("CPK_DF_ALPHA")) : kDataflowTripCost;
-    std::vector<float> ratio((size_t)(b1 - b0) * 2, 0.f);
+    const double alpha = kDataflowTripCost;
     parallel_for(b1 - b0, [&](int64_t lo, int64_t hi) {
         std::vector<int32_t> lb;
         std::vector<int> nterm;
@@ -208,24 +234,10 @@ void mark_dataflow(std::vector<int32_t> &meta, const std::vector<int64_t> &round
                 }
                 const int64_t lt = level_trips(lb, byl, dir ? CPK_UPPER_CH_BWD : CPK_UPPER_CH_FWD);
                 const int64_t dt = dataflow_trips(terms, dir == 1, CPK_DF_CH(dir == 1), (int64_t)(4 * lt) + 8);
-                ratio[(size_t)(b - b0) * 2 + dir] = (float)lt / (float)std::max<int64_t>(dt, 1);
                 if (mode == 2 || alpha * (double)dt < (double)lt) m[3] |= dir ? kMetaDfBwd : kMetaDfFwd;
             }
         }
     }, 4);
-    if (getenv("CPK_DEBUG_DATAFLOW")) {  // diagnostic: blocks per direction on the dataflow loop
-        int64_t nf = 0, nb = 0;
-        for (int64_t b = b0; b < b1; b++) nf += (meta[(size_t)b * 8 + 3] & kMetaDfFwd) != 0, nb += (meta[(size_t)b * 8 + 3] & kMetaDfBwd) != 0;
-        fprintf(stderr, "dataflow: %lld upper blocks, forward %lld, backward %lld (trip cost %.2f)\n", (long long)(b1 - b0),
-                (long long)nf, (long long)nb, alpha);
-        for (int dir = 0; dir < 2; dir++) {  // level-loop trips / dataflow trips, quantiles
-            std::vector<float> q;
-            for (int64_t b = 0; b < b1 - b0; b++) q.push_back(ratio[(size_t)b * 2 + dir]);
-            std::sort(q.begin(), q.end());
-            fprintf(stderr, "  %s lt/dt: p10 %.2f p50 %.2f p90 %.2f max %.2f\n", dir ? "bwd" : "fwd", q[q.size() / 10],
-                    q[q.size() / 2], q[q.size() * 9 / 10], q.back());
-        }
-    }
 }
 
 constexpr int64_t kInsertionSortMax = 32;  // rows up to this long sort by insertion (keys are distinct)
@@ -373,6 +385,8 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
     d.perm.upload(f.perm);
     d.nblk = (int64_t)s.blk_row.size() - 1;
     d.nlvl = (int64_t)s.lvl_row.size() - 1;
+    // the block records keep a level index and two flag bits in one int32 (kMetaL1Mask)
+    if (d.nlvl > kMetaL1Mask) throw Error(CPK_ERR_UNSUPPORTED, "more sweep levels than the block records can index");
     std::vector<int32_t> bl(s.blk_lvl.begin(), s.blk_lvl.end()), lr(s.lvl_row.begin(), s.lvl_row.end());
     d.blk_lvl.upload(bl);
     d.lvl_row.upload(lr);
@@ -472,6 +486,7 @@ struct EpiResidSched {  // r(k) = xin(perm(k)) - (A y)(k), A and y in schedule o
     __device__ void row(int64_t i, double acc, double xi) { r[i] = xi - acc; }
     __device__ void finish() {}
 };
+template <class A = double>
 struct EpiResidNorm {
     const double *xin;
     int64_t neg_from;
@@ -480,19 +495,24 @@ struct EpiResidNorm {
     int *active_out;
     RedBuf rb;
     const int *run, *active;
-    double rr = 0.0, xx = 0.0;
+    A rr{}, xx{};
+    static constexpr int kWaves = std::is_same<A, XAcc>::value ? 4 : CPK_SPMV_WAVES;
     __device__ bool skip() const { return cpk::skip(run, active); }
-    __device__ const double *xvec(const double *x) const { return x; }
+    __device__ const double *xvec(const double *x) {
+        acc_init(rr, rb.xsub, 0, 2), acc_init(xx, rb.xsub, 1, 2);
+        return x;
+    }
     __device__ double pre(int64_t i) const { return xin[i]; }
     __device__ void row(int64_t i, double acc, double xi) {
         if (i >= neg_from) xi = -xi;
         double ri = xi - acc;
         r[i] = ri;
-        rr += ri * ri;
-        xx += xi * xi;
+        dadd(rr, ri, ri);
+        dadd(xx, xi, xi);
     }
     __device__ void finish() {
-        double v[2] = {rr, xx}, tot[2];
+        A v[2] = {rr, xx};
+        double tot[2];
         if (grid_sum<2>(v, rb, tot) && threadIdx.x == 0) {
             // while nit < nitref & (rNorm >= itref_tol * xNorm | force_itref)   (opLDL2.m:183)
             double rNorm = sqrt(tot[0]), xNorm = sqrt(tot[1]);
@@ -560,6 +580,20 @@ void launch_sum_slots(hipStream_t st, const double *slots, int P, size_t n, doub
     CPK_HIP(hipGetLastError());
 }
 
+__global__ void sum_slots_i64_kernel(const int64_t *__restrict__ slots, int P, int64_t n, int64_t *__restrict__ out) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+        int64_t s = slots[j];
+        for (int q = 1; q < P; q++) s += slots[(int64_t)q * n + j];
+        out[j] = s;
+    }
+}
+void launch_sum_slots_i64(hipStream_t st, const int64_t *slots, int P, size_t n, int64_t *out) {
+    if (!n) return;
+    const int grid = (int)std::min<size_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(sum_slots_i64_kernel, dim3(grid), dim3(256), 0, st, slots, P, (int64_t)n, out);
+    CPK_HIP(hipGetLastError());
+}
+
 void launch_spmv(Ctx &c, const DMat &A, const double *x, double *y, const int *run) {
     launch_halo(c, A, x);
     if (!A.nblk) return;
@@ -608,12 +642,17 @@ void launch_spmv_resid_norm(Ctx &c, const DMat &A, const double *xin, int64_t ne
     const bool dist = c.dist();
     if (A.nblk) {
         c.ensure_partials((size_t)A.nblk * 2);
-        EpiResidNorm e{xin, neg_from, r, tol, active_out, RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr},
-                       run, active};
-        spmv_launch(c, A, y, 0, e);
+        const RedBuf rb = red_buf(c);
+        if (c.exact())
+            spmv_launch(c, A, y, 0, EpiResidNorm<XAcc>{xin, neg_from, r, tol, active_out, rb, run, active});
+        else
+            spmv_launch(c, A, y, 0, EpiResidNorm<>{xin, neg_from, r, tol, active_out, rb, run, active});
+    } else if (dist) {  // no rows here: zero local sums
+        if (c.exact()) CPK_HIP(hipMemsetAsync(c.xred.p, 0, 2 * kXW * sizeof(int64_t), c.stream));
+        else CPK_HIP(hipMemsetAsync(c.red.p, 0, 2 * sizeof(double), c.stream));
     }
     if (dist) {
-        c.comm->allreduce_sum(c.red.p, 2, c.stream);
+        allreduce_red(c, 2);
         hipLaunchKernelGGL(resid_norm_fin_kernel, dim3(1), dim3(64), 0, c.stream, (const double *)c.red.p, tol,
                            active_out, run, active);
         CPK_HIP(hipGetLastError());
@@ -1042,6 +1081,7 @@ void dsep_sweep_setup(Ctx &c, DSep &T, const RankPlan &rp, int P) {
     fval.resize(fval.size() + kFactorPadEntries, 0.0), bval.resize(bval.size() + kFactorPadEntries, 0.0);
     d.nblk = (int64_t)S.blk_row.size() - 1;
     d.nlvl = (int64_t)S.lvl_row.size() - 1;
+    if (d.nlvl > kMetaL1Mask) throw Error(CPK_ERR_UNSUPPORTED, "more sweep levels than the block records can index");
     std::vector<int32_t> bl(S.blk_lvl.begin(), S.blk_lvl.end()), lr(S.lvl_row.size());
     for (size_t i = 0; i < lr.size(); i++) lr[i] = (int32_t)(base + S.lvl_row[i]);
     std::vector<int32_t> meta((size_t)d.nblk * 8);
@@ -1138,22 +1178,35 @@ __global__ void tsep_out_kernel(int nT, const int32_t *__restrict__ q, const dou
     }
 }
 
-void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active,
-                      const int32_t *hslot, double *hbuf, const int32_t *tkr_ptr, const int32_t *tkr_col,
-                      const double *tkr_val, const double *tkr_yT) {
-    if (!tkr_yT) tkr_yT = wT;
-    if (S.nT == 0) return;
+// LDS of the stepped separator solve: up to 64 KB always, up to kTsolveMaxLds when the device
+// grants the kernels that much dynamic LDS (asked once)
+bool sep_lds_fits(size_t bytes) {
     static const bool lds_attr = [] {
         return hipFuncSetAttribute((const void *)tsolve_steps_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)kTsolveMaxLds) == hipSuccess &&
                hipFuncSetAttribute((const void *)tsolve_steps_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)kTsolveMaxLds) == hipSuccess;
     }();
-    auto fits = [&](size_t b) { return b && (b <= 64 * 1024 || lds_attr); };
-    const bool grec = S.tsolve_global || !fits(S.lds);  // engine option: records in HBM
+    return bytes && (bytes <= 64 * 1024 || lds_attr);
+}
+
+// the stepped solve can run T: records staged in LDS, or (records in HBM: tsolve_global, or
+// staged records too large) the rest of its image -- one predicate for setup (precond.cpp: else
+// the T sweep is built) and launch (launch_sep_solve), so the two cannot disagree
+bool sep_steps_fit(const DSep &S) {
+    const bool grec = S.tsolve_global || !sep_lds_fits(S.lds);
+    return S.nrec > 0 && sep_lds_fits(grec ? S.lds_g : S.lds);
+}
+
+void launch_sep_solve(Ctx &c, const DSep &S, double *wT, double *y, bool add, const int *run, const int *active,
+                      const int32_t *hslot, double *hbuf, const int32_t *tkr_ptr, const int32_t *tkr_col,
+                      const double *tkr_val, const double *tkr_yT) {
+    if (!tkr_yT) tkr_yT = wT;
+    if (S.nT == 0) return;
+    const bool grec = S.tsolve_global || !sep_lds_fits(S.lds);  // engine option: records in HBM
     const size_t lds = grec ? S.lds_g : S.lds;
     const TkrArgs tkr{tkr_ptr, tkr_col, tkr_val, tkr_yT};  // y's T values (wT itself: this solve writes it last)
-    if (!S.tsweep && S.nrec > 0 && fits(lds)) {
+    if (!S.tsweep && sep_steps_fit(S)) {
         hipLaunchKernelGGL(tprefix_kernel, dim3((unsigned)((S.nT + 3) / 4)), dim3(256), 0, c.stream, (int)S.nT,
                            S.tk_ptr.p, S.tk_col.p, S.tk_val.p, S.tr_ptr.p, S.tr_col.p, S.tr_val.p, S.tr_slot.p,
                            S.tf_src.p, S.rbuf.p, S.pre.p, S.rec_v.p, run, active, tkr);
@@ -2556,6 +2609,7 @@ static bool fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
     if (defer && fuse_last_ok(F)) {  // the last round runs with the backward sweep
         *defer = FwdIn{xin, neg_from, sched_in, xs, true, R - 1};
         R -= 1;
+        packed = false;  // the deferred round's rows are packed by no launch here
     }
     const PackArgs none{};
     for (int64_t r = rfirst; r < R; r++) {

@@ -70,6 +70,7 @@ const BoolOpt kBool[] = {
     {"no_minres_fuse", &EngineOpts::no_minres_fuse},
     {"dist_graph", &EngineOpts::dist_graph},
     {"dist1", &EngineOpts::dist1},
+    {"exact_dots", &EngineOpts::exact_dots},
     {"profile_fwd_sched", &EngineOpts::profile_fwd_sched},
 };
 

@@ -437,7 +437,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     T.tf_src.upload(rp.tf_src), T.DT.upload(rp.DT), T.tdof.upload(rp.tdof);
     dsep_stage(T, rp);
     // a T the stepped solve cannot hold (LDS, step table) goes through the block sweeps
-    if (T.nT > 0 && (c.opts.tsolve_sweep || T.nrec == 0 || (T.lds == 0 && T.lds_g == 0))) dsep_sweep_setup(c, T, rp, c.nranks);
+    if (T.nT > 0 && (c.opts.tsolve_sweep || !sep_steps_fit(T))) dsep_sweep_setup(c, T, rp, c.nranks);
     T.sbuf.alloc((size_t)std::max<int64_t>(T.kt, 1));
     T.sbuf.zero(c.stream);
     T.rbuf.alloc((size_t)std::max<int64_t>(T.kt * c.nranks + (T.tsweep ? T.nT : 0), 1));

@@ -3,9 +3,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
 
 #include "dev.hpp"
 #include "devutil.hpp"
+#include "xacc.hpp"
 
 namespace cpk {
 
@@ -24,6 +26,7 @@ struct DState {
     int err;          // 1: indefinite (beta < -100 eps or negative squared norm)
     int flag;         // solver-specific flag (symmlq: moved to CG point)
     int64_t err_iter;
+    int exact;        // engine option exact_dots: norm([a b]) by xnorm2 (the oracle's formula)
     double err_val;
     double atol, rtol, btol, stopTol, bstopTol, residNorm;
     // Lanczos family
@@ -45,6 +48,11 @@ struct DState {
 __device__ __forceinline__ void push(double *h, int64_t &len, int64_t cap, double v) {
     if (len < cap) h[len] = v;
     len++;
+}
+
+// MATLAB norm([a b]) of a 2-vector (cpminres.m:218, cpsymmlq.m:239,291,324)
+__device__ __forceinline__ double norm2(const DState *st, double a, double b) {
+    return st->exact ? xnorm2(a, b) : hypot(a, b);
 }
 
 __device__ __forceinline__ double msign(double a) { return (double)((a > 0) - (a < 0)); }
@@ -85,12 +93,13 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(int64_t N, F f) {
 }
 
 // Elementwise + grid reduction of NV sums: F::operator()(i, acc), F::fin(tot) in the last workgroup.
-template <int NV, class F>
+// A: the accumulator (double: the default fixed-tree sums; XAcc: exact_dots, xacc.hpp).
+template <int NV, class F, class A = double>
 __global__ __launch_bounds__(kBlock) void ewred_kernel(int64_t N, F f, RedBuf rb) {
     if (!f.setup()) return;
-    double acc[NV];
+    A acc[NV];
 #pragma unroll
-    for (int j = 0; j < NV; j++) acc[j] = 0.0;
+    for (int j = 0; j < NV; j++) acc_init(acc[j], rb.xsub, j, NV);
     for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) f(i, acc);
     double tot[NV];
     if (grid_sum<NV>(acc, rb, tot) && threadIdx.x == 0) f.fin(tot);
@@ -108,12 +117,12 @@ __global__ __launch_bounds__(kBlock) void ewt_kernel(int64_t N, F f) {
          i0 += (int64_t)gridDim.x * kBlock * kTile)
         f.tile(i0, N);
 }
-template <int NV, class F>
+template <int NV, class F, class A = double>
 __global__ __launch_bounds__(kBlock) void ewtred_kernel(int64_t N, F f, RedBuf rb) {
     if (!f.setup()) return;
-    double acc[NV];
+    A acc[NV];
 #pragma unroll
-    for (int j = 0; j < NV; j++) acc[j] = 0.0;
+    for (int j = 0; j < NV; j++) acc_init(acc[j], rb.xsub, j, NV);
     for (int64_t i0 = blockIdx.x * (int64_t)kBlock * kTile + threadIdx.x; i0 < N;
          i0 += (int64_t)gridDim.x * kBlock * kTile)
         f.tile(i0, N, acc);
@@ -147,10 +156,12 @@ template <int NV, class F>
 inline void launch_ewred(Ctx &c, int64_t N, const F &f) {
     c.ensure_partials((size_t)ew_grid(N) * NV);
     const bool dist = c.dist();
-    hipLaunchKernelGGL((ewred_kernel<NV, F>), dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f,
-                       RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr});
+    if (c.exact())
+        hipLaunchKernelGGL((ewred_kernel<NV, F, XAcc>), dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f, red_buf(c));
+    else
+        hipLaunchKernelGGL((ewred_kernel<NV, F>), dim3(ew_grid(N)), dim3(kBlock), 0, c.stream, N, f, red_buf(c));
     if (dist) {
-        c.comm->allreduce_sum(c.red.p, NV, c.stream);
+        allreduce_red(c, NV);
         hipLaunchKernelGGL(ewred_fin_kernel<F>, dim3(1), dim3(64), 0, c.stream, f, (const double *)c.red.p);
     }
 }
@@ -168,10 +179,13 @@ template <int NV, class F>
 inline void launch_ewtred(Ctx &c, int64_t N, const F &f) {
     c.ensure_partials((size_t)ewt_grid(N) * NV);
     const bool dist = c.dist();
-    hipLaunchKernelGGL((ewtred_kernel<NV, F>), dim3(ewt_grid(N)), dim3(kBlock), 0, c.stream, N, f,
-                       RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr});
+    if (c.exact())
+        hipLaunchKernelGGL((ewtred_kernel<NV, F, XAcc>), dim3(ewt_grid(N)), dim3(kBlock), 0, c.stream, N, f,
+                           red_buf(c));
+    else
+        hipLaunchKernelGGL((ewtred_kernel<NV, F>), dim3(ewt_grid(N)), dim3(kBlock), 0, c.stream, N, f, red_buf(c));
     if (dist) {
-        c.comm->allreduce_sum(c.red.p, NV, c.stream);
+        allreduce_red(c, NV);
         hipLaunchKernelGGL(ewred_fin_kernel<F>, dim3(1), dim3(64), 0, c.stream, f, (const double *)c.red.p);
     }
 }
@@ -191,7 +205,7 @@ inline void launch_scalar(Ctx &c, const F &f) {
 #ifndef CPK_SPMV_NORM_WAVES
 #define CPK_SPMV_NORM_WAVES 5
 #endif
-template <class F>
+template <class F, class A = double>
 struct EpiKrylov {
     DState *st;
     const double *xsel;  // resolved input vector
@@ -199,14 +213,16 @@ struct EpiKrylov {
     int64_t n;
     RedBuf rb;
     F f;
-    double dn = 0.0, dm = 0.0;
-    static constexpr int kWaves = F::kNorm ? CPK_SPMV_NORM_WAVES : CPK_SPMV_WAVES;
+    A dn{}, dm{};
+    // exact mode: fewer waves (the two expansions take 12 VGPRs where the sums took 4)
+    static constexpr int kWaves = std::is_same<A, XAcc>::value ? 4 : (F::kNorm ? CPK_SPMV_NORM_WAVES : CPK_SPMV_WAVES);
     double nb = 0.0;          // F::kNorm: the divisor (0: none)
     double *xo = nullptr;     // F::kNorm: where the normalised input goes
     __device__ bool skip() { return f.skip(st); }
     __device__ const double *xvec(const double *base) {
         xsel = f.select(st, base);
         if constexpr (F::kNorm) nb = f.norm(st), xo = f.out(st);
+        acc_init(dn, rb.xsub, 0, 2), acc_init(dm, rb.xsub, 1, 2);
         return xsel;
     }
     __device__ double xl(double v) const {
@@ -218,11 +234,12 @@ struct EpiKrylov {
         y[r] = acc;
         if constexpr (F::kNorm)
             if (xo) xo[r] = xr;
-        if (r < n) dn += acc * xr;
-        else dm += acc * xr;
+        if (r < n) dadd(dn, acc, xr);
+        else dadd(dm, acc, xr);
     }
     __device__ void finish() {
-        double v[2] = {dn, dm}, tot[2];
+        A v[2] = {dn, dm};
+        double tot[2];
         if (grid_sum<2>(v, rb, tot) && threadIdx.x == 0) f.fin(st, tot);
     }
 };

@@ -76,7 +76,7 @@ struct PolLanczosSpmv {
             double den = st->gammabar;
             if (den == 0) den = epsmat;
             st->den = den;
-            st->lqresid = hypot(st->epsdelzeta, st->epsilonzeta);
+            st->lqresid = norm2(st, st->epsdelzeta, st->epsilonzeta);
             st->qrresid = st->snprod * st->beta1;
             st->cgresid = st->qrresid * st->beta / fabs(den);
             push(st->hist2, st->nh2, st->hcap, st->lqresid);
@@ -235,24 +235,30 @@ void launch_lanczos_step_halo(Ctx &c, const DMat &AC, DState *st, int64_t N, con
 
 // defer (distributed): leave the local partials in c.red for the caller to carry
 // halo_ready: the input's halo is already in AC.rbuf (launch_lanczos_step_halo)
+template <class P, class A>
+void launch_krylov_spmv_as(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n, const P &pol) {
+    using E = EpiKrylov<P, A>;
+    E e{st, nullptr, y, n, red_buf(c), pol};
+    const unsigned grid = AC.halo() ? spmv_grid<E, true>(AC.nblk) : spmv_grid<E, false>(AC.nblk);
+    if (AC.halo())
+        hipLaunchKernelGGL((spmv_stream<E, true>), dim3(grid), dim3(kBlock), 0, c.stream, AC.ptr.p, AC.col.p, AC.val.p,
+                           AC.blk.p, AC.nblk, (const double *)nullptr, (int64_t)0, e, (const double *)AC.rbuf.p,
+                           AC.nloc);
+    else
+        hipLaunchKernelGGL((spmv_stream<E, false>), dim3(grid), dim3(kBlock), 0, c.stream, AC.ptr.p, AC.col.p,
+                           AC.val.p, AC.blk.p, AC.nblk, (const double *)nullptr, (int64_t)0, e,
+                           (const double *)nullptr, (int64_t)0);
+}
 template <class P>
 void launch_krylov_spmv(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n, const P &pol, bool defer = false,
                         bool halo_ready = false) {
     const bool dist = c.dist();
+    if (defer && c.exact()) throw Error(CPK_ERR_ARGS, "internal: deferred Krylov partials in exact mode");
     if (AC.halo() && AC.kmax > 0 && !halo_ready) launch_krylov_halo(c, AC, st, pol);
-    EpiKrylov<P> e{st, nullptr, y, n, RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr}, pol};
-    const unsigned grid =
-        AC.halo() ? spmv_grid<EpiKrylov<P>, true>(AC.nblk) : spmv_grid<EpiKrylov<P>, false>(AC.nblk);
-    if (AC.halo())
-        hipLaunchKernelGGL((spmv_stream<EpiKrylov<P>, true>), dim3(grid), dim3(kBlock), 0, c.stream, AC.ptr.p,
-                           AC.col.p, AC.val.p, AC.blk.p, AC.nblk, (const double *)nullptr, (int64_t)0, e,
-                           (const double *)AC.rbuf.p, AC.nloc);
-    else
-        hipLaunchKernelGGL((spmv_stream<EpiKrylov<P>, false>), dim3(grid), dim3(kBlock), 0, c.stream, AC.ptr.p,
-                           AC.col.p, AC.val.p, AC.blk.p, AC.nblk, (const double *)nullptr, (int64_t)0, e,
-                           (const double *)nullptr, (int64_t)0);
+    if (c.exact()) launch_krylov_spmv_as<P, XAcc>(c, AC, st, y, n, pol);
+    else launch_krylov_spmv_as<P, double>(c, AC, st, y, n, pol);
     if (dist && !defer) {
-        c.comm->allreduce_sum(c.red.p, 2, c.stream);
+        allreduce_red(c, 2);
         hipLaunchKernelGGL(krylov_fin_kernel<P>, dim3(1), dim3(64), 0, c.stream, pol, st, (const double *)c.red.p);
     }
 }
@@ -329,13 +335,14 @@ struct LanczosStep {
         const double v = vk[i] - vprec[i];
         return v - alpha * vk[i] - beta * vkm1[i];
     }
-    __device__ void operator()(int64_t i, double *acc) {
+    template <class A>
+    __device__ void operator()(int64_t i, A *acc) {
         const double v = value(i);
         if (i < n) {
-            acc[0] += ut[i] * v;
+            dadd(acc[0], ut[i], v);
             if (KIND == 1) xy[i] = xy[i] + zeta * W[i];  // cpcglanczos.m:238 x = x + zeta*wv
         } else {
-            acc[1] += ut[i] * v;
+            dadd(acc[1], ut[i], v);
             if (KIND == 1) xy[i] = xy[i] - zeta * W[i];  // y = y - zeta*wq
         }
         vkp1[i] = v;
@@ -343,7 +350,8 @@ struct LanczosStep {
     }
     // kTile elements kBlock apart (ewtred_kernel): every load of the tile in flight at once; the
     // per-element arithmetic and the thread's accumulation order over its elements are unchanged
-    __device__ void tile(int64_t i0, int64_t Nn, double *acc) {
+    template <class A>
+    __device__ void tile(int64_t i0, int64_t Nn, A *acc) {
         if (i0 + (kTile - 1) * kBlock >= Nn) {
             for (int e = 0; e < kTile; e++)
                 if (i0 + e * kBlock < Nn) (*this)(i0 + e * kBlock, acc);
@@ -365,12 +373,12 @@ struct LanczosStep {
             double v;
             if (i < n) {
                 v = p[e] - alpha * a[e] - beta * b[e];
-                acc[0] += u[e] * v;
+                dadd(acc[0], u[e], v);
                 if (KIND == 1) xy[i] = xy[i] + zeta * W[i];
             } else {
                 const double t = a[e] - p[e];
                 v = t - alpha * a[e] - beta * b[e];
-                acc[1] += u[e] * v;
+                dadd(acc[1], u[e], v);
                 if (KIND == 1) xy[i] = xy[i] - zeta * W[i];
             }
             vkp1[i] = v;
@@ -378,7 +386,8 @@ struct LanczosStep {
     }
     // tile() with the fused MINRES update: all seven loads of the tile in flight at once; the
     // step's arithmetic and accumulation order as in tile(), the update's as in MinresUpdate
-    __device__ void tile_upd(int64_t i0, double *acc) {
+    template <class A>
+    __device__ void tile_upd(int64_t i0, A *acc) {
         double p[kTile], a[kTile], b[kTile], u[kTile], w1[kTile], w2[kTile], x[kTile];
 #pragma unroll
         for (int e = 0; e < kTile; e++) {
@@ -392,11 +401,11 @@ struct LanczosStep {
             double v;
             if (i < n) {
                 v = p[e] - alpha * a[e] - beta * b[e];
-                acc[0] += u[e] * v;
+                dadd(acc[0], u[e], v);
             } else {
                 const double t = a[e] - p[e];
                 v = t - alpha * a[e] - beta * b[e];
-                acc[1] += u[e] * v;
+                dadd(acc[1], u[e], v);
             }
             vkp1[i] = v;
             minres_wx(i, b[e], w1[e], w2[e], x[e]);
@@ -429,7 +438,7 @@ __device__ void LanczosStep<0>::fin(const double *tot) {
     const double gammabar = st->sn * st->deltabar - st->cs * st->alpha;
     st->epsln = st->sn * b;
     st->deltabar = -st->cs * b;
-    const double gamma = hypot(gammabar, b);
+    const double gamma = norm2(st, gammabar, b);
     const double cs = gammabar / gamma, sn = b / gamma;
     st->tau = cs * st->taubar;
     st->taubar = sn * st->taubar;
@@ -487,7 +496,7 @@ __device__ void LanczosStep<2>::fin(const double *tot) {
     const double b = sqrt(fabs(raw));
     st->beta = b;
     st->matnorm2 = st->matnorm2 + st->alpha * st->alpha + b * b + st->betaold * st->betaold;
-    const double gamma = hypot(st->gammabar, st->betaold);
+    const double gamma = norm2(st, st->gammabar, st->betaold);
     const double cs = st->gammabar / gamma, sn = st->betaold / gamma;
     const double delta = cs * st->deltabar + sn * st->alpha;
     st->gammabar = sn * st->deltabar - cs * st->alpha;
@@ -515,11 +524,12 @@ struct InitLanczos {
     double *v1, *v0, *z2, *xy;
     int64_t n;
     __device__ bool setup() { return true; }
-    __device__ void operator()(int64_t i, double *acc) {
+    template <class A>
+    __device__ void operator()(int64_t i, A *acc) {
         double v;
         if (i < n) {
             v = vprec[i];
-            acc[0] += b[i] * v;
+            dadd(acc[0], b[i], v);
         } else {
             v = -vprec[i];
         }
@@ -694,15 +704,16 @@ struct SymmlqPre {
         alpha = st->alpha;
         return true;
     }
-    __device__ void operator()(int64_t i, double *acc) {
+    template <class A>
+    __device__ void operator()(int64_t i, A *acc) {
         double v;
         if (i < n) {
             v = vprec[i] - alpha * vk[i];
-            acc[0] += ut[i] * v;
+            dadd(acc[0], ut[i], v);
         } else {
             v = vk[i] - vprec[i];
             v = v - alpha * vk[i];
-            acc[1] += ut[i] * v;
+            dadd(acc[1], ut[i], v);
         }
         vkp1[i] = v;
     }
@@ -738,7 +749,7 @@ struct SymmlqPostScalar {
         double den = st->gammabar;
         if (den == 0) den = epsmat;
         st->den = den;
-        st->lqresid = hypot(st->epsdelzeta, st->epsilonzeta);
+        st->lqresid = norm2(st, st->epsdelzeta, st->epsilonzeta);
         st->qrresid = st->snprod * st->beta1;
         push(st->hist2, st->nh2, st->hcap, st->lqresid);
         push(st->hist3, st->nh3, st->hcap, st->qrresid);
@@ -797,9 +808,10 @@ struct CgInit1 {  // p = -r; q = -u; residNorm2 = g'*r   (cpcg.m:126-133)
     double *PQ;
     int64_t n;
     __device__ bool setup() { return true; }
-    __device__ void operator()(int64_t i, double *acc) {
+    template <class A>
+    __device__ void operator()(int64_t i, A *acc) {
         PQ[i] = -RU[i];
-        if (i < n) acc[0] += GW[i] * RU[i];
+        if (i < n) dadd(acc[0], GW[i], RU[i]);
     }
     __device__ void fin(const double *tot) {
         st->k = 0;
@@ -836,13 +848,14 @@ struct CgResid {  // t = a + u; residNorm2_new = g'*r + t'*w   (cpcg.m:166-176)
     double *TT;
     int64_t n;
     __device__ bool setup() { return st->running != 0; }
-    __device__ void operator()(int64_t i, double *acc) {
+    template <class A>
+    __device__ void operator()(int64_t i, A *acc) {
         if (i < n) {
-            acc[0] += GW[i] * RU[i];
+            dadd(acc[0], GW[i], RU[i]);
         } else {
             const double t = XA[i] + RU[i];
             TT[i] = t;
-            acc[1] += t * GW[i];
+            dadd(acc[1], t, GW[i]);
         }
     }
     __device__ void fin(const double *tot) {
@@ -885,14 +898,15 @@ struct ArnoldiStart {
     int dq;             // DQGMRES: dot(u, V1) only (cpdqgmres.m:157)
     int first;          // first cycle: sets stopTol and pushes the history
     __device__ bool setup() { return true; }
-    __device__ void operator()(int64_t i, double *acc) {
+    template <class A>
+    __device__ void operator()(int64_t i, A *acc) {
         double v;
         if (i < n) {
             v = w[i];
-            acc[0] += ut[i] * v;
+            dadd(acc[0], ut[i], v);
         } else {
             v = restart_cycle ? xy[i] - w[i] : -w[i];
-            if (!dq) acc[1] += ut[i] * v;
+            if (!dq) dadd(acc[1], ut[i], v);
         }
         v1[i] = v;
     }
@@ -989,7 +1003,7 @@ __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double
                 if (g0 == 0) vnew[i] = i < n ? w[i] : vk[i] - w[i];
 #pragma unroll
                 for (int j = 0; j < kDotGroup; j++)
-                    if (vj[j]) acc[j] += vj[j][i] * u;
+                    if (vj[j]) dadd(acc[j], vj[j][i], u);
             }
         } else {
             for (int64_t i0 = blockIdx.x * (int64_t)kBlock * kDotTile + threadIdx.x; i0 < N;
@@ -1014,7 +1028,7 @@ __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double
                     if (g0 == 0) vnew[i] = i < n ? w[i] : vk[i] - w[i];
 #pragma unroll
                     for (int j = 0; j < kDotGroup; j++)
-                        if (vj[j]) acc[j] += x[e][j] * u[e];
+                        if (vj[j]) dadd(acc[j], x[e][j], u[e]);
                 }
             }
         }
@@ -1076,6 +1090,67 @@ __global__ __launch_bounds__(kBlock) void arnoldi_dots_kernel(DState *st, double
     }
 }
 
+// exact_dots: the same window sums, each exact (xacc.hpp).  One streaming pass per group of
+// kXDotGroup window vectors (an x-part and a y-part expansion per vector: 24 doubles at 4), the
+// workgroup's expansions deposited after each group, and the last workgroup rounds the 2 * nv
+// sums in chunks of 16 (an even count: a window pair stays in one chunk).  Sum index
+// 2 * (window position) + (0: x-part, 1: y-part) of 2 * maxv per launch.
+constexpr int kXDotGroup = 4;
+__global__ __launch_bounds__(kBlock) void arnoldi_dots_exact_kernel(DState *st, double *V, const double *w,
+                                                                    const double *ut, int64_t n, int64_t N,
+                                                                    int64_t ring, int64_t maxv, RedBuf rb) {
+    if (!st->running) return;
+    const Window win = window(st, ring);
+    const int64_t kk = win.kk;
+    double *vnew = V + (ring ? (kk % ring) : kk) * N;
+    const double *vk = V + win.slot(kk) * N;
+    const int nsum = (int)(2 * maxv);
+    for (int64_t g0 = 0; g0 < win.nv; g0 += kXDotGroup) {
+        XAcc acc[2 * kXDotGroup];  // [2q]: x-part of window vector g0 + q, [2q + 1]: y-part
+        const double *vj[kXDotGroup];
+#pragma unroll
+        for (int q = 0; q < kXDotGroup; q++) {
+            acc_init(acc[2 * q], rb.xsub, (int)(2 * (g0 + q)) % nsum, nsum);
+            acc_init(acc[2 * q + 1], rb.xsub, (int)(2 * (g0 + q) + 1) % nsum, nsum);
+            vj[q] = (g0 + q < win.nv) ? V + win.slot(win.jlo + g0 + q) * N : nullptr;
+        }
+        for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) {
+            const double u = ut[i];
+            if (g0 == 0) vnew[i] = i < n ? w[i] : vk[i] - w[i];
+#pragma unroll
+            for (int q = 0; q < kXDotGroup; q++)
+                if (vj[q]) {
+                    if (i < n) dadd(acc[2 * q], vj[q][i], u);
+                    else dadd(acc[2 * q + 1], vj[q][i], u);
+                }
+        }
+        block_deposit<2 * kXDotGroup>(acc);  // the unused tail of the last group deposits zeros
+    }
+    __shared__ int s_last;
+    if (threadIdx.x == 0) s_last = arrive_last(rb.counter);
+    __syncthreads();
+    if (!s_last) return;
+    __shared__ int64_t dig[16][kXW];
+    __shared__ double hv[16];
+    if (!rb.xdefer && ring && threadIdx.x == 0)  // fresh ring row for H(kk, .)
+        for (int64_t c = 1; c <= st->mem + 2; c++) Hd(st, kk, c) = 0.0;
+    for (int j0 = 0; j0 < 2 * win.nv; j0 += 16) {
+        const int ns = (int)min((int64_t)16, 2 * win.nv - j0);
+        gather_digits(rb.xsub, nsum, j0, ns, dig, rb.xdefer);
+        if (rb.xdefer) continue;
+        if (threadIdx.x < ns) hv[threadIdx.x] = xround(dig[threadIdx.x]);
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int q = 1; q < ns; q += 2) {
+                const int64_t jj = win.jlo + (j0 + q) / 2;
+                const double h = hv[q - 1] + hv[q];
+                if (ring) Hd(st, jj, 2 + kk - jj) = h;
+                else Hg(st, jj, kk) = h;
+            }
+        __syncthreads();
+    }
+}
+
 // distributed mode: H(j, k) from the allreduced window sums (same additions as above)
 __global__ void arnoldi_fin_kernel(DState *st, int64_t ring, const double *tot) {
     if (threadIdx.x || blockIdx.x || !st->running) return;
@@ -1108,10 +1183,14 @@ static void launch_arnoldi_dots(Ctx &c, DState *st, double *V, const double *w, 
         return occ * cus;
     }();
     const int grid = std::min(ew_grid(N), resident);
-    hipLaunchKernelGGL(arnoldi_dots_kernel, dim3(grid), dim3(kBlock), 0, c.stream, st, V, w, ut, n, N, ring, maxv,
-                       RedBuf{c.partials.p, c.counter.p, dist ? c.red.p : nullptr});
+    if (c.exact())
+        hipLaunchKernelGGL(arnoldi_dots_exact_kernel, dim3(grid), dim3(kBlock), 0, c.stream, st, V, w, ut, n, N, ring,
+                           maxv, red_buf(c));
+    else
+        hipLaunchKernelGGL(arnoldi_dots_kernel, dim3(grid), dim3(kBlock), 0, c.stream, st, V, w, ut, n, N, ring, maxv,
+                           red_buf(c));
     if (dist) {
-        c.comm->allreduce_sum(c.red.p, (size_t)(2 * maxv), c.stream);
+        allreduce_red(c, (int)(2 * maxv));
         hipLaunchKernelGGL(arnoldi_fin_kernel, dim3(1), dim3(64), 0, c.stream, st, ring, (const double *)c.red.p);
     }
 }
@@ -1154,7 +1233,8 @@ struct ArnoldiOrth {
     __device__ double h(int64_t j) const {
         return ring ? Hd(st, j, 2 + win.kk - j) : Hg(st, j, win.kk);
     }
-    __device__ void operator()(int64_t i, double *acc) {
+    template <class A>
+    __device__ void operator()(int64_t i, A *acc) {
         double v = vnew[i];
         if (tab.nv >= 0) {
 #pragma unroll 8
@@ -1163,11 +1243,13 @@ struct ArnoldiOrth {
             for (int64_t j = win.jlo; j <= win.kk; j++) v = v - h(j) * V[win.slot(j) * N + i];
         }
         vnew[i] = v;
-        acc[i < n ? 0 : 1] += ut[i] * v;
+        if (i < n) dadd(acc[0], ut[i], v);  // (no dynamic index: an XAcc array stays in registers)
+        else dadd(acc[1], ut[i], v);
     }
     // kTile elements i0 + e * kBlock (ewtred_kernel): the same operations per element; the
     // thread's partial sums take its elements in this tiled order (deterministic)
-    __device__ void tile(int64_t i0, int64_t Nn, double *acc) {
+    template <class A>
+    __device__ void tile(int64_t i0, int64_t Nn, A *acc) {
         if (tab.nv < 0 || i0 + (kTile - 1) * kBlock >= Nn) {
             for (int e = 0; e < kTile; e++)
                 if (i0 + e * kBlock < Nn) (*this)(i0 + e * kBlock, acc);
@@ -1187,7 +1269,8 @@ struct ArnoldiOrth {
         for (int e = 0; e < kTile; e++) {
             const int64_t i = i0 + e * kBlock;
             vnew[i] = v[e];
-            acc[i < n ? 0 : 1] += ut[i] * v[e];
+            if (i < n) dadd(acc[0], ut[i], v[e]);
+            else dadd(acc[1], ut[i], v[e]);
         }
     }
     __device__ void fin(const double *tot) {
@@ -1381,8 +1464,9 @@ struct AnyNonzero {  // any(b(n+1:n+m))
     int64_t n;
     int *out;
     __device__ bool setup() { return true; }
-    __device__ void operator()(int64_t i, double *acc) {
-        if (b[n + i] != 0) acc[0] = 1.0;
+    template <class A>
+    __device__ void operator()(int64_t i, A *acc) {
+        if (b[n + i] != 0) dadd(acc[0], 1.0, 1.0);  // a count: nonzero iff any
     }
     __device__ void fin(const double *tot) { *out = tot[0] != 0 ? 1 : 0; }
 };
@@ -1479,6 +1563,7 @@ struct SolveCore {
         if (h.itmax < 0) h.itmax = 0;
         h.atol = atol, h.rtol = rtol, h.btol = btol;
         h.hcap = hcap;
+        h.exact = c.exact() ? 1 : 0;
         ensure(hist, hcap);
         ensure(hist2, hcap);
         ensure(hist3, hcap);
@@ -1504,6 +1589,7 @@ struct SolveCore {
         need = std::max<size_t>(need, ewg * 2);
         need = std::max<size_t>(need, ewg * 2 * std::max<int64_t>(maxv, 1));
         c.ensure_partials(need);
+        if (c.exact()) c.ensure_xacc((size_t)std::max<int64_t>(2 * maxv, 4));
     }
 
     void pull() {
@@ -1682,7 +1768,8 @@ void SolveCore::minres_like(int kind, const double *b, double *xy, cpk_stats *st
         }
         // distributed: vprec = M*[u; -t] does not depend on alpha (cpminres.m:187-190), so alpha's
         // partials ride in the preconditioner's first separator allgather instead of an allreduce
-        const bool piggy = c.dist() && M.piggyback_ok() && !c.opts.no_piggy;
+        // exact mode: alpha's and beta's digits take their own int64 allreduce (no piggyback)
+        const bool piggy = c.dist() && M.piggyback_ok() && !c.opts.no_piggy && !c.exact();
         // and beta's partials ride in the next Lanczos vector's halo exchange (spare slots)
         const bool hmerge = piggy && AC.halo() && AC.kstride >= AC.kmax + 2 && !c.opts.no_halo_merge;
         // fused update: the Lanczos step leaves the new vector unnormalised in RAW and makes the

@@ -128,7 +128,162 @@ static void spmv(const orc_csr *a, const double *x, double *y) {
     );
 }
 
+/* ------------------------------------------------------------------------------------ */
+/* Exact inner products (orc_set_exact; the product's engine option exact_dots)           */
+/* ------------------------------------------------------------------------------------ */
+/* MATLAB's dot and norm go to MKL, whose summation order is unknown, so a
+ * plain sum matches the GPU only within rounding.  In exact mode every inner product is the
+ * correctly rounded value of the exact sum of its TwoProd pairs (p = a*b, e = fma(a, b, -p):
+ * p + e = a*b exactly unless a product under- or overflows), which no summation order can
+ * change: the GPU's grid reductions, the OpenMP partials and this serial loop all give the
+ * same bits.  The exact sum is held in a fixed-point superaccumulator of XW - 1 signed 32-bit
+ * digits in int64 words, value = sum d[i] * 2^(32 i - 1074) (every double is an integer
+ * multiple of 2^-1074); word XW - 1 counts non-finite terms (result NaN).  The device keeps a
+ * floating-point expansion per thread and merges into the same digit layout (xacc.hpp); the
+ * two implementations share no code, only the definition of the result. */
+enum { XW = 68 };
+static int g_exact = 0;
+void orc_set_exact(int on) { g_exact = on != 0; }
+int orc_get_exact(void) { return g_exact; }
+
+static void xs_add(int64_t *d, double x) {
+    if (x == 0) return;
+    if (!isfinite(x)) {
+        d[XW - 1]++;
+        return;
+    }
+    uint64_t bits;
+    memcpy(&bits, &x, sizeof bits);
+    const int E = (int)((bits >> 52) & 0x7ff);
+    uint64_t mant = bits & ((1ull << 52) - 1);
+    int off = 0;
+    if (E) mant |= 1ull << 52, off = E - 1;
+    const int i = off >> 5, sh = off & 31;
+    const uint64_t lo = mant << sh, hi = sh ? mant >> (64 - sh) : 0;
+    const int64_t c0 = (int64_t)(lo & 0xffffffffu), c1 = (int64_t)(lo >> 32), c2 = (int64_t)hi;
+    if (bits >> 63) d[i] -= c0, d[i + 1] -= c1, d[i + 2] -= c2;
+    else d[i] += c0, d[i + 1] += c1, d[i + 2] += c2;
+}
+
+/* TwoProd with a hardware FMA (the rest of the oracle keeps -ffp-contract=off semantics) */
+__attribute__((target("fma"))) static void xs_add_prod(int64_t *d, double a, double b) {
+    const double p = a * b;
+    const double e = __builtin_fma(a, b, -p);
+    xs_add(d, p);
+    xs_add(d, e);
+}
+
+/* bits [lo, lo + 64) of the magnitude digits u[0..nd) (zeros beyond either end) */
+static uint64_t xs_bits64(const uint32_t *u, int nd, int lo) {
+    if (lo < 0) return 0;  /* only called with lo >= 0 */
+    const int i = lo >> 5, sh = lo & 31;
+    const uint64_t w0 = i < nd ? u[i] : 0, w1 = i + 1 < nd ? u[i + 1] : 0, w2 = i + 2 < nd ? u[i + 2] : 0;
+    uint64_t r = (w0 | (w1 << 32)) >> sh;
+    if (sh) r |= w2 << (64 - sh);
+    return r;
+}
+
+/* round the exact sum to the nearest double, ties to even */
+static double xs_round(const int64_t *din) {
+    if (din[XW - 1]) return NAN;
+    enum { ND = XW - 1 };
+    uint32_t u[ND];
+    int64_t carry = 0;
+    for (int i = 0; i < ND; i++) {
+        const int64_t t = din[i] + carry;
+        u[i] = (uint32_t)(t & 0xffffffff);
+        carry = t >> 32; /* arithmetic: floor division */
+    }
+    const int neg = carry < 0;
+    if (neg) {
+        carry = 0;
+        for (int i = 0; i < ND; i++) {
+            const int64_t t = -din[i] + carry;
+            u[i] = (uint32_t)(t & 0xffffffff);
+            carry = t >> 32;
+        }
+    }
+    if (carry != 0) return neg ? -INFINITY : INFINITY;
+    int top = ND - 1;
+    while (top >= 0 && u[top] == 0) top--;
+    if (top < 0) return 0.0;
+    const int b = 32 * top + (32 - __builtin_clz(u[top])); /* bit length of the magnitude */
+    uint64_t rb;
+    if (b <= 53) { /* exact: V * 2^-1074 with V < 2^53 (subnormal or the lowest binade) */
+        const uint64_t V = xs_bits64(u, ND, 0) & ((1ull << 53) - 1);
+        if (V < (1ull << 52)) rb = V; /* subnormal: exponent field 0 */
+        else rb = (1ull << 52) | (V & ((1ull << 52) - 1));
+    } else {
+        int sh = b - 53;
+        uint64_t M = xs_bits64(u, ND, sh) & ((1ull << 53) - 1);
+        const int guard = (int)(xs_bits64(u, ND, sh - 1) & 1);
+        int sticky = 0;
+        const int lo = sh - 1; /* bits [0, lo) */
+        for (int i = 0; i < (lo >> 5) && !sticky; i++) sticky = u[i] != 0;
+        if (!sticky && (lo & 31)) sticky = (u[lo >> 5] & ((1u << (lo & 31)) - 1)) != 0;
+        if (guard && (sticky || (M & 1))) {
+            M++;
+            if (M == (1ull << 53)) M >>= 1, sh++;
+        }
+        const int e = sh - 1074; /* value M * 2^e, M in [2^52, 2^53) */
+        const int ef = e + 52 + 1023;
+        if (ef >= 2047) return neg ? -INFINITY : INFINITY;
+        rb = ((uint64_t)ef << 52) | (M & ((1ull << 52) - 1));
+    }
+    double r;
+    memcpy(&r, &rb, sizeof r);
+    return neg ? -r : r;
+}
+
+static double xdot(int64_t n, const double *a, const double *b) {
+    int64_t d[XW];
+    memset(d, 0, sizeof d);
+#ifdef _OPENMP
+    if (g_threads > 1 && n > 4096) {
+        _Pragma("omp parallel num_threads(g_threads)") {
+            int64_t t[XW];
+            memset(t, 0, sizeof t);
+            _Pragma("omp for schedule(static)") for (int64_t i = 0; i < n; i++) xs_add_prod(t, a[i], b[i]);
+            _Pragma("omp critical") for (int k = 0; k < XW; k++) d[k] += t[k];
+        }
+        return xs_round(d);
+    }
+#endif
+    for (int64_t i = 0; i < n; i++) xs_add_prod(d, a[i], b[i]);
+    return xs_round(d);
+}
+
+/* the exact mode's norm([a b]) of a 2-vector, shared operation for operation with the device
+ * (xacc.hpp xnorm2) instead of two libm hypot implementations: a power-of-two scaling into
+ * [2^-600, 2^600] where a*a cannot over- or underflow, a^2 + b^2 as a double-double (TwoProd by
+ * FMA, TwoSum), its square root, one Newton correction against the double-double */
+__attribute__((target("fma"))) static double xnorm2(double a, double b) {
+    a = fabs(a), b = fabs(b);
+    if (a < b) {
+        const double t = a;
+        a = b, b = t;
+    }
+    if (!(b > 0) || !isfinite(a)) return a + b; /* b == 0, inf, nan */
+    double sc = 1.0, us = 1.0;
+    if (a > 0x1p500) sc = 0x1p-600, us = 0x1p600;
+    else if (a < 0x1p-500) sc = 0x1p600, us = 0x1p-600;
+    a = a * sc, b = b * sc;
+    const double p1 = a * a, e1 = __builtin_fma(a, a, -p1);
+    const double p2 = b * b, e2 = __builtin_fma(b, b, -p2);
+    const double s = p1 + p2, bb = s - p1, t = (p1 - (s - bb)) + (p2 - bb);
+    double lo = t + (e1 + e2);
+    const double hi = s + lo;
+    lo = lo - (hi - s);
+    const double r = sqrt(hi);
+    const double res = __builtin_fma(-r, r, hi) + lo;
+    return (r + res / (2.0 * r)) * us;
+}
+
+double orc_xdot(int64_t n, const double *a, const double *b) { return xdot(n, a, b); }
+double orc_xnorm2(double a, double b) { return xnorm2(a, b); }
+
 static double dot(int64_t n, const double *a, const double *b) {
+    if (g_exact) return xdot(n, a, b);
     double s = 0.0;
 #ifdef _OPENMP
     if (g_threads > 1 && n > 4096) {
@@ -144,7 +299,7 @@ static double dot(int64_t n, const double *a, const double *b) {
 static double nrm2(int64_t n, const double *a) { return sqrt(dot(n, a, a)); }
 
 /* MATLAB norm([a b]) of a 2-vector */
-static double norm2(double a, double b) { return hypot(a, b); }
+static double norm2(double a, double b) { return g_exact ? xnorm2(a, b) : hypot(a, b); }
 
 static double msign(double a) { return (a > 0) - (a < 0); } /* MATLAB sign, sign(0)=0 */
 
@@ -965,18 +1120,27 @@ done:
  * per-thread partials, combined in thread order (deterministic for a given thread count). */
 enum { DQ_ROWS = 2048 };
 
-/* hj[q] = dot(V(:,jpos), u) + dot(Q(:,jpos), t) for window columns j = j0 .. j0+nj-1 */
+/* hj[q] = dot(V(:,jpos), u) + dot(Q(:,jpos), t) for window columns j = j0 .. j0+nj-1.  Exact
+ * mode: per-thread superaccumulators per column, summed digit-wise (the same bits as xdot). */
 static void dq_window_dots(int64_t n, int64_t m, const double *V, const double *Q, int64_t M1, int64_t j0,
                            int64_t nj, const double *u, const double *t, double *hj) {
     const int T = g_threads;
-    double *part = calloc((size_t)(2 * T * (nj > 0 ? nj : 1)), sizeof(double));
+    const int ex = g_exact;
+    const size_t nw = ex ? XW : 1; /* words per partial sum */
+    double *part = ex ? NULL : calloc((size_t)(2 * T * (nj > 0 ? nj : 1)), sizeof(double));
+    int64_t *xpart = ex ? calloc((size_t)(2 * T * (nj > 0 ? nj : 1)) * nw, sizeof(int64_t)) : NULL;
     _Pragma("omp parallel num_threads(T)") {
         const int th = omp_get_thread_num();
-        double *pv = part + (size_t)th * 2 * nj, *pq = pv + nj;
+        double *pv = ex ? NULL : part + (size_t)th * 2 * nj, *pq = ex ? NULL : pv + nj;
+        int64_t *xv = ex ? xpart + (size_t)th * 2 * nj * nw : NULL, *xq = ex ? xv + nj * nw : NULL;
         _Pragma("omp for schedule(static)") for (int64_t b = 0; b < n; b += DQ_ROWS) {
             const int64_t e = b + DQ_ROWS < n ? b + DQ_ROWS : n;
             for (int64_t q = 0; q < nj; q++) {
                 const double *v = V + ((j0 + q - 1) % M1) * n;
+                if (ex) {
+                    for (int64_t i = b; i < e; i++) xs_add_prod(xv + q * nw, v[i], u[i]);
+                    continue;
+                }
                 double s = pv[q];
                 for (int64_t i = b; i < e; i++) s += v[i] * u[i];
                 pv[q] = s;
@@ -986,6 +1150,10 @@ static void dq_window_dots(int64_t n, int64_t m, const double *V, const double *
             const int64_t e = b + DQ_ROWS < m ? b + DQ_ROWS : m;
             for (int64_t q = 0; q < nj; q++) {
                 const double *v = Q + ((j0 + q - 1) % M1) * m;
+                if (ex) {
+                    for (int64_t i = b; i < e; i++) xs_add_prod(xq + q * nw, v[i], t[i]);
+                    continue;
+                }
                 double s = pq[q];
                 for (int64_t i = b; i < e; i++) s += v[i] * t[i];
                 pq[q] = s;
@@ -993,11 +1161,21 @@ static void dq_window_dots(int64_t n, int64_t m, const double *V, const double *
         }
     }
     for (int64_t q = 0; q < nj; q++) {
+        if (ex) {
+            int64_t dv[XW], dq[XW];
+            memset(dv, 0, sizeof dv), memset(dq, 0, sizeof dq);
+            for (int th = 0; th < T; th++)
+                for (int k = 0; k < XW; k++)
+                    dv[k] += xpart[((size_t)th * 2 * nj + q) * nw + k], dq[k] += xpart[((size_t)th * 2 * nj + nj + q) * nw + k];
+            hj[q] = xs_round(dv) + xs_round(dq);
+            continue;
+        }
         double sv = 0.0, sq = 0.0;
         for (int th = 0; th < T; th++) sv += part[(size_t)th * 2 * nj + q], sq += part[(size_t)th * 2 * nj + nj + q];
         hj[q] = sv + sq;
     }
     free(part);
+    free(xpart);
 }
 
 /* V(:,kp1) -= hj[q] V(:,jpos) in window order (likewise Q), then returns
@@ -1005,18 +1183,22 @@ static void dq_window_dots(int64_t n, int64_t m, const double *V, const double *
 static double dq_window_orth(int64_t n, int64_t m, double *V, double *Q, int64_t M1, int64_t j0, int64_t nj,
                              const double *hj, int64_t kp1pos, const double *u, const double *t) {
     const int T = g_threads;
+    const int ex = g_exact;
     double *part = calloc((size_t)(2 * T), sizeof(double));
+    int64_t *xpart = ex ? calloc((size_t)(2 * T) * XW, sizeof(int64_t)) : NULL;
     double *vk = V + (kp1pos - 1) * n, *qk = Q + (kp1pos - 1) * m;
     _Pragma("omp parallel num_threads(T)") {
         const int th = omp_get_thread_num();
         double sv = 0.0, sq = 0.0;
+        int64_t *xv = ex ? xpart + (size_t)(2 * th) * XW : NULL, *xq = ex ? xv + XW : NULL;
         _Pragma("omp for schedule(static)") for (int64_t b = 0; b < n; b += DQ_ROWS) {
             const int64_t e = b + DQ_ROWS < n ? b + DQ_ROWS : n;
             for (int64_t q = 0; q < nj; q++) {
                 const double *v = V + ((j0 + q - 1) % M1) * n, h = hj[q];
                 for (int64_t i = b; i < e; i++) vk[i] = vk[i] - h * v[i];
             }
-            for (int64_t i = b; i < e; i++) sv += u[i] * vk[i];
+            if (ex) for (int64_t i = b; i < e; i++) xs_add_prod(xv, u[i], vk[i]);
+            else for (int64_t i = b; i < e; i++) sv += u[i] * vk[i];
         }
         _Pragma("omp for schedule(static)") for (int64_t b = 0; b < m; b += DQ_ROWS) {
             const int64_t e = b + DQ_ROWS < m ? b + DQ_ROWS : m;
@@ -1024,13 +1206,23 @@ static double dq_window_orth(int64_t n, int64_t m, double *V, double *Q, int64_t
                 const double *v = Q + ((j0 + q - 1) % M1) * m, h = hj[q];
                 for (int64_t i = b; i < e; i++) qk[i] = qk[i] - h * v[i];
             }
-            for (int64_t i = b; i < e; i++) sq += t[i] * qk[i];
+            if (ex) for (int64_t i = b; i < e; i++) xs_add_prod(xq, t[i], qk[i]);
+            else for (int64_t i = b; i < e; i++) sq += t[i] * qk[i];
         }
         part[2 * th] = sv, part[2 * th + 1] = sq;
     }
     double sv = 0.0, sq = 0.0;
-    for (int th = 0; th < T; th++) sv += part[2 * th], sq += part[2 * th + 1];
+    if (ex) {
+        int64_t dv[XW], dq[XW];
+        memset(dv, 0, sizeof dv), memset(dq, 0, sizeof dq);
+        for (int th = 0; th < T; th++)
+            for (int k = 0; k < XW; k++) dv[k] += xpart[(size_t)(2 * th) * XW + k], dq[k] += xpart[(size_t)(2 * th + 1) * XW + k];
+        sv = xs_round(dv), sq = xs_round(dq);
+    } else {
+        for (int th = 0; th < T; th++) sv += part[2 * th], sq += part[2 * th + 1];
+    }
     free(part);
+    free(xpart);
     return sv + sq;
 }
 
@@ -1553,30 +1745,12 @@ int orc_method(int method, const double *b, const orc_csr *A, const orc_csr *C, 
     }
 }
 
-/* reg_cpkrylov.m:121-180 */
-int orc_reg_cpkrylov(int method, const double *b, const orc_csr *A, const orc_csr *B, const orc_csr *C,
-                     const orc_csr *G, const orc_opts *opts, int order_kind, const int32_t *perm, double *x,
-                     orc_stats *st, orc_ldl2 **M_out) {
-    double t0 = now_s();
+/* reg_cpkrylov.m:150-175 with an existing M: the shift (:152-160), the method call (:163) and the
+ * recovery (:166-173) -- cpk_reg_solve_device's counterpart */
+int orc_reg_solve(int method, const double *b, const orc_csr *A, const orc_csr *B, const orc_csr *C,
+                  orc_ldl2 *M, const orc_opts *opts, double *x, orc_stats *st) {
     int64_t n = A->nrows, m = B->nrows, N = n + m;
-    /* M = opLDL2(G, B, -C) */
-    csr negC;
-    if (csr_alloc(&negC, C->nrows, C->ncols, C->ptr[C->nrows])) return set_err(ORC_ERR_NOMEM, "oom");
-    memcpy(negC.ptr, C->ptr, (size_t)(C->nrows + 1) * sizeof(int64_t));
-    memcpy(negC.ind, C->ind, (size_t)C->ptr[C->nrows] * sizeof(int32_t));
-    for (int64_t p = 0; p < C->ptr[C->nrows]; p++) negC.val[p] = -C->val[p];
-    orc_csr vnegC = view(&negC);
-    orc_ldl2 *M;
-    int rc = orc_ldl2_create(G, B, &vnegC, order_kind, perm, &M);
-    csr_free(&negC);
-    if (rc) return rc;
-    double ptime = now_s() - t0;
-    if (opts) {
-        if (opts->has_nitref) orc_ldl2_set_nitref(M, opts->nitref);
-        if (opts->has_itref_tol) orc_ldl2_set_itref_tol(M, opts->itref_tol);
-        if (opts->has_residual_update) orc_ldl2_set_residual_update(M, opts->residual_update);
-        if (opts->has_force_itref) orc_ldl2_set_force_itref(M, opts->force_itref);
-    }
+    int rc;
     double t1 = now_s();
     double *xy0 = calloc((size_t)N, sizeof(double));
     double *in = calloc((size_t)N, sizeof(double));
@@ -1612,8 +1786,35 @@ int orc_reg_cpkrylov(int method, const double *b, const orc_csr *A, const orc_cs
         }
     }
     st->stime = now_s() - t1;
-    st->ptime = ptime;
     free(xy0); free(in); free(b1); free(tmp); free(tmp2); free(dx); free(dy);
+    return rc;
+}
+
+/* reg_cpkrylov.m:121-180 */
+int orc_reg_cpkrylov(int method, const double *b, const orc_csr *A, const orc_csr *B, const orc_csr *C,
+                     const orc_csr *G, const orc_opts *opts, int order_kind, const int32_t *perm, double *x,
+                     orc_stats *st, orc_ldl2 **M_out) {
+    double t0 = now_s();
+    /* M = opLDL2(G, B, -C) */
+    csr negC;
+    if (csr_alloc(&negC, C->nrows, C->ncols, C->ptr[C->nrows])) return set_err(ORC_ERR_NOMEM, "oom");
+    memcpy(negC.ptr, C->ptr, (size_t)(C->nrows + 1) * sizeof(int64_t));
+    memcpy(negC.ind, C->ind, (size_t)C->ptr[C->nrows] * sizeof(int32_t));
+    for (int64_t p = 0; p < C->ptr[C->nrows]; p++) negC.val[p] = -C->val[p];
+    orc_csr vnegC = view(&negC);
+    orc_ldl2 *M;
+    int rc = orc_ldl2_create(G, B, &vnegC, order_kind, perm, &M);
+    csr_free(&negC);
+    if (rc) return rc;
+    double ptime = now_s() - t0;
+    if (opts) {
+        if (opts->has_nitref) orc_ldl2_set_nitref(M, opts->nitref);
+        if (opts->has_itref_tol) orc_ldl2_set_itref_tol(M, opts->itref_tol);
+        if (opts->has_residual_update) orc_ldl2_set_residual_update(M, opts->residual_update);
+        if (opts->has_force_itref) orc_ldl2_set_force_itref(M, opts->force_itref);
+    }
+    rc = orc_reg_solve(method, b, A, B, C, M, opts, x, st);
+    st->ptime = ptime;
     if (M_out && rc == 0) *M_out = M;
     else orc_ldl2_destroy(M);
     return rc;

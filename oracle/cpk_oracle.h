@@ -98,6 +98,11 @@ int orc_reg_cpkrylov(int method, const double *b, const orc_csr *A, const orc_cs
                      const orc_csr *C, const orc_csr *G, const orc_opts *opts, int order_kind,
                      const int32_t *perm, double *x, orc_stats *stats, orc_ldl2 **M_out);
 
+/* reg_cpkrylov.m:150-175 with an existing preconditioner M (opts' preconditioner fields are not
+ * applied here): the shift, the method call and the recovery; b and x of length N */
+int orc_reg_solve(int method, const double *b, const orc_csr *A, const orc_csr *B, const orc_csr *C,
+                  orc_ldl2 *M, const orc_opts *opts, double *x, orc_stats *stats);
+
 /* [c, s, d] = SymGivens(a, b) -- util/SymGivens.m:1-29 */
 void orc_symgivens(double a, double b, double *c, double *s, double *d);
 
@@ -107,6 +112,14 @@ const char *orc_last_error(void);
  * level-scheduled sweeps under OpenMP (bit-identical) and chunked dot products (not). */
 void orc_set_threads(int t);
 int orc_get_threads(void);
+/* Exact inner products (default off): every dot and norm is the correctly rounded exact sum of
+ * its TwoProd pairs, and norm([a b]) the shared double-double formula -- the product's engine
+ * option exact_dots computes the same values, so histories compare bit for bit and the thread
+ * count no longer changes any result.  orc_xdot exposes one such dot (tests). */
+void orc_set_exact(int on);
+int orc_get_exact(void);
+double orc_xdot(int64_t n, const double *a, const double *b);
+double orc_xnorm2(double a, double b);
 
 #ifdef __cplusplus
 }

@@ -72,8 +72,16 @@ def lib():
                                  P(C.c_double), P(C.c_double), P(_Stats)]
         L.orc_reg_cpkrylov.argtypes = [C.c_int, P(C.c_double), P(_Csr), P(_Csr), P(_Csr), P(_Csr), P(_Opts),
                                        C.c_int, P(C.c_int32), P(C.c_double), P(_Stats), P(C.c_void_p)]
+        L.orc_reg_solve.argtypes = [C.c_int, P(C.c_double), P(_Csr), P(_Csr), P(_Csr), C.c_void_p, P(_Opts),
+                                    P(C.c_double), P(_Stats)]
         L.orc_symgivens.argtypes = [C.c_double, C.c_double] + [P(C.c_double)] * 3
         L.orc_set_threads.argtypes = [C.c_int]
+        L.orc_set_exact.argtypes = [C.c_int]
+        L.orc_get_exact.restype = C.c_int
+        L.orc_xdot.argtypes = [C.c_int64, P(C.c_double), P(C.c_double)]
+        L.orc_xdot.restype = C.c_double
+        L.orc_xnorm2.argtypes = [C.c_double, C.c_double]
+        L.orc_xnorm2.restype = C.c_double
         L.orc_get_threads.restype = C.c_int
         L.orc_last_error.restype = C.c_char_p
         _lib = L
@@ -249,11 +257,61 @@ def reg_cpkrylov(name, b, A, B, Cm, G, opts=None, order="rcm", perm=None, hist_c
     return x, stats
 
 
+def reg_solve(name, b, A, B, Cm, M, opts=None, hist_cap=None):
+    """reg_cpkrylov's shift + method + recovery with an existing preconditioner M (an LDL2, e.g.
+    built from the product's exported factors) -- x (N), stats"""
+    n, m = A.shape[0], B.shape[0]
+    b = np.ascontiguousarray(b, np.float64)
+    hs = [_CsrHold(X) for X in (A, B, Cm)]
+    o = _opts(opts)
+    x = np.zeros(n + m)
+    cap = hist_cap or int((opts or {}).get("itmax", n + m)) + 3
+    stats, st = _run(lambda mid, xp, stp: lib().orc_reg_solve(
+        mid, _ptr(b, C.c_double), *[C.byref(h.s) for h in hs], M.h, C.byref(o), xp, stp),
+        name, cap, _ptr(x, C.c_double))
+    return x, stats
+
+
 def set_threads(t):
     """Threads of the CPU-baseline timing leg (1 = the serial restatement); returns the count
     actually in effect (1 when the oracle was built without OpenMP)."""
     lib().orc_set_threads(int(t))
     return lib().orc_get_threads()
+
+
+def set_exact(on):
+    """Exact inner products (orc_set_exact): every dot / norm the correctly rounded exact sum of
+    its TwoProd pairs, norm([a b]) the shared double-double formula -- the values of the
+    product's engine option exact_dots.  Returns the previous setting."""
+    prev = bool(lib().orc_get_exact())
+    lib().orc_set_exact(1 if on else 0)
+    return prev
+
+
+class exact:
+    """with oracle.exact(): ... -- exact inner products inside the block"""
+
+    def __init__(self, on=True):
+        self.on = on
+
+    def __enter__(self):
+        self.prev = set_exact(self.on)
+        return self
+
+    def __exit__(self, *exc):
+        set_exact(self.prev)
+
+
+def xdot(a, b):
+    """One exact-mode inner product (the correctly rounded sum of the TwoProd pairs)."""
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    return lib().orc_xdot(a.shape[0], _ptr(a, C.c_double), _ptr(b, C.c_double))
+
+
+def xnorm2(a, b):
+    """The exact mode's norm([a b])."""
+    return lib().orc_xnorm2(float(a), float(b))
 
 
 def symgivens(a, b):
