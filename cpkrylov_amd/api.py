@@ -323,7 +323,7 @@ class opLDL2:
         v = (C.c_int64 * 8)()
         check(lib.cpk_pc_sweep_info(self.h, v))
         return dict(zip(("rounds", "round0_blocks", "upper_blocks", "round0_assigned", "resid_assigned",
-                         "bwd_assigned", "persistent", "reserved"), list(v)))
+                         "bwd_assigned", "persistent", "chain_tasks"), list(v)))
 
     def local_dofs(self):
         """Global indices of this rank's local vector entries ([x-part; y-part]) and n_loc."""

@@ -444,6 +444,7 @@ int cpk_pc_apply(cpk_pc M, const double *x, double *y) {
     } else {
         CPK_HIP(hipMemcpyAsync(y, dy.p, p.N * sizeof(double), hipMemcpyDeviceToHost, c.stream));
         CPK_HIP(hipStreamSynchronize(c.stream));
+        check_chain(p.dF);
     }
     API_END
 }
@@ -633,7 +634,8 @@ int cpk_pc_sweep_info(cpk_pc M, int64_t *info) {
     const DFactor &F = M->p->dF;
     const int64_t nr = (int64_t)F.round_ptr.size() - 1;
     const int64_t r0 = nr >= 1 ? F.round_ptr[1] - F.round_ptr[0] : 0;
-    const int64_t v[8] = {nr, r0, F.nblk - r0, F.agrid[0], F.agrid[1], F.agrid[2], F.pipelined ? 1 : 0, 0};
+    const int64_t chain = (F.ch_ntask > 0 && !F.no_chain && fuse_last_ok(F)) ? F.ch_ntask : 0;
+    const int64_t v[8] = {nr, r0, F.nblk - r0, F.agrid[0], F.agrid[1], F.agrid[2], F.pipelined ? 1 : 0, chain};
     std::memcpy(info, v, sizeof v);
     API_END
 }

@@ -118,6 +118,7 @@ struct EngineOpts {
     bool no_fuse_last = false;    // no_fuse_last:       the last sweep round as two launches
     bool no_tkr = false;          // no_tkr:             distributed refinement residual through the Kp halo
     bool no_minres_fuse = false;  // no_minres_fuse:     cpminres update as its own pass (normalise + w, x)
+    bool no_chain = false;        // no_chain:           upper rounds one launch per round (not the sweep chain)
     bool dist_graph = true;       // dist_graph:         capture collectives in the graphs
     bool dist1 = false;           // dist1:              a 1-rank communicator runs the distributed path
                                   //                     (diagnostic; set before building operators)
@@ -232,6 +233,15 @@ struct DFactor {
     // grid they were made for (0: none; the launch then strides over meta)
     DBuf<int32_t> aptr[3], ameta[3];
     int agrid[3] = {0, 0, 0};
+    // the sweep chain (kernels.hip, sptrsv_chain_kernel): the upper rounds forward, the last round
+    // (forward + backward) and the upper rounds backward as ONE launch whose blocks wait for
+    // their own producers (flags) instead of for whole rounds.  Tasks in topological order
+    // (task = kind << 28 | block; kind 0 forward, 1 last, 2 backward), each task's producer tasks
+    // (dep_ptr / dep_idx), a done flag per task and {epoch, ticket, error} (zero at build)
+    int64_t ch_ntask = 0;
+    DBuf<int32_t> ch_task, ch_dptr, ch_didx;
+    DBuf<uint32_t> ch_flag, ch_ctrl;
+    bool no_chain = false;  // engine option no_chain (set before make_dfactor)
     std::vector<int64_t> round_ptr;  // host copy: blocks per round
     std::vector<char> round_fits;    // host: every block of round r fits (sweep_rows[1], sweep_cap[1])
     int sweep_rows[2] = {192, 1024}, sweep_cap[2] = {576, 4096}, sweep_threads[2] = {64, 512};  // round 0 / rest
@@ -289,8 +299,11 @@ struct FwdIn {
     int sched_in = 0;
     double *xs = nullptr;
     bool valid = false;
-    int64_t from = 0;  // the deferred round (the last one)
+    int64_t from = 0;  // the deferred round (the last one; with chain, the first upper round)
+    bool chain = false;  // every upper round deferred to the backward sweep's chain launch
 };
+// the sweep chain's error word (a producer wait timed out): CPK_ERR_HIP, cleared
+void check_chain(const DFactor &F);
 bool fuse_last_ok(const DFactor &F);
 // defer (optional): the last round is left to the backward sweep (sptrsv_last_kernel solves it
 // forward and backward in one launch); *defer then says how, for launch_sptrsv_bwd's last

@@ -240,6 +240,9 @@ void mark_dataflow(std::vector<int32_t> &meta, const std::vector<int64_t> &round
     }, 4);
 }
 
+static void build_chain(DFactor &d, const std::vector<int32_t> &meta, const std::vector<uint32_t> &fptr,
+                        const std::vector<int32_t> &fcol, const std::vector<uint32_t> &bptr,
+                        const std::vector<int32_t> &bcol);
 constexpr int64_t kInsertionSortMax = 32;  // rows up to this long sort by insertion (keys are distinct)
 void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vector<int64_t> *key,
                   const std::vector<std::vector<BwdExtra>> *extra, std::vector<int32_t> *fsrc,
@@ -442,6 +445,8 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
         }
     }
     clk.lap("layout: int16 round-0 columns");
+    build_chain(d, meta, fptr, fcol, bptr, bcol);
+    clk.lap("layout: sweep chain");
 }
 
 // ---- SpMV launchers --------------------------------------------------------------------------
@@ -1773,7 +1778,20 @@ __device__ uint64_t g_blk_cyc[12 * kBlkCycMax];
 #define CPK_UP_STAMP(k) (void)0
 #endif
 // one block of an upper round (the body of sptrsv_upper_kernel); ends with the block's write-back
-template <int TPB, int RPU, int EPU, bool BWD, bool ADD>
+// SC (the chain kernel): w is handed between blocks of one launch, so every w value a block may
+// read from another block, and every w value it writes, goes through agent-scope (sc1) loads and
+// stores (MI355X_MICROARCH.md "Valid forms", row 1), never through this CU's L1
+template <bool SC>
+__device__ __forceinline__ double wld(const double *p) {
+    if constexpr (SC) return ld_agent(p);
+    return *p;
+}
+template <bool SC>
+__device__ __forceinline__ void wst(double *p, double v) {
+    if constexpr (SC) st_agent(p, v);
+    else *p = v;
+}
+template <int TPB, int RPU, int EPU, bool BWD, bool ADD, bool SC = false>
 __device__ __forceinline__ void upper_block(
     char *smem, const BlkMeta m, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
@@ -1799,7 +1817,7 @@ __device__ __forceinline__ void upper_block(
     for (int j = 0; j < RPU; j++) {
         const int i = tid + j * TPB, rr = r0 + (i < nr ? i : nr - 1);
         q[j] = ptr[rr], sp[j] = (BWD ? out != nullptr : !sched_in) ? perm[rr] : rr;
-        if (BWD) a[j] = w[rr], d[j] = D[rr];
+        if (BWD) a[j] = wld<SC>(w + rr), d[j] = D[rr];
     }
 #pragma unroll
     for (int u = 0; u < EPU; u++) {
@@ -1813,7 +1831,7 @@ __device__ __forceinline__ void upper_block(
         if (!BWD) a[j] = xin[sp[j]];
     }
 #pragma unroll
-    for (int u = 0; u < EPU; u++) g[u] = w[(c[u] >= r0 && c[u] < r1) ? r0 : c[u]];
+    for (int u = 0; u < EPU; u++) g[u] = wld<SC>(w + ((c[u] >= r0 && c[u] < r1) ? r0 : c[u]));
 #pragma unroll
     for (int j = 0; j < RPU; j++) {
         const int i = tid + j * TPB;
@@ -1854,7 +1872,7 @@ __device__ __forceinline__ void upper_block(
         const int i = tid + j * TPB;
         if (i < nr) {
             const double z = S.w[i];
-            w[r0 + i] = z;
+            wst<SC>(w + r0 + i, z);
             if (BWD) {
                 if (out) {
                     const double o = ADD ? (ys ? ys[r0 + i] : out[sp[j]]) + z : z;
@@ -1893,7 +1911,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
 // forward fold and levels, divides by D in LDS and runs the backward levels -- the operations of
 // sptrsv_upper_kernel forward, its write-back and w / D, and sptrsv_upper_kernel backward, in
 // that order: bit-identical, one launch and one staging round trip fewer per solve.
-template <int TPB, int RPU, int EPU, bool ADD>
+template <int TPB, int RPU, int EPU, bool ADD, bool SC = false>
 __device__ __forceinline__ void last_block(
     char *smem, const BlkMeta m, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ fptr, const int32_t *__restrict__ fcol, const double *__restrict__ fval,
@@ -1928,7 +1946,7 @@ __device__ __forceinline__ void last_block(
 #pragma unroll
     for (int j = 0; j < RPU; j++) a[j] = xin[sp[j]];
 #pragma unroll
-    for (int u = 0; u < EPU; u++) g[u] = w[(cf[u] >= r0 && cf[u] < r1) ? r0 : cf[u]];
+    for (int u = 0; u < EPU; u++) g[u] = wld<SC>(w + ((cf[u] >= r0 && cf[u] < r1) ? r0 : cf[u]));
     // ---- forward (sptrsv_upper_kernel<..., false, false>)
 #pragma unroll
     for (int j = 0; j < RPU; j++) {
@@ -1961,7 +1979,7 @@ __device__ __forceinline__ void last_block(
     // ---- backward (sptrsv_upper_kernel<..., true, ADD>): w / D, the entries, fold, levels; the
     // backward terms of a last-round block are its own rows (the 1.0 slot path is kept for any other)
 #pragma unroll
-    for (int u = 0; u < EPU; u++) g[u] = (tid + u * TPB < neb && (cb[u] < r0 || cb[u] >= r1)) ? w[cb[u]] : 0.0;
+    for (int u = 0; u < EPU; u++) g[u] = (tid + u * TPB < neb && (cb[u] < r0 || cb[u] >= r1)) ? wld<SC>(w + cb[u]) : 0.0;
 #pragma unroll
     for (int j = 0; j < RPU; j++) {
         const int i = tid + j * TPB;
@@ -1996,7 +2014,7 @@ __device__ __forceinline__ void last_block(
         const int i = tid + j * TPB;
         if (i < nr) {
             const double z = S.w[i];
-            w[r0 + i] = z;
+            wst<SC>(w + r0 + i, z);
             if (out) out[dp[j]] = ADD ? (ys ? ys[r0 + i] : out[dp[j]]) + z : z;
             else if (ADD) ys[r0 + i] = ys[r0 + i] + z;
         }
@@ -2047,6 +2065,184 @@ static void launch_last(Ctx &c, const DFactor &F, const FwdIn &in, double *w, do
                            meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p,
                            in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys);
     CPK_HIP(hipGetLastError());
+}
+
+// ---- the sweep chain -----------------------------------------------------------------------------
+// All upper rounds of a solve in ONE launch: forward rounds 1 .. R-2, the last round (forward and
+// backward, as sptrsv_last_kernel), backward rounds R-2 .. 1.  One workgroup per task, tasks in
+// topological order (blockIdx = task); a task waits for its own producers -- the blocks holding
+// the rows its entries read (build_chain) -- not for the whole previous round, then runs the
+// block exactly as the round kernels do (bit-identical) and publishes a done flag.  Deadlock-free
+// without co-residency: workgroups are dispatched in blockIdx order, so every producer of a
+// resident waiter (a smaller index) has been dispatched.  Hand-off: MI355X_MICROARCH.md "Valid
+// forms" row 1 -- every w value crossing blocks is stored and loaded sc1 (upper_block<SC>), each
+// storing wave drains (vmcnt(0)) before the workgroup barrier, one lane stores the flag sc1, and
+// consumers poll it sc1.  Flags hold the launch's epoch + 1 (no reset pass); the last workgroup
+// (ticket) advances the epoch.  Every spin is bounded: a wait that outlives kChainSpinCap sets the
+// error word, every other waiter then gives up, and the host raises CPK_ERR_HIP (check_chain).
+constexpr int kChainTPB = 256, kChainRPU = 2, kChainEPU = 12;
+constexpr uint32_t kChainSpinCap = 1u << 22;
+struct ChainArgs {
+    const int32_t *task, *dptr, *didx;
+    uint32_t *flag, *ctrl;
+    int ntask;
+};
+__device__ __forceinline__ uint32_t ld_agent32(const uint32_t *p) {
+    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent32(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool ADD>
+__global__ __launch_bounds__(kChainTPB) void sptrsv_chain_kernel(
+    ChainArgs ch, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
+    const uint32_t *__restrict__ fptr, const int32_t *__restrict__ fcol, const double *__restrict__ fval,
+    const uint32_t *__restrict__ bptr, const int32_t *__restrict__ bcol, const double *__restrict__ bval,
+    const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
+    int sched_in, double *xs, double *w, double *out, const int *run, const int *active, double *ys) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ uint32_t s_epoch;
+    if (skip(run, active)) return;
+    const int t = blockIdx.x;
+    if (threadIdx.x == 0) s_epoch = ld_agent32(ch.ctrl);
+    __syncthreads();
+    const uint32_t want = s_epoch + 1;
+    const int d1 = ch.dptr[t + 1];
+    for (int k = ch.dptr[t] + (int)threadIdx.x; k < d1; k += kChainTPB) {
+        const uint32_t *f = ch.flag + ch.didx[k];
+        uint32_t spins = 0;
+        while (ld_agent32(f) != want) {
+            if (ld_agent32(ch.ctrl + 2) != 0) break;  // a wait timed out somewhere: give up
+            if (++spins > kChainSpinCap) {
+                st_agent32(ch.ctrl + 2, 1);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+    const int32_t task = ch.task[t];
+    const int kind = task >> 28, b = task & ((1 << 28) - 1);
+    const PackArgs none{};
+    if (kind == 0)
+        upper_block<kChainTPB, kChainRPU, kChainEPU, false, false, true>(smem, meta[b], lvl_row, fptr, fcol, fval, D, perm,
+                                                                         xin, neg_from, w, nullptr, sched_in, nullptr,
+                                                                         xs, none, b);
+    else if (kind == 1)
+        last_block<kChainTPB, kChainRPU, kChainEPU, ADD, true>(smem, meta[b], lvl_row, fptr, fcol, fval, bptr, bcol, bval,
+                                                               D, perm, xin, neg_from, sched_in, xs, w, out, ys);
+    else
+        upper_block<kChainTPB, kChainRPU, kChainEPU, true, ADD, true>(smem, meta[b], lvl_row, bptr, bcol, bval, D, perm,
+                                                                      nullptr, 0, w, out, 0, ys, nullptr, none, b);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w stores done
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        st_agent32(ch.flag + t, want);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (__hip_atomic_fetch_add(ch.ctrl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)ch.ntask - 1) {
+            st_agent32(ch.ctrl + 1, 0u);
+            st_agent32(ch.ctrl, want);  // the next launch's epoch
+        }
+    }
+}
+
+static void build_chain(DFactor &d, const std::vector<int32_t> &meta, const std::vector<uint32_t> &fptr,
+                        const std::vector<int32_t> &fcol, const std::vector<uint32_t> &bptr,
+                        const std::vector<int32_t> &bcol) {
+    d.ch_ntask = 0;
+    const int64_t R = (int64_t)d.round_ptr.size() - 1;
+    if (d.no_chain || d.no_upper || R < 3 || d.round0_rows < 0) return;
+    if (d.sweep_threads[1] != kChainTPB || d.sweep_rows[1] > kChainRPU * kChainTPB ||
+        d.sweep_cap[1] > kChainEPU * kChainTPB)
+        return;
+    for (int64_t r = 1; r < R; r++)
+        if (r >= (int64_t)d.round_fits.size() || !d.round_fits[r]) return;
+    const int64_t N = d.N, base = d.round0_rows;
+    const int64_t b1 = d.round_ptr[1], bl = d.round_ptr[R - 1], be = d.round_ptr[R];
+    std::vector<int32_t> blk((size_t)(N - base), -1);
+    for (int64_t b = b1; b < be; b++)
+        for (int32_t i = meta[(size_t)b * 8]; i < meta[(size_t)b * 8 + 1]; i++) blk[(size_t)(i - base)] = (int32_t)b;
+    for (int32_t x : blk)
+        if (x < 0) return;  // upper rows not all in upper blocks
+    // task ids: forward and last tasks in block order (= round order), then backward tasks from
+    // the highest round down
+    const int64_t nfl = be - b1, nt = nfl + (bl - b1);
+    auto fwd_task = [&](int64_t b) { return (int32_t)(b - b1); };
+    auto bwd_task = [&](int64_t b) { return b >= bl ? (int32_t)(b - b1) : (int32_t)(nfl + (bl - 1 - b)); };
+    std::vector<int32_t> task((size_t)nt), dptr((size_t)nt + 1, 0), didx;
+    std::vector<int32_t> deps;
+    bool ok = true;
+    auto emit = [&](int32_t t) {
+        std::sort(deps.begin(), deps.end());
+        deps.erase(std::unique(deps.begin(), deps.end()), deps.end());
+        for (int32_t p : deps) ok = ok && p < t;
+        didx.insert(didx.end(), deps.begin(), deps.end());
+        dptr[(size_t)t + 1] = (int32_t)didx.size();
+        deps.clear();
+    };
+    for (int64_t b = b1; b < be && ok; b++) {  // forward (rounds 1 .. R-2) and last (round R-1)
+        const int32_t *m = &meta[(size_t)b * 8];
+        for (int32_t i = m[0]; i < m[1]; i++) {
+            for (uint32_t e = fptr[i]; e < fptr[i + 1]; e++) {
+                const int32_t c = fcol[e];
+                if (c >= base && c < N && (c < m[0] || c >= m[1])) deps.push_back(fwd_task(blk[(size_t)(c - base)]));
+            }
+            if (b >= bl)  // a last-round block's backward terms must stay inside it (sptrsv_last_kernel)
+                for (uint32_t e = bptr[i]; e < bptr[i + 1]; e++)
+                    if (bcol[e] < N && bcol[e] >= base && (bcol[e] < m[0] || bcol[e] >= m[1])) ok = false;
+        }
+        task[(size_t)fwd_task(b)] = (int32_t)((b >= bl ? 1 : 0) << 28 | b);
+        emit(fwd_task(b));
+    }
+    for (int64_t b = bl - 1; b >= b1 && ok; b--) {  // backward, highest round first
+        const int32_t *m = &meta[(size_t)b * 8];
+        deps.push_back(fwd_task(b));  // its own forward values
+        for (int32_t i = m[0]; i < m[1]; i++)
+            for (uint32_t e = bptr[i]; e < bptr[i + 1]; e++) {
+                const int32_t c = bcol[e];
+                if (c >= base && c < N && (c < m[0] || c >= m[1])) deps.push_back(bwd_task(blk[(size_t)(c - base)]));
+            }
+        task[(size_t)bwd_task(b)] = (int32_t)(2 << 28 | b);
+        emit(bwd_task(b));
+    }
+    if (!ok || nt >= (1 << 28)) return;
+    d.ch_task.upload(task);
+    d.ch_dptr.upload(dptr);
+    d.ch_didx.upload(didx.empty() ? std::vector<int32_t>{0} : didx);
+    d.ch_flag.alloc((size_t)nt);
+    CPK_HIP(hipMemset(d.ch_flag.p, 0, d.ch_flag.bytes()));
+    d.ch_ctrl.alloc(4);
+    CPK_HIP(hipMemset(d.ch_ctrl.p, 0, d.ch_ctrl.bytes()));
+    d.ch_ntask = nt;
+}
+
+static bool chain_ok(const DFactor &F) { return F.ch_ntask > 0 && !F.no_chain && fuse_last_ok(F); }
+
+static void launch_chain(Ctx &c, const DFactor &F, const FwdIn &in, double *w, double *out, bool add, const int *run,
+                         const int *active, double *ys) {
+    const size_t lds = sweep_lds_bytes(kChainRPU * kChainTPB, kChainEPU * kChainTPB);
+    const ChainArgs ch{F.ch_task.p, F.ch_dptr.p, F.ch_didx.p, F.ch_flag.p, F.ch_ctrl.p, (int)F.ch_ntask};
+    const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
+    if (add)
+        hipLaunchKernelGGL(sptrsv_chain_kernel<true>, dim3((unsigned)F.ch_ntask), dim3(kChainTPB), lds, c.stream, ch, meta,
+                           F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p,
+                           in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys);
+    else
+        hipLaunchKernelGGL(sptrsv_chain_kernel<false>, dim3((unsigned)F.ch_ntask), dim3(kChainTPB), lds, c.stream, ch,
+                           meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
+                           F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys);
+    CPK_HIP(hipGetLastError());
+}
+
+void check_chain(const DFactor &F) {
+    if (F.ch_ntask <= 0) return;
+    uint32_t err = 0;
+    CPK_HIP(hipMemcpy(&err, F.ch_ctrl.p + 2, sizeof err, hipMemcpyDeviceToHost));
+    if (err) {
+        CPK_HIP(hipMemset(F.ch_ctrl.p + 2, 0, sizeof err));
+        throw Error(CPK_ERR_HIP, "sweep chain: a block's wait for its producers timed out");
+    }
 }
 
 template <int TPB, int RPU, int EPU>
@@ -2606,7 +2802,11 @@ static bool fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
                     const PackArgs *pk = nullptr) {
     int64_t R = (int64_t)F.round_ptr.size() - 1;
     bool packed = pk != nullptr;  // every round launched here through a packing kernel
-    if (defer && fuse_last_ok(F)) {  // the last round runs with the backward sweep
+    if (defer && chain_ok(F) && rfirst <= 1) {  // every upper round runs in the backward sweep's chain
+        *defer = FwdIn{xin, neg_from, sched_in, xs, true, 1, true};
+        R = 1;
+        packed = false;
+    } else if (defer && fuse_last_ok(F)) {  // the last round runs with the backward sweep
         *defer = FwdIn{xin, neg_from, sched_in, xs, true, R - 1};
         R -= 1;
         packed = false;  // the deferred round's rows are packed by no launch here
@@ -2695,7 +2895,10 @@ bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
     int64_t R = (int64_t)F.round_ptr.size() - 1;
     bool packed = pk != nullptr && !(last && last->valid);
     const PackArgs none{};
-    if (last && last->valid) {  // the deferred last round, forward and backward (sptrsv_last_kernel)
+    if (last && last->valid && last->chain) {  // the deferred upper rounds: one chain launch
+        launch_chain(c, F, *last, w, out, add, run, active, ys);
+        R = 1;
+    } else if (last && last->valid) {  // the deferred last round, forward and backward (sptrsv_last_kernel)
         launch_last(c, F, *last, w, out, add, run, active, ys);
         R = last->from;
     }

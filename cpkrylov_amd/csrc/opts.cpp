@@ -71,6 +71,7 @@ const BoolOpt kBool[] = {
     {"dist_graph", &EngineOpts::dist_graph},
     {"dist1", &EngineOpts::dist1},
     {"exact_dots", &EngineOpts::exact_dots},
+    {"no_chain", &EngineOpts::no_chain},
     {"profile_fwd_sched", &EngineOpts::profile_fwd_sched},
 };
 

@@ -96,6 +96,7 @@ Precond *precond_create(Ctx &c, Analysis &&an, PrecondPre *pre) {
         pc->dF.sweep_rows[i] = an.sweep.rows[i], pc->dF.sweep_cap[i] = an.sweep.cap[i],
         pc->dF.sweep_threads[i] = an.sweep.threads[i];
     pc->dF.pipelined = !c.opts.no_pipe, pc->dF.no_upper = c.opts.no_upper, pc->dF.no_col16 = c.opts.no_col16;
+    pc->dF.no_chain = c.opts.no_chain;
     pc->dF.dataflow = c.opts.no_dataflow ? 1 : (c.opts.all_dataflow ? 2 : 0);
     pc->dF.no_fused_resid = c.opts.no_fused_resid;
     pc->dF.fuse_last = !c.opts.no_fuse_last;  // single GPU: no entries outside the factor
@@ -262,6 +263,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     for (int i = 0; i < 2; i++)
         pc->dF.sweep_rows[i] = sw.rows[i], pc->dF.sweep_cap[i] = sw.cap[i], pc->dF.sweep_threads[i] = sw.threads[i];
     pc->dF.pipelined = !c.opts.no_pipe, pc->dF.no_upper = c.opts.no_upper, pc->dF.no_col16 = c.opts.no_col16;
+    pc->dF.no_chain = c.opts.no_chain;
     pc->dF.dataflow = c.opts.no_dataflow ? 1 : (c.opts.all_dataflow ? 2 : 0);
     pc->dF.no_fused_resid = c.opts.no_fused_resid;
     {

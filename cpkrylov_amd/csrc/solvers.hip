@@ -2095,6 +2095,7 @@ void method_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, 
     }
     CPK_HIP(hipEventRecord(c.ev1, c.stream));
     CPK_HIP(hipEventSynchronize(c.ev1));
+    check_chain(M.dF);
     if (stats) {
         float ms = 0;
         CPK_HIP(hipEventElapsedTime(&ms, c.ev0, c.ev1));
@@ -2201,14 +2202,15 @@ void profile_kernels(Ctx &c, const DMat &AC, Precond &M, int reps, cpk_profile *
     out->apply_ms = timeit([&]() { M.apply(x.p, M.n, z.p, nullptr); });
     out->apply_bytes = M.apply_bytes();
     out->fwd_launches = out->bwd_launches = (int64_t)M.dF.round_ptr.size() - 1;
-    if (last.valid) {  // the deferred last round: one launch inside the backward count
+    if (last.valid) {  // the deferred rounds (the last one; with the sweep chain every upper round)
+        // run as one launch inside the backward count
         out->fwd_launches = last.from;
         out->bwd_launches = last.from + 1;
         // its forward half runs in the backward launch: its bytes move with it, so
         // fwd / bwd each pair time and bytes of the same launches (the sum is unchanged)
         const DFactor &F = M.dF;
         double rows = 0, ents = 0;
-        for (int64_t b = F.round_ptr[last.from]; b < F.round_ptr[last.from + 1]; b++) {
+        for (int64_t b = F.round_ptr[last.from]; b < F.round_ptr.back(); b++) {
             const int32_t *m = &F.hmeta[(size_t)b * 8];
             rows += m[1] - m[0], ents += m[5] - m[4];
         }

@@ -211,7 +211,8 @@ int cpk_pc_get_info(cpk_pc M, cpk_pc_info *info);
 int cpk_pc_sep_info(cpk_pc M, int64_t *info);
 /* Diagnostic (not in the reference): the sweep schedule as launched, info[8] = {rounds, round-0
  * blocks, blocks above round 0, grid of the cost-balanced round-0 assignment of the forward /
- * fused-residual forward / backward kernel (0: the launch strides), round 0 persistent, 0}. */
+ * fused-residual forward / backward kernel (0: the launch strides), round 0 persistent, tasks of
+ * the sweep chain (every upper round of a solve in one launch; 0: one launch per round)}. */
 int cpk_pc_sweep_info(cpk_pc M, int64_t *info);
 int cpk_pc_local_dofs(cpk_pc M, int64_t *n_loc, int64_t *m_loc, int32_t *dofs);
 /* Export the factors P'*Kp*P = L*D*L': strict-lower L in CSC (Lcolptr[N+1], Lrowind[nnz_l],

@@ -362,6 +362,50 @@ _W64 = {}
 @pytest.mark.parametrize("name", ["cvxqp1_m", "synthetic", "w64"])
 @pytest.mark.parametrize("props", [dict(nitref=0), dict(nitref=1, force_itref=True),
                                    dict(nitref=2, force_itref=False, itref_tol=1e-30)])
+def test_precond_apply_sweep_chain(gpu_ctx, name, props):
+    """Every upper round of a solve in one launch whose blocks wait for their own producers
+    (sptrsv_chain_kernel, the default when the upper rounds use the 256-thread blocks) against
+    one launch per round (engine option no_chain) and the oracle: the default staging and small
+    upper blocks (many rounds), in every apply path (plain, forced refinement with the fused
+    residual, data-dependent refinement), repeated applies (the flags' epochs)."""
+    import cpkrylov_amd as cpk
+    if name == "w64":
+        from cpkrylov_amd.synthetic import saddle_system
+        if "s" not in _W64:
+            _W64["s"] = saddle_system(N=60000, window=64, seed=5)
+        S = _W64["s"]
+        G, B, C = S["G"], S["B"], S["C"]
+    else:
+        G, B, C = _system_gbc(name)
+    rng = np.random.default_rng(43)
+    zs = [rng.standard_normal(G.shape[0] + B.shape[0]) for _ in range(3)]
+    for sweep in ("", "64,192,64,128,512,256"):
+        ys, chains = [], []
+        for off in (False, True):
+            opts = dict(no_chain=off)
+            if sweep:
+                opts["sweep"] = sweep
+            with cpk.engine_options(**opts):
+                M = cpk.opLDL2(G, B, -C)
+            for k, v in props.items():
+                setattr(M, k, v)
+            ys.append([M * z for z in zs])
+            chains.append(M.sweep_info()["chain_tasks"])
+        assert chains[1] == 0
+        if sweep:
+            assert chains[0] > 0, M.sweep_info()
+        L, D, perm = M.export_factors()
+        Mo = O.LDL2(G, B, -C, factors=(L, D, perm))
+        Mo.set(**{k: float(v) for k, v in props.items()})
+        for i, z in enumerate(zs):
+            yo = Mo @ z
+            for y in ys:
+                assert np.array_equal(y[i], yo)
+
+
+@pytest.mark.parametrize("name", ["cvxqp1_m", "synthetic", "w64"])
+@pytest.mark.parametrize("props", [dict(nitref=0), dict(nitref=1, force_itref=True),
+                                   dict(nitref=2, force_itref=False, itref_tol=1e-30)])
 def test_precond_apply_dataflow_levels(gpu_ctx, name, props):
     """The upper rounds' two level loops: the level-synchronous loop (engine option no_dataflow)
     and the dataflow loop (levels_dataflow; all_dataflow forces it on every upper block), and the
