@@ -634,7 +634,10 @@ int cpk_pc_sweep_info(cpk_pc M, int64_t *info) {
     const DFactor &F = M->p->dF;
     const int64_t nr = (int64_t)F.round_ptr.size() - 1;
     const int64_t r0 = nr >= 1 ? F.round_ptr[1] - F.round_ptr[0] : 0;
-    const int64_t chain = (F.ch_ntask > 0 && !F.no_chain && fuse_last_ok(F)) ? F.ch_ntask : 0;
+    // the chain the sweeps launch: the full one (last round fused), else the forward one
+    const int64_t chain = F.no_chain ? 0
+                          : (F.chain[kChainFull].ntask > 0 && fuse_last_ok(F)) ? F.chain[kChainFull].ntask
+                                                                               : F.chain[kChainFwd].ntask;
     const int64_t v[8] = {nr, r0, F.nblk - r0, F.agrid[0], F.agrid[1], F.agrid[2], F.pipelined ? 1 : 0, chain};
     std::memcpy(info, v, sizeof v);
     API_END

@@ -198,6 +198,17 @@ void launch_halo(Ctx &c, const DMat &A, const double *x, bool packed = false);
 void launch_spmv_resid_loc(Ctx &c, const DMat &A, const double *xin, int64_t neg_from, const double *y, double *r,
                            const int *run, const double *halo);
 
+// A sweep chain's tasks in topological order (task = kind << 28 | block; kind 0 forward, 1 last,
+// 2 backward), each task's producer tasks (dptr / didx), a done flag per task and {epoch,
+// ticket, error} (zero at build); tpb: the block kernel it runs (256 or 512 threads)
+enum { kChainFull = 0, kChainFwd = 1, kChainBwd = 2 };
+struct DChain {
+    int64_t ntask = 0;
+    int tpb = 0;
+    DBuf<int32_t> task, dptr, didx;
+    DBuf<uint32_t> flag, ctrl;
+};
+
 // HBM-resident factor + sweep schedule (rows in schedule order).
 struct DFactor {
     int64_t N = 0, nnz = 0, nblk = 0, nlvl = 0;
@@ -233,14 +244,12 @@ struct DFactor {
     // grid they were made for (0: none; the launch then strides over meta)
     DBuf<int32_t> aptr[3], ameta[3];
     int agrid[3] = {0, 0, 0};
-    // the sweep chain (kernels.hip, sptrsv_chain_kernel): the upper rounds forward, the last round
-    // (forward + backward) and the upper rounds backward as ONE launch whose blocks wait for
-    // their own producers (flags) instead of for whole rounds.  Tasks in topological order
-    // (task = kind << 28 | block; kind 0 forward, 1 last, 2 backward), each task's producer tasks
-    // (dep_ptr / dep_idx), a done flag per task and {epoch, ticket, error} (zero at build)
-    int64_t ch_ntask = 0;
-    DBuf<int32_t> ch_task, ch_dptr, ch_didx;
-    DBuf<uint32_t> ch_flag, ch_ctrl;
+    // the sweep chains (kernels.hip, sptrsv_chain_kernel): upper rounds in ONE launch whose blocks
+    // wait for their own producers (flags) instead of for whole rounds.  kChainFull: forward
+    // rounds 1 .. R-2, the last round (forward + backward) and backward R-2 .. 1 (single GPU,
+    // the last round fused); kChainFwd / kChainBwd: the forward rounds 1 .. R-1 / the backward
+    // rounds R-1 .. 1 (a distributed solve, the separator exchange between them)
+    DChain chain[3];
     bool no_chain = false;  // engine option no_chain (set before make_dfactor)
     std::vector<int64_t> round_ptr;  // host copy: blocks per round
     std::vector<char> round_fits;    // host: every block of round r fits (sweep_rows[1], sweep_cap[1])

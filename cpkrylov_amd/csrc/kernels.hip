@@ -2067,20 +2067,21 @@ static void launch_last(Ctx &c, const DFactor &F, const FwdIn &in, double *w, do
     CPK_HIP(hipGetLastError());
 }
 
-// ---- the sweep chain -----------------------------------------------------------------------------
-// All upper rounds of a solve in ONE launch: forward rounds 1 .. R-2, the last round (forward and
-// backward, as sptrsv_last_kernel), backward rounds R-2 .. 1.  One workgroup per task, tasks in
-// topological order (blockIdx = task); a task waits for its own producers -- the blocks holding
-// the rows its entries read (build_chain) -- not for the whole previous round, then runs the
-// block exactly as the round kernels do (bit-identical) and publishes a done flag.  Deadlock-free
-// without co-residency: workgroups are dispatched in blockIdx order, so every producer of a
-// resident waiter (a smaller index) has been dispatched.  Hand-off: MI355X_MICROARCH.md "Valid
-// forms" row 1 -- every w value crossing blocks is stored and loaded sc1 (upper_block<SC>), each
-// storing wave drains (vmcnt(0)) before the workgroup barrier, one lane stores the flag sc1, and
-// consumers poll it sc1.  Flags hold the launch's epoch + 1 (no reset pass); the last workgroup
-// (ticket) advances the epoch.  Every spin is bounded: a wait that outlives kChainSpinCap sets the
-// error word, every other waiter then gives up, and the host raises CPK_ERR_HIP (check_chain).
-constexpr int kChainTPB = 256, kChainRPU = 2, kChainEPU = 12;
+// ---- the sweep chains ----------------------------------------------------------------------------
+// Upper rounds in ONE launch.  kChainFull: forward rounds 1 .. R-2, the last round (forward and
+// backward, as sptrsv_last_kernel), backward rounds R-2 .. 1 (single GPU); kChainFwd / kChainBwd:
+// forward rounds 1 .. R-1 / backward rounds R-1 .. 1 (distributed: the separator solve sits
+// between them).  One workgroup per task, tasks in topological order (blockIdx = task); a task
+// waits for its own producers -- the blocks holding the rows its entries read (build_chain) --
+// not for the whole previous round, then runs the block exactly as the round kernels do
+// (bit-identical) and publishes a done flag.  Deadlock-free without co-residency: workgroups are
+// dispatched in blockIdx order (per XCD queue), so every producer of a resident waiter (a smaller
+// index) has been dispatched.  Hand-off: MI355X_MICROARCH.md "Valid forms" row 1 -- every w value
+// crossing blocks is stored and loaded sc1 (upper_block<SC>), each storing wave drains
+// (vmcnt(0)) before the workgroup barrier, one lane stores the flag sc1, and consumers poll it
+// sc1.  Flags hold the launch's epoch + 1 (no reset pass); the last workgroup (ticket) advances
+// the epoch.  Every spin is bounded: a wait that outlives kChainSpinCap sets the error word, every
+// other waiter then gives up, and the host raises CPK_ERR_HIP (check_chain).
 constexpr uint32_t kChainSpinCap = 1u << 22;
 struct ChainArgs {
     const int32_t *task, *dptr, *didx;
@@ -2094,13 +2095,13 @@ __device__ __forceinline__ void st_agent32(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool ADD>
-__global__ __launch_bounds__(kChainTPB) void sptrsv_chain_kernel(
+template <int TPB, int RPU, int EPU, bool ADD>
+__global__ __launch_bounds__(TPB) void sptrsv_chain_kernel(
     ChainArgs ch, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ fptr, const int32_t *__restrict__ fcol, const double *__restrict__ fval,
     const uint32_t *__restrict__ bptr, const int32_t *__restrict__ bcol, const double *__restrict__ bval,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
-    int sched_in, double *xs, double *w, double *out, const int *run, const int *active, double *ys) {
+    int sched_in, double *xs, double *w, double *out, const int *run, const int *active, double *ys, PackArgs pk) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ uint32_t s_epoch;
     if (skip(run, active)) return;
@@ -2109,7 +2110,7 @@ __global__ __launch_bounds__(kChainTPB) void sptrsv_chain_kernel(
     __syncthreads();
     const uint32_t want = s_epoch + 1;
     const int d1 = ch.dptr[t + 1];
-    for (int k = ch.dptr[t] + (int)threadIdx.x; k < d1; k += kChainTPB) {
+    for (int k = ch.dptr[t] + (int)threadIdx.x; k < d1; k += TPB) {
         const uint32_t *f = ch.flag + ch.didx[k];
         uint32_t spins = 0;
         while (ld_agent32(f) != want) {
@@ -2124,17 +2125,15 @@ __global__ __launch_bounds__(kChainTPB) void sptrsv_chain_kernel(
     __syncthreads();
     const int32_t task = ch.task[t];
     const int kind = task >> 28, b = task & ((1 << 28) - 1);
-    const PackArgs none{};
     if (kind == 0)
-        upper_block<kChainTPB, kChainRPU, kChainEPU, false, false, true>(smem, meta[b], lvl_row, fptr, fcol, fval, D, perm,
-                                                                         xin, neg_from, w, nullptr, sched_in, nullptr,
-                                                                         xs, none, b);
+        upper_block<TPB, RPU, EPU, false, false, true>(smem, meta[b], lvl_row, fptr, fcol, fval, D, perm, xin, neg_from, w,
+                                                       nullptr, sched_in, nullptr, xs, pk, b);
     else if (kind == 1)
-        last_block<kChainTPB, kChainRPU, kChainEPU, ADD, true>(smem, meta[b], lvl_row, fptr, fcol, fval, bptr, bcol, bval,
-                                                               D, perm, xin, neg_from, sched_in, xs, w, out, ys);
+        last_block<TPB, RPU, EPU, ADD, true>(smem, meta[b], lvl_row, fptr, fcol, fval, bptr, bcol, bval, D, perm, xin,
+                                             neg_from, sched_in, xs, w, out, ys);
     else
-        upper_block<kChainTPB, kChainRPU, kChainEPU, true, ADD, true>(smem, meta[b], lvl_row, bptr, bcol, bval, D, perm,
-                                                                      nullptr, 0, w, out, 0, ys, nullptr, none, b);
+        upper_block<TPB, RPU, EPU, true, ADD, true>(smem, meta[b], lvl_row, bptr, bcol, bval, D, perm, nullptr, 0, w, out,
+                                                    0, ys, nullptr, pk, b);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w stores done
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2147,101 +2146,138 @@ __global__ __launch_bounds__(kChainTPB) void sptrsv_chain_kernel(
     }
 }
 
-static void build_chain(DFactor &d, const std::vector<int32_t> &meta, const std::vector<uint32_t> &fptr,
-                        const std::vector<int32_t> &fcol, const std::vector<uint32_t> &bptr,
-                        const std::vector<int32_t> &bcol) {
-    d.ch_ntask = 0;
+// the block kernel a chain runs: 256 threads (blocks of <= 512 rows / 3072 entries, the single-
+// GPU default) or 512 (<= 1024 / 4096, the distributed default); 0: none
+static int chain_tpb(const DFactor &d) {
+    if (d.sweep_threads[1] == 256 && d.sweep_rows[1] <= 512 && d.sweep_cap[1] <= 3072) return 256;
+    if (d.sweep_threads[1] == 512 && d.sweep_rows[1] <= 1024 && d.sweep_cap[1] <= 4096) return 512;
+    return 0;
+}
+
+static void build_chain_kind(DFactor &d, int kind, const std::vector<int32_t> &blk, const std::vector<int32_t> &meta,
+                             const std::vector<uint32_t> &fptr, const std::vector<int32_t> &fcol,
+                             const std::vector<uint32_t> &bptr, const std::vector<int32_t> &bcol) {
+    DChain &ch = d.chain[kind];
     const int64_t R = (int64_t)d.round_ptr.size() - 1;
-    if (d.no_chain || d.no_upper || R < 3 || d.round0_rows < 0) return;
-    if (d.sweep_threads[1] != kChainTPB || d.sweep_rows[1] > kChainRPU * kChainTPB ||
-        d.sweep_cap[1] > kChainEPU * kChainTPB)
-        return;
-    for (int64_t r = 1; r < R; r++)
-        if (r >= (int64_t)d.round_fits.size() || !d.round_fits[r]) return;
     const int64_t N = d.N, base = d.round0_rows;
-    const int64_t b1 = d.round_ptr[1], bl = d.round_ptr[R - 1], be = d.round_ptr[R];
-    std::vector<int32_t> blk((size_t)(N - base), -1);
-    for (int64_t b = b1; b < be; b++)
-        for (int32_t i = meta[(size_t)b * 8]; i < meta[(size_t)b * 8 + 1]; i++) blk[(size_t)(i - base)] = (int32_t)b;
-    for (int32_t x : blk)
-        if (x < 0) return;  // upper rows not all in upper blocks
-    // task ids: forward and last tasks in block order (= round order), then backward tasks from
-    // the highest round down
-    const int64_t nfl = be - b1, nt = nfl + (bl - b1);
-    auto fwd_task = [&](int64_t b) { return (int32_t)(b - b1); };
-    auto bwd_task = [&](int64_t b) { return b >= bl ? (int32_t)(b - b1) : (int32_t)(nfl + (bl - 1 - b)); };
-    std::vector<int32_t> task((size_t)nt), dptr((size_t)nt + 1, 0), didx;
-    std::vector<int32_t> deps;
+    const int64_t b1 = d.round_ptr[1], be = d.round_ptr[R];
+    // forward tasks for blocks [b1, bf), the last round's blocks [bf, be) as last tasks (full
+    // chain), backward tasks for blocks [b1, bb) from the highest round down
+    const int64_t bl = d.round_ptr[R - 1];
+    const int64_t bf = kind == kChainFull ? bl : (kind == kChainFwd ? be : b1);
+    const int64_t nlast = kind == kChainFull ? be - bl : 0;
+    const int64_t bb = kind == kChainFull ? bl : (kind == kChainBwd ? be : b1);
+    const int64_t nfl = (bf - b1) + nlast, nt = nfl + (bb - b1);
+    if (nt <= 0 || nt >= (1 << 28)) return;
+    auto fwd_task = [&](int64_t b) { return (int32_t)(b - b1); };  // forward and last tasks: block order
+    auto bwd_task = [&](int64_t b) {
+        return (kind == kChainFull && b >= bl) ? (int32_t)(b - b1) : (int32_t)(nfl + (bb - 1 - b));
+    };
+    std::vector<int32_t> task((size_t)nt), dptr((size_t)nt + 1, 0), didx, deps;
     bool ok = true;
     auto emit = [&](int32_t t) {
         std::sort(deps.begin(), deps.end());
         deps.erase(std::unique(deps.begin(), deps.end()), deps.end());
-        for (int32_t p : deps) ok = ok && p < t;
+        for (int32_t p : deps) ok = ok && p >= 0 && p < t;
         didx.insert(didx.end(), deps.begin(), deps.end());
         dptr[(size_t)t + 1] = (int32_t)didx.size();
         deps.clear();
     };
-    for (int64_t b = b1; b < be && ok; b++) {  // forward (rounds 1 .. R-2) and last (round R-1)
+    auto upper = [&](int32_t c) { return c >= base && c < N; };  // a row of this launch (T rows: c >= N)
+    for (int64_t b = b1; b < b1 + nfl && ok; b++) {  // forward / last
         const int32_t *m = &meta[(size_t)b * 8];
+        const bool last = b >= bf;
         for (int32_t i = m[0]; i < m[1]; i++) {
-            for (uint32_t e = fptr[i]; e < fptr[i + 1]; e++) {
-                const int32_t c = fcol[e];
-                if (c >= base && c < N && (c < m[0] || c >= m[1])) deps.push_back(fwd_task(blk[(size_t)(c - base)]));
-            }
-            if (b >= bl)  // a last-round block's backward terms must stay inside it (sptrsv_last_kernel)
+            for (uint32_t e = fptr[i]; e < fptr[i + 1]; e++)
+                if (upper(fcol[e]) && (fcol[e] < m[0] || fcol[e] >= m[1])) deps.push_back(fwd_task(blk[(size_t)(fcol[e] - base)]));
+            if (last)  // a last-round block's backward terms must stay inside it (sptrsv_last_kernel)
                 for (uint32_t e = bptr[i]; e < bptr[i + 1]; e++)
-                    if (bcol[e] < N && bcol[e] >= base && (bcol[e] < m[0] || bcol[e] >= m[1])) ok = false;
+                    if (upper(bcol[e]) && (bcol[e] < m[0] || bcol[e] >= m[1])) ok = false;
         }
-        task[(size_t)fwd_task(b)] = (int32_t)((b >= bl ? 1 : 0) << 28 | b);
+        task[(size_t)fwd_task(b)] = (int32_t)((last ? 1 : 0) << 28 | b);
         emit(fwd_task(b));
     }
-    for (int64_t b = bl - 1; b >= b1 && ok; b--) {  // backward, highest round first
+    for (int64_t b = bb - 1; b >= b1 && ok; b--) {  // backward, highest round first
         const int32_t *m = &meta[(size_t)b * 8];
-        deps.push_back(fwd_task(b));  // its own forward values
+        if (kind == kChainFull) deps.push_back(fwd_task(b));  // its own forward values, this launch
         for (int32_t i = m[0]; i < m[1]; i++)
-            for (uint32_t e = bptr[i]; e < bptr[i + 1]; e++) {
-                const int32_t c = bcol[e];
-                if (c >= base && c < N && (c < m[0] || c >= m[1])) deps.push_back(bwd_task(blk[(size_t)(c - base)]));
-            }
+            for (uint32_t e = bptr[i]; e < bptr[i + 1]; e++)
+                if (upper(bcol[e]) && (bcol[e] < m[0] || bcol[e] >= m[1])) deps.push_back(bwd_task(blk[(size_t)(bcol[e] - base)]));
         task[(size_t)bwd_task(b)] = (int32_t)(2 << 28 | b);
         emit(bwd_task(b));
     }
-    if (!ok || nt >= (1 << 28)) return;
-    d.ch_task.upload(task);
-    d.ch_dptr.upload(dptr);
-    d.ch_didx.upload(didx.empty() ? std::vector<int32_t>{0} : didx);
-    d.ch_flag.alloc((size_t)nt);
-    CPK_HIP(hipMemset(d.ch_flag.p, 0, d.ch_flag.bytes()));
-    d.ch_ctrl.alloc(4);
-    CPK_HIP(hipMemset(d.ch_ctrl.p, 0, d.ch_ctrl.bytes()));
-    d.ch_ntask = nt;
+    if (!ok) return;
+    ch.task.upload(task);
+    ch.dptr.upload(dptr);
+    ch.didx.upload(didx.empty() ? std::vector<int32_t>{0} : didx);
+    ch.flag.alloc((size_t)nt);
+    CPK_HIP(hipMemset(ch.flag.p, 0, ch.flag.bytes()));
+    ch.ctrl.alloc(4);
+    CPK_HIP(hipMemset(ch.ctrl.p, 0, ch.ctrl.bytes()));
+    ch.tpb = chain_tpb(d);
+    ch.ntask = nt;
 }
 
-static bool chain_ok(const DFactor &F) { return F.ch_ntask > 0 && !F.no_chain && fuse_last_ok(F); }
+static void build_chain(DFactor &d, const std::vector<int32_t> &meta, const std::vector<uint32_t> &fptr,
+                        const std::vector<int32_t> &fcol, const std::vector<uint32_t> &bptr,
+                        const std::vector<int32_t> &bcol) {
+    for (DChain &c : d.chain) c.ntask = 0;
+    const int64_t R = (int64_t)d.round_ptr.size() - 1;
+    // two upper rounds at least (one round has nothing to chain), every one through the block kernel
+    if (d.no_chain || d.no_upper || R < 3 || d.round0_rows < 0 || !chain_tpb(d)) return;
+    for (int64_t r = 1; r < R; r++)
+        if (r >= (int64_t)d.round_fits.size() || !d.round_fits[r]) return;
+    const int64_t N = d.N, base = d.round0_rows;
+    std::vector<int32_t> blk((size_t)(N - base), -1);
+    for (int64_t b = d.round_ptr[1]; b < d.round_ptr[R]; b++)
+        for (int32_t i = meta[(size_t)b * 8]; i < meta[(size_t)b * 8 + 1]; i++) blk[(size_t)(i - base)] = (int32_t)b;
+    for (int32_t x : blk)
+        if (x < 0) return;  // upper rows not all in upper blocks
+    for (int k : {kChainFull, kChainFwd, kChainBwd}) build_chain_kind(d, k, blk, meta, fptr, fcol, bptr, bcol);
+}
 
-static void launch_chain(Ctx &c, const DFactor &F, const FwdIn &in, double *w, double *out, bool add, const int *run,
-                         const int *active, double *ys) {
-    const size_t lds = sweep_lds_bytes(kChainRPU * kChainTPB, kChainEPU * kChainTPB);
-    const ChainArgs ch{F.ch_task.p, F.ch_dptr.p, F.ch_didx.p, F.ch_flag.p, F.ch_ctrl.p, (int)F.ch_ntask};
+static bool chain_ok(const DFactor &F, int kind) {
+    return F.chain[kind].ntask > 0 && !F.no_chain && (kind != kChainFull || fuse_last_ok(F));
+}
+
+template <int TPB, int RPU, int EPU>
+static void launch_chain_t(Ctx &c, const DFactor &F, int kind, const FwdIn &in, double *w, double *out, bool add,
+                           const int *run, const int *active, double *ys, const PackArgs &pk) {
+    const DChain &h = F.chain[kind];
+    const size_t lds = sweep_lds_bytes(RPU * TPB, EPU * TPB);
+    static const bool lds_ok = lds <= 64 * 1024 ||
+        (hipFuncSetAttribute((const void *)sptrsv_chain_kernel<TPB, RPU, EPU, false>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
+         hipFuncSetAttribute((const void *)sptrsv_chain_kernel<TPB, RPU, EPU, true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess);
+    if (!lds_ok) throw Error(CPK_ERR_HIP, "sptrsv_chain_kernel: LDS image not admitted");
+    const ChainArgs ch{h.task.p, h.dptr.p, h.didx.p, h.flag.p, h.ctrl.p, (int)h.ntask};
     const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
     if (add)
-        hipLaunchKernelGGL(sptrsv_chain_kernel<true>, dim3((unsigned)F.ch_ntask), dim3(kChainTPB), lds, c.stream, ch, meta,
-                           F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p,
-                           in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys);
+        hipLaunchKernelGGL((sptrsv_chain_kernel<TPB, RPU, EPU, true>), dim3((unsigned)h.ntask), dim3(TPB), lds, c.stream,
+                           ch, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
+                           F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, pk);
     else
-        hipLaunchKernelGGL(sptrsv_chain_kernel<false>, dim3((unsigned)F.ch_ntask), dim3(kChainTPB), lds, c.stream, ch,
-                           meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys);
+        hipLaunchKernelGGL((sptrsv_chain_kernel<TPB, RPU, EPU, false>), dim3((unsigned)h.ntask), dim3(TPB), lds,
+                           c.stream, ch, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p,
+                           F.D.p, F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, pk);
     CPK_HIP(hipGetLastError());
+}
+static void launch_chain(Ctx &c, const DFactor &F, int kind, const FwdIn &in, double *w, double *out, bool add,
+                         const int *run, const int *active, double *ys, const PackArgs &pk) {
+    if (F.chain[kind].tpb == 512) launch_chain_t<512, 2, 8>(c, F, kind, in, w, out, add, run, active, ys, pk);
+    else launch_chain_t<256, 2, 12>(c, F, kind, in, w, out, add, run, active, ys, pk);
 }
 
 void check_chain(const DFactor &F) {
-    if (F.ch_ntask <= 0) return;
-    uint32_t err = 0;
-    CPK_HIP(hipMemcpy(&err, F.ch_ctrl.p + 2, sizeof err, hipMemcpyDeviceToHost));
-    if (err) {
-        CPK_HIP(hipMemset(F.ch_ctrl.p + 2, 0, sizeof err));
-        throw Error(CPK_ERR_HIP, "sweep chain: a block's wait for its producers timed out");
+    for (const DChain &h : F.chain) {
+        if (h.ntask <= 0) continue;
+        uint32_t err = 0;
+        CPK_HIP(hipMemcpy(&err, h.ctrl.p + 2, sizeof err, hipMemcpyDeviceToHost));
+        if (err) {
+            CPK_HIP(hipMemset(h.ctrl.p + 2, 0, sizeof err));
+            throw Error(CPK_ERR_HIP, "sweep chain: a block's wait for its producers timed out");
+        }
     }
 }
 
@@ -2802,7 +2838,7 @@ static bool fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
                     const PackArgs *pk = nullptr) {
     int64_t R = (int64_t)F.round_ptr.size() - 1;
     bool packed = pk != nullptr;  // every round launched here through a packing kernel
-    if (defer && chain_ok(F) && rfirst <= 1) {  // every upper round runs in the backward sweep's chain
+    if (defer && chain_ok(F, kChainFull) && rfirst <= 1) {  // every upper round runs in the backward sweep's chain
         *defer = FwdIn{xin, neg_from, sched_in, xs, true, 1, true};
         R = 1;
         packed = false;
@@ -2812,7 +2848,14 @@ static bool fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
         packed = false;  // the deferred round's rows are packed by no launch here
     }
     const PackArgs none{};
+    // no deferral: the forward chain runs rounds 1 .. R-1 (distributed: the separator follows)
+    const bool fchain = !(defer && defer->valid) && chain_ok(F, kChainFwd) && rfirst <= 1 && R >= 2;
     for (int64_t r = rfirst; r < R; r++) {
+        if (r == 1 && fchain) {
+            launch_chain(c, F, kChainFwd, FwdIn{xin, neg_from, sched_in, xs, true, 1}, w, nullptr, false, run, active,
+                         nullptr, pk ? *pk : none);
+            break;
+        }
         bool used = true;
         if (r == 0 &&
             pipe_round0(c, F, false, false, xin, neg_from, w, nullptr, run, active, sched_in, nullptr, xs, nullptr, pk,
@@ -2896,7 +2939,10 @@ bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
     bool packed = pk != nullptr && !(last && last->valid);
     const PackArgs none{};
     if (last && last->valid && last->chain) {  // the deferred upper rounds: one chain launch
-        launch_chain(c, F, *last, w, out, add, run, active, ys);
+        launch_chain(c, F, kChainFull, *last, w, out, add, run, active, ys, none);
+        R = 1;
+    } else if (!(last && last->valid) && chain_ok(F, kChainBwd) && R >= 3) {  // backward rounds R-1 .. 1
+        launch_chain(c, F, kChainBwd, FwdIn{}, w, out, add, run, active, ys, pk ? *pk : none);
         R = 1;
     } else if (last && last->valid) {  // the deferred last round, forward and backward (sptrsv_last_kernel)
         launch_last(c, F, *last, w, out, add, run, active, ys);

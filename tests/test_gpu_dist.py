@@ -84,6 +84,39 @@ def test_dist_apply_bitexact(name, P, props):
         assert np.all(d[:nl] < S["n"]) and np.all(d[nl:] >= S["n"])
 
 
+@pytest.mark.parametrize("P", [1, 2, 4])
+@pytest.mark.parametrize("name", ["cvxqp1_m", "synthetic20k"])
+def test_dist_apply_sweep_chain_bitexact(name, P):
+    """The sweep chains on a distributed preconditioner: each rank's forward upper rounds in one
+    launch (kChainFwd, before the separator exchange) and its backward upper rounds in one launch
+    (kChainBwd, after the separator solve) -- at P = 1 the full chain with the last round fused --
+    against one launch per round (no_chain) and the oracle, with small upper blocks (many rounds),
+    three applies with one forced refinement step."""
+    import cpkrylov_amd as cpk
+    S = _system(name)
+    rng = np.random.default_rng(53)
+    zs = [rng.standard_normal(S["n"] + S["m"]) for _ in range(3)]
+
+    def work(ctx, r):
+        M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+        M.nitref, M.force_itref = 1, True
+        return [M * z for z in zs], M.export_factors() if r == 0 else None, M.sweep_info()["chain_tasks"]
+
+    res = {}
+    for off in (False, True):
+        res[off] = _run_ranks(P, work, dict(sweep="64,192,64,128,512,512", no_chain=off))
+        chains = [ch for _, _, ch in res[off]]
+        assert (max(chains) > 0) != off, chains
+    L, D, perm = res[False][0][1]
+    Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=(L, D, perm))
+    Mo.set(nitref=1.0, force_itref=1.0)
+    for i, z in enumerate(zs):
+        yo = Mo @ z
+        for off in (False, True):
+            for ys, _, _ in res[off]:
+                assert np.array_equal(ys[i], yo), (off, np.max(np.abs(ys[i] - yo)))
+
+
 @pytest.mark.parametrize("P", [1, 2, 3, 4])
 @pytest.mark.parametrize("name", ["cvxqp1_m", "synthetic20k"])
 def test_dist_refinement_without_kp_halo(name, P):

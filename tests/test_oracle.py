@@ -179,3 +179,51 @@ def test_threaded_leg_sweeps_bitexact():
     h1, h4 = s1["residHistory"], s4["residHistory"]
     assert np.max(np.abs(h1 - h4)) <= 1e-8 * h1[0]
     assert np.linalg.norm(x1 - x4) <= 1e-8 * np.linalg.norm(x1)
+
+
+def test_exact_dot_correctly_rounded():
+    """orc_set_exact's inner product: the correctly rounded exact sum of the TwoProd pairs, i.e.
+    (no product under- or overflowing) the correctly rounded exact dot product -- checked against
+    Python's exact rational arithmetic, including cancellation, subnormals, ties to even and
+    overflow; and independent of the thread count."""
+    from fractions import Fraction as Fr
+    rng = np.random.default_rng(11)
+    for _ in range(25):
+        n = int(rng.integers(1, 2000))
+        a = rng.standard_normal(n) * np.exp(rng.uniform(-40, 40, n))
+        b = rng.standard_normal(n) * np.exp(rng.uniform(-40, 40, n))
+        ref = float(sum(Fr(float(x)) * Fr(float(y)) for x, y in zip(a, b)))
+        assert O.xdot(a, b) == ref
+    one = np.ones(8)
+    cases = [([1e100, 1.0, -1e100, 1e-300, 3.0], 4.0),
+             ([5e-324, 5e-324, -1e-320], -9.99e-321),
+             ([1.0, 2.0 ** -53], 1.0),                          # tie: to even
+             ([1.0, 2.0 ** -53, 2.0 ** -200], 1.0 + 2.0 ** -52),  # above the tie
+             ([1.0 + 2.0 ** -52, 2.0 ** -53], 1.0 + 2.0 ** -51),  # tie: to even (up)
+             ([1.7e308, 1.7e308], np.inf), ([-1.5, 0.25], -1.25), ([0.0, -0.0], 0.0)]
+    for v, want in cases:
+        v = np.array(v)
+        assert O.xdot(v, one[:len(v)]) == want, (v, O.xdot(v, one[:len(v)]), want)
+    a, b = rng.standard_normal(500_000), rng.standard_normal(500_000)
+    vals = []
+    for t in (1, 2, 5, 8):
+        O.set_threads(t)
+        try:
+            vals.append(O.xdot(a, b))
+        finally:
+            O.set_threads(1)
+    assert len(set(vals)) == 1
+
+
+def test_exact_norm2_formula():
+    """the exact mode's norm([a b]) (shared with the device): exact on Pythagorean triples,
+    no overflow or underflow at the ends of the range, within an ulp of hypot elsewhere"""
+    import math
+    assert O.xnorm2(3.0, 4.0) == 5.0 and O.xnorm2(-5.0, 12.0) == 13.0
+    assert O.xnorm2(0.0, -2.5) == 2.5 and O.xnorm2(0.0, 0.0) == 0.0
+    assert O.xnorm2(1e300, 1e300) == math.hypot(1e300, 1e300)
+    assert O.xnorm2(3e-310, 4e-310) == math.hypot(3e-310, 4e-310)
+    rng = np.random.default_rng(5)
+    for x, y in rng.standard_normal((2000, 2)) * np.exp(rng.uniform(-20, 20, (2000, 2))):
+        h = math.hypot(x, y)
+        assert abs(O.xnorm2(x, y) - h) <= math.ulp(h)
