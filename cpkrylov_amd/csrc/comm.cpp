@@ -8,6 +8,7 @@
 //           not capturable and not a performance path.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -99,8 +100,20 @@ struct SimGroup {
     uint64_t gen = 0;
     DBuf<double> shared;  // grown on demand to the largest collective (every rank asks the same n)
     static constexpr size_t kCap0 = size_t(16) << 20;  // doubles
-    explicit SimGroup(int p) : P(p) {}
-    void barrier() {
+    // each rank's collective count and the last one it entered: a rank that waits in vain names
+    // where every rank is (a mismatched collective sequence, or a rank stuck in a device wait)
+    std::vector<uint64_t> seq;
+    std::vector<std::string> last;
+    int timeout_s = 300;  // CPK_SIM_TIMEOUT_S
+    explicit SimGroup(int p) : P(p), seq(p, 0), last(p) {
+        if (const char *e = std::getenv("CPK_SIM_TIMEOUT_S")) timeout_s = std::max(1, std::atoi(e));
+    }
+    void enter(int rank, const char *op, size_t n) {
+        std::lock_guard<std::mutex> lk(mu);
+        seq[rank]++;
+        last[rank] = std::string(op) + "(" + std::to_string(n) + ")";
+    }
+    void barrier(int rank) {
         std::unique_lock<std::mutex> lk(mu);
         const uint64_t g = gen;
         if (++arrived == P) {
@@ -108,8 +121,12 @@ struct SimGroup {
             cv.notify_all();
             return;
         }
-        if (!cv.wait_for(lk, std::chrono::seconds(300), [&] { return gen != g; }))
-            throw Error(CPK_ERR_RCCL, "simulated collective: a rank did not arrive within 300 s");
+        if (!cv.wait_for(lk, std::chrono::seconds(timeout_s), [&] { return gen != g; })) {
+            std::string m = "simulated collective: rank " + std::to_string(rank) + " waited " +
+                            std::to_string(timeout_s) + " s;";
+            for (int q = 0; q < P; q++) m += " [" + std::to_string(q) + ": #" + std::to_string(seq[q]) + " " + last[q] + "]";
+            throw Error(CPK_ERR_RCCL, m);
+        }
     }
 };
 
@@ -122,37 +139,40 @@ struct SimComm : Comm {
         if (n * (size_t)g->P <= g->shared.n) return;
         // every rank of a collective passes the same n: all arrive, rank 0 grows the buffer
         // while the others wait, then all continue with the new one
-        g->barrier();
+        g->barrier(rank);
         if (rank == 0) g->shared.alloc(n * (size_t)g->P);
-        g->barrier();
+        g->barrier(rank);
     }
     void allreduce_sum(double *buf, size_t n, hipStream_t s) override {
+        g->enter(rank, "allreduce_sum", n);
+        g->enter(rank, "allreduce_sum_i64", n);
+        g->enter(rank, "allgather", n);
         check(n);
         CPK_HIP(hipMemcpyAsync(g->shared.p + rank * n, buf, n * sizeof(double), hipMemcpyDeviceToDevice, s));
         CPK_HIP(hipStreamSynchronize(s));
-        g->barrier();
+        g->barrier(rank);
         launch_sum_slots(s, g->shared.p, g->P, n, buf);
         CPK_HIP(hipStreamSynchronize(s));
-        g->barrier();
+        g->barrier(rank);
     }
     void allreduce_sum_i64(int64_t *buf, size_t n, hipStream_t s) override {
         check(n);  // the shared buffer holds 8-byte words: the digits travel as their bits
         int64_t *sh = reinterpret_cast<int64_t *>(g->shared.p);
         CPK_HIP(hipMemcpyAsync(sh + rank * n, buf, n * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
         CPK_HIP(hipStreamSynchronize(s));
-        g->barrier();
+        g->barrier(rank);
         launch_sum_slots_i64(s, sh, g->P, n, buf);
         CPK_HIP(hipStreamSynchronize(s));
-        g->barrier();
+        g->barrier(rank);
     }
     void allgather(const double *send, double *recv, size_t n, hipStream_t s) override {
         check(n);
         if (n) CPK_HIP(hipMemcpyAsync(g->shared.p + rank * n, send, n * sizeof(double), hipMemcpyDeviceToDevice, s));
         CPK_HIP(hipStreamSynchronize(s));
-        g->barrier();
+        g->barrier(rank);
         if (n) CPK_HIP(hipMemcpyAsync(recv, g->shared.p, n * g->P * sizeof(double), hipMemcpyDeviceToDevice, s));
         CPK_HIP(hipStreamSynchronize(s));
-        g->barrier();
+        g->barrier(rank);
     }
     bool capturable() const override { return false; }
     int kind() const override { return CPK_COMM_SIM; }

@@ -244,12 +244,13 @@ struct DFactor {
     // grid they were made for (0: none; the launch then strides over meta)
     DBuf<int32_t> aptr[3], ameta[3];
     int agrid[3] = {0, 0, 0};
-    // the sweep chains (kernels.hip, sptrsv_chain_kernel): upper rounds in ONE launch whose blocks
-    // wait for their own producers (flags) instead of for whole rounds.  kChainFull: forward
-    // rounds 1 .. R-2, the last round (forward + backward) and backward R-2 .. 1 (single GPU,
-    // the last round fused); kChainFwd / kChainBwd: the forward rounds 1 .. R-1 / the backward
-    // rounds R-1 .. 1 (a distributed solve, the separator exchange between them)
+    // the sweep chains (kernels.hip, sptrsv_chain_kernel): the narrow top rounds [chain_first, R)
+    // in ONE launch whose blocks wait for their own producers (flags) instead of for whole
+    // rounds.  kChainFull: those rounds forward, the last round (forward + backward) and those
+    // rounds backward (single GPU, the last round fused); kChainFwd / kChainBwd: forward only /
+    // backward only (a distributed solve, the separator exchange between them)
     DChain chain[3];
+    int64_t chain_first = 1;  // the first chained round (the chains cover [chain_first, R))
     bool no_chain = false;  // engine option no_chain (set before make_dfactor)
     std::vector<int64_t> round_ptr;  // host copy: blocks per round
     std::vector<char> round_fits;    // host: every block of round r fits (sweep_rows[1], sweep_cap[1])

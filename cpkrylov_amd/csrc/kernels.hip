@@ -2082,7 +2082,12 @@ static void launch_last(Ctx &c, const DFactor &F, const FwdIn &in, double *w, do
 // sc1.  Flags hold the launch's epoch + 1 (no reset pass); the last workgroup (ticket) advances
 // the epoch.  Every spin is bounded: a wait that outlives kChainSpinCap sets the error word, every
 // other waiter then gives up, and the host raises CPK_ERR_HIP (check_chain).
-constexpr uint32_t kChainSpinCap = 1u << 22;
+constexpr uint32_t kChainSpinCap = 1u << 20;
+// the rounds a chain covers: the narrow top of the tree (rounds of at most kChainWide blocks,
+// and at least two of them).  A wide round's blocks are all ready at once -- a launch of their
+// own costs nothing there -- and in a chain hundreds of its blocks would sit polling the few
+// flags of the round above: the guide's warning, many pollers cut the chip's bandwidth.
+constexpr int64_t kChainWide = 256;
 struct ChainArgs {
     const int32_t *task, *dptr, *didx;
     uint32_t *flag, *ctrl;
@@ -2119,7 +2124,9 @@ __global__ __launch_bounds__(TPB) void sptrsv_chain_kernel(
                 st_agent32(ch.ctrl + 2, 1);
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            // back off: a few quick polls, then ~1000 cycles apart (poll traffic stays low)
+            if (spins < 16) __builtin_amdgcn_s_sleep(2);
+            else __builtin_amdgcn_s_sleep(16);
         }
     }
     __syncthreads();
@@ -2159,8 +2166,8 @@ static void build_chain_kind(DFactor &d, int kind, const std::vector<int32_t> &b
                              const std::vector<uint32_t> &bptr, const std::vector<int32_t> &bcol) {
     DChain &ch = d.chain[kind];
     const int64_t R = (int64_t)d.round_ptr.size() - 1;
-    const int64_t N = d.N, base = d.round0_rows;
-    const int64_t b1 = d.round_ptr[1], be = d.round_ptr[R];
+    const int64_t b1 = d.round_ptr[d.chain_first], be = d.round_ptr[R];
+    const int64_t N = d.N, base = meta[(size_t)b1 * 8];  // the chain's first row
     // forward tasks for blocks [b1, bf), the last round's blocks [bf, be) as last tasks (full
     // chain), backward tasks for blocks [b1, bb) from the highest round down
     const int64_t bl = d.round_ptr[R - 1];
@@ -2223,13 +2230,18 @@ static void build_chain(DFactor &d, const std::vector<int32_t> &meta, const std:
                         const std::vector<int32_t> &bcol) {
     for (DChain &c : d.chain) c.ntask = 0;
     const int64_t R = (int64_t)d.round_ptr.size() - 1;
-    // two upper rounds at least (one round has nothing to chain), every one through the block kernel
     if (d.no_chain || d.no_upper || R < 3 || d.round0_rows < 0 || !chain_tpb(d)) return;
-    for (int64_t r = 1; r < R; r++)
+    // the chained rounds: the narrow top [first, R), two rounds at least, every one through the
+    // block kernel
+    int64_t first = R;
+    while (first > 1 && d.round_ptr[first] - d.round_ptr[first - 1] <= kChainWide) first--;
+    if (R - first < 2) return;
+    for (int64_t r = first; r < R; r++)
         if (r >= (int64_t)d.round_fits.size() || !d.round_fits[r]) return;
-    const int64_t N = d.N, base = d.round0_rows;
+    d.chain_first = first;
+    const int64_t N = d.N, base = meta[(size_t)d.round_ptr[first] * 8];
     std::vector<int32_t> blk((size_t)(N - base), -1);
-    for (int64_t b = d.round_ptr[1]; b < d.round_ptr[R]; b++)
+    for (int64_t b = d.round_ptr[first]; b < d.round_ptr[R]; b++)
         for (int32_t i = meta[(size_t)b * 8]; i < meta[(size_t)b * 8 + 1]; i++) blk[(size_t)(i - base)] = (int32_t)b;
     for (int32_t x : blk)
         if (x < 0) return;  // upper rows not all in upper blocks
@@ -2838,9 +2850,9 @@ static bool fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
                     const PackArgs *pk = nullptr) {
     int64_t R = (int64_t)F.round_ptr.size() - 1;
     bool packed = pk != nullptr;  // every round launched here through a packing kernel
-    if (defer && chain_ok(F, kChainFull) && rfirst <= 1) {  // every upper round runs in the backward sweep's chain
-        *defer = FwdIn{xin, neg_from, sched_in, xs, true, 1, true};
-        R = 1;
+    if (defer && chain_ok(F, kChainFull) && rfirst <= F.chain_first) {  // the chained rounds run in the backward sweep's chain
+        *defer = FwdIn{xin, neg_from, sched_in, xs, true, F.chain_first, true};
+        R = F.chain_first;
         packed = false;
     } else if (defer && fuse_last_ok(F)) {  // the last round runs with the backward sweep
         *defer = FwdIn{xin, neg_from, sched_in, xs, true, R - 1};
@@ -2849,10 +2861,10 @@ static bool fwd_all(Ctx &c, const DFactor &F, const double *xin, int64_t neg_fro
     }
     const PackArgs none{};
     // no deferral: the forward chain runs rounds 1 .. R-1 (distributed: the separator follows)
-    const bool fchain = !(defer && defer->valid) && chain_ok(F, kChainFwd) && rfirst <= 1 && R >= 2;
+    const bool fchain = !(defer && defer->valid) && chain_ok(F, kChainFwd) && rfirst <= F.chain_first;
     for (int64_t r = rfirst; r < R; r++) {
-        if (r == 1 && fchain) {
-            launch_chain(c, F, kChainFwd, FwdIn{xin, neg_from, sched_in, xs, true, 1}, w, nullptr, false, run, active,
+        if (r == F.chain_first && fchain) {  // the chained rounds [chain_first, R)
+            launch_chain(c, F, kChainFwd, FwdIn{xin, neg_from, sched_in, xs, true, r}, w, nullptr, false, run, active,
                          nullptr, pk ? *pk : none);
             break;
         }
@@ -2938,12 +2950,12 @@ bool launch_sptrsv_bwd(Ctx &c, const DFactor &F, double *w, double *out, bool ad
     int64_t R = (int64_t)F.round_ptr.size() - 1;
     bool packed = pk != nullptr && !(last && last->valid);
     const PackArgs none{};
-    if (last && last->valid && last->chain) {  // the deferred upper rounds: one chain launch
+    if (last && last->valid && last->chain) {  // the deferred chained rounds: one launch
         launch_chain(c, F, kChainFull, *last, w, out, add, run, active, ys, none);
-        R = 1;
-    } else if (!(last && last->valid) && chain_ok(F, kChainBwd) && R >= 3) {  // backward rounds R-1 .. 1
+        R = F.chain_first;
+    } else if (!(last && last->valid) && chain_ok(F, kChainBwd)) {  // backward rounds R-1 .. chain_first
         launch_chain(c, F, kChainBwd, FwdIn{}, w, out, add, run, active, ys, pk ? *pk : none);
-        R = 1;
+        R = F.chain_first;
     } else if (last && last->valid) {  // the deferred last round, forward and backward (sptrsv_last_kernel)
         launch_last(c, F, *last, w, out, add, run, active, ys);
         R = last->from;

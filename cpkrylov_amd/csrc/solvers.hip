@@ -1540,7 +1540,7 @@ struct SolveCore {
     double *vec(size_t i) {
         while (vecs.size() <= i) {
             vecs.emplace_back();
-            vecs.back().alloc(N);
+            vecs.back().alloc(std::max<size_t>((size_t)N, 1));  // a rank may own no rows
         }
         return vecs[i].p;
     }
@@ -1548,7 +1548,8 @@ struct SolveCore {
     double *ring(size_t count) {
         if (ring_next == rings.size()) rings.emplace_back();
         DBuf<double> &r = rings[ring_next++];
-        if (r.n != count * (size_t)N) r.alloc(std::max<size_t>(count * (size_t)N, 1));
+        const size_t want = std::max<size_t>(count * (size_t)N, 1);  // a rank may own no rows
+        if (r.n != want) r.alloc(want);
         return r.p;
     }
     template <class T>

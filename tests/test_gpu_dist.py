@@ -194,6 +194,38 @@ def test_dist_reg_cpkrylov_matches_oracle(name, method, extra, P):
     assert dx <= max(FLOOR, SAFETY * bd["x"]), (dx, bd["x"])
 
 
+@pytest.mark.parametrize("P", [4, 8])
+def test_dist_live_refinement_solve(P):
+    """Data-dependent refinement (nitref = 3, force_itref = false: the norms and the predicate live
+    on the device) inside a distributed cpminres, at rank counts where a rank of cvxqp1_m's split
+    may own no rows (its solver vectors are then empty: round 5 found such a rank passing null
+    vectors to the accumulating backward sweep).  Every rank returns the same answer and the
+    solve tracks the oracle within the sensitivity band."""
+    import cpkrylov_amd as cpk
+    name, method, extra = "cvxqp1_m", "minres", {"nitref": 3, "force_itref": False}
+    Pd = F.load(name)
+    opts = dict(F.EXPROG_OPTS, **extra)
+
+    def work(ctx, r):
+        x, stats, flag = cpk.reg_cpkrylov(cpk.cpminres, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts, ctx=ctx)
+        M = stats["M"]
+        perm = M.export_factors()[2] if r == 0 else None
+        return x, {k: v for k, v in stats.items() if k != "M"}, flag, perm, len(M.local_dofs()[0])
+
+    res = _run_ranks(P, work)
+    x, stats, flag, perm, _ = res[0]
+    sizes = [s for *_, s in res]
+    for xr, sr, fr, _, _ in res[1:]:
+        assert np.array_equal(xr, x) and sr["niters"] == stats["niters"] and fr == flag, sizes
+    xo, so = O.reg_cpkrylov(method, Pd["rhs"], Pd["Q"], Pd["B"], Pd["C"], Pd["G"], opts, perm=perm)
+    assert stats["niters"] == so["niters"] and flag["solved"] == so["solved"], sizes
+    bd = band(name, method, extra, perm)
+    dev = np.max(np.abs(stats["residHistory"] - so["residHistory"])) / stats["residHistory"][0]
+    assert dev <= max(FLOOR, SAFETY * bd["residHistory"]), (dev, bd["residHistory"], sizes)
+    dx = np.linalg.norm(x - xo) / np.linalg.norm(xo)
+    assert dx <= max(FLOOR, SAFETY * bd["x"]), (dx, bd["x"], sizes)
+
+
 def test_dist_device_vectors_synthetic():
     """Device-resident local slices (the bench's path): shift + cpminres on 4 ranks agree with
     the 1-GPU solve of the same system."""
