@@ -187,6 +187,8 @@ struct DMat {
     DBuf<int32_t> send;         // local indices published to the other ranks
     DBuf<double> sbuf, rbuf;    // halo payload [kstride], allgathered halo [nranks * kstride]
     bool halo() const { return nloc >= 0; }
+    // ghost columns to read (a distributed matrix with a non-empty halo): the SpMV's HALO variant
+    bool ghosts() const { return halo() && kmax > 0; }
     size_t bytes() const { return ptr.bytes() + col.bytes() + val.bytes() + blk.bytes(); }
 };
 void make_dmat(const HCsr &a, DMat &d);
@@ -214,6 +216,10 @@ struct DFactor {
     int64_t N = 0, nnz = 0, nblk = 0, nlvl = 0;
     DBuf<uint32_t> fptr;  // forward rows of strict lower L, columns ascending
     DBuf<int32_t> fcol;
+    // the upper rounds' rows [urow0, N): leading outside-term count of each row's forward and
+    // backward entries, [2 (row - urow0) + bwd] (the kernels' fold_known; empty: fold_prefix)
+    DBuf<int16_t> ufold;
+    int32_t urow0 = 0;
     DBuf<int16_t> fcol16;  // round 0 when every forward entry is local: column - block's first row (else empty)
     int64_t nnz16 = 0;     // forward entries stored in fcol16 (10 bytes each instead of 12)
     DBuf<double> fval;
@@ -256,7 +262,7 @@ struct DFactor {
     std::vector<char> round_fits;    // host: every block of round r fits (sweep_rows[1], sweep_cap[1])
     int sweep_rows[2] = {192, 1024}, sweep_cap[2] = {576, 4096}, sweep_threads[2] = {64, 512};  // round 0 / rest
     size_t bytes() const {
-        return fptr.bytes() + fcol.bytes() + fcol16.bytes() + fval.bytes() + bptr.bytes() + bcol.bytes() + bval.bytes() + D.bytes() +
+        return fptr.bytes() + fcol.bytes() + fcol16.bytes() + ufold.bytes() + fval.bytes() + bptr.bytes() + bcol.bytes() + bval.bytes() + D.bytes() +
                perm.bytes() + blk_lvl.bytes() + lvl_row.bytes() + meta.bytes();
     }
 };

@@ -243,6 +243,37 @@ void mark_dataflow(std::vector<int32_t> &meta, const std::vector<int64_t> &round
 static void build_chain(DFactor &d, const std::vector<int32_t> &meta, const std::vector<uint32_t> &fptr,
                         const std::vector<int32_t> &fcol, const std::vector<uint32_t> &bptr,
                         const std::vector<int32_t> &bcol);
+// the upper rounds' leading outside-term counts (DFactor::ufold, the kernels' fold_known): per
+// row and direction, the entries before the first one inside the row's block -- what
+// fold_prefix finds by testing each column.  Capped at INT16_MAX (a shorter fold is still exact:
+// the level loop takes the rest against the 1.0 slot).
+static void build_ufold(DFactor &d, const std::vector<int32_t> &meta, const std::vector<int64_t> &round_ptr,
+                        const std::vector<uint32_t> &fptr, const std::vector<int32_t> &fcol,
+                        const std::vector<uint32_t> &bptr, const std::vector<int32_t> &bcol) {
+    d.ufold.release();
+    d.urow0 = 0;
+    if (round_ptr.size() < 3) return;
+    const int64_t ub0 = round_ptr[1], ub1 = round_ptr.back();
+    int64_t lo = INT64_MAX, hi = 0;
+    for (int64_t b = ub0; b < ub1; b++) lo = std::min<int64_t>(lo, meta[(size_t)b * 8]), hi = std::max<int64_t>(hi, meta[(size_t)b * 8 + 1]);
+    if (lo >= hi) return;
+    std::vector<int16_t> uf((size_t)(2 * (hi - lo)), 0);
+    parallel_for(ub1 - ub0, [&](int64_t a, int64_t z) {
+        for (int64_t b = ub0 + a; b < ub0 + z; b++) {
+            const int32_t r0 = meta[(size_t)b * 8], r1 = meta[(size_t)b * 8 + 1];
+            for (int32_t i = r0; i < r1; i++)
+                for (int dir = 0; dir < 2; dir++) {
+                    const std::vector<uint32_t> &ptr = dir ? bptr : fptr;
+                    const std::vector<int32_t> &col = dir ? bcol : fcol;
+                    uint32_t e = ptr[i];
+                    while (e < ptr[i + 1] && !(col[e] >= r0 && col[e] < r1)) e++;
+                    uf[(size_t)(2 * (i - lo) + dir)] = (int16_t)std::min<uint32_t>(e - ptr[i], INT16_MAX);
+                }
+        }
+    }, 64);
+    d.urow0 = (int32_t)lo;
+    d.ufold.upload(uf);
+}
 constexpr int64_t kInsertionSortMax = 32;  // rows up to this long sort by insertion (keys are distinct)
 void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vector<int64_t> *key,
                   const std::vector<std::vector<BwdExtra>> *extra, std::vector<int32_t> *fsrc,
@@ -404,6 +435,7 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
         m[4] = (int32_t)fptr[r0], m[5] = (int32_t)fptr[r1], m[6] = (int32_t)bptr[r0], m[7] = (int32_t)bptr[r1];
     }
     mark_dataflow(meta, s.round_ptr, fptr, fcol, bptr, bcol, d.dataflow);
+    build_ufold(d, meta, s.round_ptr, fptr, fcol, bptr, bcol);
     d.meta.upload(meta);
     d.hmeta = meta;
     clk.lap("layout: uploads, block records, level-loop choice");
@@ -531,8 +563,8 @@ static inline int grid_of(const DMat &A) { return (int)A.nblk; }
 
 template <class Epi>
 static void spmv_launch(Ctx &c, const DMat &A, const double *x, int64_t col_min, const Epi &e) {
-    const unsigned grid = A.halo() ? spmv_grid<Epi, true>(A.nblk) : spmv_grid<Epi, false>(A.nblk);
-    if (A.halo())
+    const unsigned grid = A.ghosts() ? spmv_grid<Epi, true>(A.nblk) : spmv_grid<Epi, false>(A.nblk);
+    if (A.ghosts())
         hipLaunchKernelGGL((spmv_stream<Epi, true>), dim3(grid), dim3(kBlock), 0, c.stream, A.ptr.p, A.col.p,
                            A.val.p, A.blk.p, A.nblk, x, col_min, e, (const double *)A.rbuf.p, A.nloc);
     else
@@ -1311,6 +1343,39 @@ __device__ __forceinline__ void fold_prefix(SweepLds &S, int nr, int tid = -1, i
     __syncthreads();
 }
 
+// fold_prefix with the prefix lengths known (UFold, counted at layout): ps[k] is set by the
+// staging, so the fold is a plain run of subtractions of staged products -- 16 per pass, loads
+// first -- with no per-term column test.  fold_prefix spends ~12 instructions per term on the
+// test and its select chain (~140 cycles per term on the ±64 window's separator rows of ~190
+// leading outside terms, r05 stamps); here a term is a load and a subtraction.  Same terms, same
+// order: bit-identical.
+template <int TPB>
+__device__ __forceinline__ void fold_known(SweepLds &S, int nr, int tid) {
+    constexpr int K = 16;
+    for (int i = tid; i < nr; i += TPB) {
+        int e = S.p[i];
+        const int e1 = S.ps[i];
+        double acc = S.w[i];
+        for (; e + K <= e1; e += K) {
+            double v[K];
+#pragma unroll
+            for (int j = 0; j < K; j++) v[j] = S.v[e + j];
+#pragma unroll
+            for (int j = 0; j < K; j++) acc -= v[j];
+        }
+        for (; e < e1; e++) acc -= S.v[e];
+        S.w[i] = acc;
+    }
+    __syncthreads();
+}
+
+// leading outside-term counts of the upper rounds' rows (DFactor::ufold): [2 (row - row0) + bwd]
+struct UFold {
+    const int16_t *p = nullptr;
+    int32_t row0 = 0;
+};
+static inline UFold ufold_of(const DFactor &F) { return UFold{F.ufold.n ? F.ufold.p : nullptr, F.urow0}; }
+
 // The level phase, out of LDS.  Per level every thread takes whole rows and consumes a row's
 // entries four at a time without branches: the (col, val) arrays are padded by four entries,
 // absent terms subtract +0.0 (which leaves every bit of the accumulator unchanged) and the
@@ -1791,12 +1856,19 @@ __device__ __forceinline__ void wst(double *p, double v) {
     if constexpr (SC) st_agent(p, v);
     else *p = v;
 }
-template <int TPB, int RPU, int EPU, bool BWD, bool ADD, bool SC = false>
+// wait (the chain kernel): called by every thread between the block's static loads (row pointers,
+// entries, perm, D, level bounds, the forward input) and its loads of w -- a chained task issues
+// the former before it polls its producers' flags, so their HBM round trip overlaps the wait
+struct NoWait {
+    __device__ void operator()() const {}
+};
+template <int TPB, int RPU, int EPU, bool BWD, bool ADD, bool SC = false, class Wait = NoWait>
 __device__ __forceinline__ void upper_block(
     char *smem, const BlkMeta m, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
-    double *w, double *out, int sched_in, double *ys, double *xs, const PackArgs &pk, int64_t b) {
+    double *w, double *out, int sched_in, double *ys, double *xs, const PackArgs &pk, const UFold &uf, int64_t b,
+    const Wait &wait = Wait{}) {
     constexpr int R = RPU * TPB, CAP = EPU * TPB;
 #ifdef CPK_PIPE_STAMPS
     uint64_t tp = (uint64_t)clock64();
@@ -1809,7 +1881,7 @@ __device__ __forceinline__ void upper_block(
     const int tid = threadIdx.x;
     SweepLds S(smem, R, CAP);
     uint32_t q[RPU];
-    int32_t sp[RPU];
+    int32_t sp[RPU], fo[RPU];
     double a[RPU], d[RPU];
     int32_t c[EPU];
     double v[EPU], g[EPU];
@@ -1817,7 +1889,8 @@ __device__ __forceinline__ void upper_block(
     for (int j = 0; j < RPU; j++) {
         const int i = tid + j * TPB, rr = r0 + (i < nr ? i : nr - 1);
         q[j] = ptr[rr], sp[j] = (BWD ? out != nullptr : !sched_in) ? perm[rr] : rr;
-        if (BWD) a[j] = wld<SC>(w + rr), d[j] = D[rr];
+        fo[j] = uf.p ? uf.p[2 * (rr - uf.row0) + (BWD ? 1 : 0)] : 0;
+        if (BWD) d[j] = D[rr];
     }
 #pragma unroll
     for (int u = 0; u < EPU; u++) {
@@ -1830,6 +1903,11 @@ __device__ __forceinline__ void upper_block(
     for (int j = 0; j < RPU; j++) {
         if (!BWD) a[j] = xin[sp[j]];
     }
+    wait();
+#pragma unroll
+    for (int j = 0; j < RPU; j++) {
+        if (BWD) a[j] = wld<SC>(w + r0 + (tid + j * TPB < nr ? tid + j * TPB : nr - 1));
+    }
 #pragma unroll
     for (int u = 0; u < EPU; u++) g[u] = wld<SC>(w + ((c[u] >= r0 && c[u] < r1) ? r0 : c[u]));
 #pragma unroll
@@ -1837,6 +1915,7 @@ __device__ __forceinline__ void upper_block(
         const int i = tid + j * TPB;
         if (i < nr) {
             S.p[i] = (int16_t)(q[j] - e0);
+            if (uf.p) S.ps[i] = (int16_t)(q[j] - e0 + fo[j]);
             S.w[i] = BWD ? a[j] / d[j] : ((sp[j] >= neg_from) ? -a[j] : a[j]);
             if (!BWD && xs) xs[r0 + i] = S.w[i];
         }
@@ -1854,7 +1933,8 @@ __device__ __forceinline__ void upper_block(
     }
     __syncthreads();
     CPK_UP_STAMP(0);
-    fold_prefix<TPB, 1>(S, nr, -1, R);
+    if (uf.p) fold_known<TPB>(S, nr, tid);
+    else fold_prefix<TPB, 1>(S, nr, -1, R);
     CPK_UP_STAMP(1);
     // levels on one wave: a level holds a few rows, and without a workgroup barrier per level
     // (a single wave's LDS accesses complete in program order) the chain is LDS latency only;
@@ -1896,11 +1976,12 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
     int64_t blk0, const BlkMeta *__restrict__ meta, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
-    double *w, double *out, const int *run, const int *active, int sched_in, double *ys, double *xs, PackArgs pk) {
+    double *w, double *out, const int *run, const int *active, int sched_in, double *ys, double *xs, PackArgs pk,
+    UFold uf) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
     upper_block<TPB, RPU, EPU, BWD, ADD>(smem, meta[blk0 + blockIdx.x], lvl_row, ptr, col, val, D, perm, xin, neg_from,
-                                         w, out, sched_in, ys, xs, pk, blk0 + blockIdx.x);
+                                         w, out, sched_in, ys, xs, pk, uf, blk0 + blockIdx.x);
 }
 
 // The last round's forward and backward sweeps in one launch (single GPU).  The sweeps meet at
@@ -1911,20 +1992,20 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
 // forward fold and levels, divides by D in LDS and runs the backward levels -- the operations of
 // sptrsv_upper_kernel forward, its write-back and w / D, and sptrsv_upper_kernel backward, in
 // that order: bit-identical, one launch and one staging round trip fewer per solve.
-template <int TPB, int RPU, int EPU, bool ADD, bool SC = false>
+template <int TPB, int RPU, int EPU, bool ADD, bool SC = false, class Wait = NoWait>
 __device__ __forceinline__ void last_block(
     char *smem, const BlkMeta m, const int32_t *__restrict__ lvl_row,
     const uint32_t *__restrict__ fptr, const int32_t *__restrict__ fcol, const double *__restrict__ fval,
     const uint32_t *__restrict__ bptr, const int32_t *__restrict__ bcol, const double *__restrict__ bval,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
-    int sched_in, double *xs, double *w, double *out, double *ys) {
+    int sched_in, double *xs, double *w, double *out, double *ys, const UFold &uf, const Wait &wait = Wait{}) {
     constexpr int R = RPU * TPB, CAP = EPU * TPB;
     const int r0 = m.r0, r1 = m.r1, nr = r1 - r0, nl = (m.l1 & kMetaL1Mask) - m.l0;
     const int nef = m.fe1 - m.fe0, neb = m.be1 - m.be0;
     const int tid = threadIdx.x;
     SweepLds S(smem, R, CAP);
     uint32_t qf[RPU], qb[RPU];
-    int32_t sp[RPU], dp[RPU];
+    int32_t sp[RPU], dp[RPU], fof[RPU], fob[RPU];
     double a[RPU], d[RPU];
     int32_t cf[EPU], cb[EPU];
     double vf[EPU], vb[EPU], g[EPU];
@@ -1932,19 +2013,28 @@ __device__ __forceinline__ void last_block(
     for (int j = 0; j < RPU; j++) {
         const int i = tid + j * TPB, rr = r0 + (i < nr ? i : nr - 1);
         qf[j] = fptr[rr], qb[j] = bptr[rr], d[j] = D[rr];
+        fof[j] = uf.p ? uf.p[2 * (rr - uf.row0)] : 0, fob[j] = uf.p ? uf.p[2 * (rr - uf.row0) + 1] : 0;
         sp[j] = sched_in ? rr : perm[rr];
         dp[j] = out ? perm[rr] : rr;
     }
 #pragma unroll
     for (int u = 0; u < EPU; u++) {
         const int e = tid + u * TPB;
-        const uint32_t ef = (uint32_t)m.fe0 + (uint32_t)(e < nef ? e : 0), eb = (uint32_t)m.be0 + (uint32_t)(e < neb ? e : 0);
+        const uint32_t ef = (uint32_t)m.fe0 + (uint32_t)(e < nef ? e : 0);
         cf[u] = __builtin_nontemporal_load(fcol + ef), vf[u] = __builtin_nontemporal_load(fval + ef);
-        cb[u] = __builtin_nontemporal_load(bcol + eb), vb[u] = __builtin_nontemporal_load(bval + eb);
     }
     for (int l = tid; l <= nl; l += TPB) S.lv[l] = (int16_t)(lvl_row[m.l0 + l] - r0);
 #pragma unroll
     for (int j = 0; j < RPU; j++) a[j] = xin[sp[j]];
+    wait();
+    // the backward entries after the wait (held across it, they spilled in the chain kernel);
+    // their round trip still overlaps the forward phase
+#pragma unroll
+    for (int u = 0; u < EPU; u++) {
+        const int e = tid + u * TPB;
+        const uint32_t eb = (uint32_t)m.be0 + (uint32_t)(e < neb ? e : 0);
+        cb[u] = __builtin_nontemporal_load(bcol + eb), vb[u] = __builtin_nontemporal_load(bval + eb);
+    }
 #pragma unroll
     for (int u = 0; u < EPU; u++) g[u] = wld<SC>(w + ((cf[u] >= r0 && cf[u] < r1) ? r0 : cf[u]));
     // ---- forward (sptrsv_upper_kernel<..., false, false>)
@@ -1953,6 +2043,7 @@ __device__ __forceinline__ void last_block(
         const int i = tid + j * TPB;
         if (i < nr) {
             S.p[i] = (int16_t)(qf[j] - (uint32_t)m.fe0);
+            if (uf.p) S.ps[i] = (int16_t)(qf[j] - (uint32_t)m.fe0 + fof[j]);
             S.w[i] = (sp[j] >= neg_from) ? -a[j] : a[j];
             if (xs) xs[r0 + i] = S.w[i];
         }
@@ -1969,7 +2060,8 @@ __device__ __forceinline__ void last_block(
         }
     }
     __syncthreads();
-    fold_prefix<TPB, 1>(S, nr, -1, R);
+    if (uf.p) fold_known<TPB>(S, nr, tid);
+    else fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
         if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd)) levels_dataflow<false, CPK_DF_CH(false), true, R / kWave>(S, nr, R, nef, tid);
         else if (CPK_UPPER_GROUP(false)) levels_grouped<CPK_UPPER_CH(false), false, true>(S, nl, false, tid);
@@ -1986,6 +2078,7 @@ __device__ __forceinline__ void last_block(
         if (i < nr) {
             S.w[i] = S.w[i] / d[j];
             S.p[i] = (int16_t)(qb[j] - (uint32_t)m.be0);
+            if (uf.p) S.ps[i] = (int16_t)(qb[j] - (uint32_t)m.be0 + fob[j]);
         }
     }
     if (tid == 0) S.p[nr] = (int16_t)neb;
@@ -2002,7 +2095,8 @@ __device__ __forceinline__ void last_block(
         }
     }
     __syncthreads();
-    fold_prefix<TPB, 1>(S, nr, -1, R);
+    if (uf.p) fold_known<TPB>(S, nr, tid);
+    else fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
         if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfBwd)) levels_dataflow<true, CPK_DF_CH(true), true, R / kWave>(S, nr, R, neb, tid);
         else if (CPK_UPPER_GROUP(true)) levels_grouped<CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
@@ -2027,11 +2121,11 @@ __global__ __launch_bounds__(TPB) void sptrsv_last_kernel(
     const uint32_t *__restrict__ fptr, const int32_t *__restrict__ fcol, const double *__restrict__ fval,
     const uint32_t *__restrict__ bptr, const int32_t *__restrict__ bcol, const double *__restrict__ bval,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
-    int sched_in, double *xs, double *w, double *out, const int *run, const int *active, double *ys) {
+    int sched_in, double *xs, double *w, double *out, const int *run, const int *active, double *ys, UFold uf) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
     last_block<TPB, RPU, EPU, ADD>(smem, meta[blk0 + blockIdx.x], lvl_row, fptr, fcol, fval, bptr, bcol, bval, D, perm,
-                                   xin, neg_from, sched_in, xs, w, out, ys);
+                                   xin, neg_from, sched_in, xs, w, out, ys, uf);
 }
 
 // the last round fused (fwd + bwd) when it is an upper round whose blocks fit sptrsv_last_kernel
@@ -2059,11 +2153,11 @@ static void launch_last(Ctx &c, const DFactor &F, const FwdIn &in, double *w, do
     if (add)
         hipLaunchKernelGGL((sptrsv_last_kernel<TPB, RPU, EPU, true>), dim3((unsigned)nb), dim3(TPB), lds, c.stream, b0,
                            meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p,
-                           in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys);
+                           in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, ufold_of(F));
     else
         hipLaunchKernelGGL((sptrsv_last_kernel<TPB, RPU, EPU, false>), dim3((unsigned)nb), dim3(TPB), lds, c.stream, b0,
                            meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p,
-                           in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys);
+                           in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, ufold_of(F));
     CPK_HIP(hipGetLastError());
 }
 
@@ -2106,7 +2200,8 @@ __global__ __launch_bounds__(TPB) void sptrsv_chain_kernel(
     const uint32_t *__restrict__ fptr, const int32_t *__restrict__ fcol, const double *__restrict__ fval,
     const uint32_t *__restrict__ bptr, const int32_t *__restrict__ bcol, const double *__restrict__ bval,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
-    int sched_in, double *xs, double *w, double *out, const int *run, const int *active, double *ys, PackArgs pk) {
+    int sched_in, double *xs, double *w, double *out, const int *run, const int *active, double *ys, PackArgs pk,
+    UFold uf) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ uint32_t s_epoch;
     if (skip(run, active)) return;
@@ -2114,33 +2209,39 @@ __global__ __launch_bounds__(TPB) void sptrsv_chain_kernel(
     if (threadIdx.x == 0) s_epoch = ld_agent32(ch.ctrl);
     __syncthreads();
     const uint32_t want = s_epoch + 1;
-    const int d1 = ch.dptr[t + 1];
-    for (int k = ch.dptr[t] + (int)threadIdx.x; k < d1; k += TPB) {
-        const uint32_t *f = ch.flag + ch.didx[k];
-        uint32_t spins = 0;
-        while (ld_agent32(f) != want) {
-            if (ld_agent32(ch.ctrl + 2) != 0) break;  // a wait timed out somewhere: give up
-            if (++spins > kChainSpinCap) {
-                st_agent32(ch.ctrl + 2, 1);
-                break;
-            }
-            // back off: a few quick polls, then ~1000 cycles apart (poll traffic stays low)
-            if (spins < 16) __builtin_amdgcn_s_sleep(2);
-            else __builtin_amdgcn_s_sleep(16);
-        }
-    }
-    __syncthreads();
     const int32_t task = ch.task[t];
     const int kind = task >> 28, b = task & ((1 << 28) - 1);
+    // the producers' flags, polled between the block's static loads and its loads of w
+    const int k0 = ch.dptr[t], k1 = ch.dptr[t + 1];
+    const int32_t *didx = ch.didx;
+    const uint32_t *flag = ch.flag;
+    uint32_t *err = ch.ctrl + 2;
+    auto wait = [k0, k1, didx, flag, err, want]() {
+        for (int k = k0 + (int)threadIdx.x; k < k1; k += TPB) {
+            const uint32_t *f = flag + didx[k];
+            uint32_t spins = 0;
+            while (ld_agent32(f) != want) {
+                if (ld_agent32(err) != 0) break;  // a wait timed out somewhere: give up
+                if (++spins > kChainSpinCap) {
+                    st_agent32(err, 1);
+                    break;
+                }
+                // back off: a few quick polls, then ~1000 cycles apart (poll traffic stays low)
+                if (spins < 16) __builtin_amdgcn_s_sleep(2);
+                else __builtin_amdgcn_s_sleep(16);
+            }
+        }
+        __syncthreads();
+    };
     if (kind == 0)
         upper_block<TPB, RPU, EPU, false, false, true>(smem, meta[b], lvl_row, fptr, fcol, fval, D, perm, xin, neg_from, w,
-                                                       nullptr, sched_in, nullptr, xs, pk, b);
+                                                       nullptr, sched_in, nullptr, xs, pk, uf, b, wait);
     else if (kind == 1)
         last_block<TPB, RPU, EPU, ADD, true>(smem, meta[b], lvl_row, fptr, fcol, fval, bptr, bcol, bval, D, perm, xin,
-                                             neg_from, sched_in, xs, w, out, ys);
+                                             neg_from, sched_in, xs, w, out, ys, uf, wait);
     else
         upper_block<TPB, RPU, EPU, true, ADD, true>(smem, meta[b], lvl_row, bptr, bcol, bval, D, perm, nullptr, 0, w, out,
-                                                    0, ys, nullptr, pk, b);
+                                                    0, ys, nullptr, pk, uf, b, wait);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w stores done
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2268,11 +2369,11 @@ static void launch_chain_t(Ctx &c, const DFactor &F, int kind, const FwdIn &in, 
     if (add)
         hipLaunchKernelGGL((sptrsv_chain_kernel<TPB, RPU, EPU, true>), dim3((unsigned)h.ntask), dim3(TPB), lds, c.stream,
                            ch, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, pk);
+                           F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, pk, ufold_of(F));
     else
         hipLaunchKernelGGL((sptrsv_chain_kernel<TPB, RPU, EPU, false>), dim3((unsigned)h.ntask), dim3(TPB), lds,
                            c.stream, ch, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p,
-                           F.D.p, F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, pk);
+                           F.D.p, F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, pk, ufold_of(F));
     CPK_HIP(hipGetLastError());
 }
 static void launch_chain(Ctx &c, const DFactor &F, int kind, const FwdIn &in, double *w, double *out, bool add,
@@ -2315,15 +2416,15 @@ static bool upper_round_t(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool ad
     if (!bwd)
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, false, false>), dim3((unsigned)nb), dim3(TPB), lds,
                            c.stream, b0, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active, sched_in, ys, xs, pk);
+                           neg_from, w, out, run, active, sched_in, ys, xs, pk, ufold_of(F));
     else if (add)
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, true>), dim3((unsigned)nb), dim3(TPB), lds,
                            c.stream, b0, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active, sched_in, ys, xs, pk);
+                           neg_from, w, out, run, active, sched_in, ys, xs, pk, ufold_of(F));
     else
         hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, false>), dim3((unsigned)nb), dim3(TPB), lds,
                            c.stream, b0, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active, sched_in, ys, xs, pk);
+                           neg_from, w, out, run, active, sched_in, ys, xs, pk, ufold_of(F));
     return true;
 }
 

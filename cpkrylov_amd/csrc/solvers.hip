@@ -239,8 +239,8 @@ template <class P, class A>
 void launch_krylov_spmv_as(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n, const P &pol) {
     using E = EpiKrylov<P, A>;
     E e{st, nullptr, y, n, red_buf(c), pol};
-    const unsigned grid = AC.halo() ? spmv_grid<E, true>(AC.nblk) : spmv_grid<E, false>(AC.nblk);
-    if (AC.halo())
+    const unsigned grid = AC.ghosts() ? spmv_grid<E, true>(AC.nblk) : spmv_grid<E, false>(AC.nblk);
+    if (AC.ghosts())
         hipLaunchKernelGGL((spmv_stream<E, true>), dim3(grid), dim3(kBlock), 0, c.stream, AC.ptr.p, AC.col.p, AC.val.p,
                            AC.blk.p, AC.nblk, (const double *)nullptr, (int64_t)0, e, (const double *)AC.rbuf.p,
                            AC.nloc);

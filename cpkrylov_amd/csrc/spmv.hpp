@@ -30,6 +30,19 @@ __device__ __forceinline__ double gathered(const Epi &e, double v) {
     return v;
 }
 
+// x[c], or for a ghost column (c >= nloc) the allgathered halo value xg[c - nloc]: ONE load from
+// a selected base (two predicated loads per entry made the distributed SpMV 23 % slower than the
+// single-GPU one at P = 1, r05); local values through the epilogue's transform, halo values as
+// they arrived (already transformed by their owner)
+template <bool HALO, class Epi>
+__device__ __forceinline__ double halo_gather(const Epi &epi, const double *x, const double *xg, int64_t nloc,
+                                              int32_t c) {
+    if constexpr (!HALO) return gathered(epi, x[c]);
+    const bool loc = c < nloc;
+    const double v = (loc ? x : xg - nloc)[c];
+    return loc ? gathered(epi, v) : v;
+}
+
 // Epi::kWaves where the epilogue sets one (EpiKrylov's normalise-on-read needs more registers)
 template <class E, class = void>
 struct SpmvWaves : std::integral_constant<int, CPK_SPMV_WAVES> {};
@@ -75,7 +88,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SpmvWave
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
             const int32_t c = cc[j];
-            xv[j] = (!HALO || c < nloc) ? gathered(epi, x[c]) : xg[c - nloc];
+            xv[j] = halo_gather<HALO>(epi, x, xg, nloc, c);
         }
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
@@ -99,7 +112,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SpmvWave
             const uint32_t c1 = min(e1, c0 + (uint32_t)kSpmvCap);
             for (uint32_t e = c0 + tid; e < c1; e += kBlock) {
                 const int32_t c = col[e];
-                const double xv = (!HALO || c < nloc) ? gathered(epi, x[c]) : xg[c - nloc];
+                const double xv = halo_gather<HALO>(epi, x, xg, nloc, c);
                 prod[e - c0] = (c >= col_min) ? val[e] * xv : 0.0;
             }
             __syncthreads();

@@ -17,7 +17,7 @@ from cpkrylov_amd import _lib  # noqa: E402
 from cpkrylov_amd.synthetic import saddle_system  # noqa: E402
 
 KMAX = 1 << 20  # kBlkCycMax (kernels.hip)
-S = saddle_system(int(os.environ.get("N", "10000000")))
+S = saddle_system(int(os.environ.get("N", "10000000")), window=int(os.environ.get("W", "4")))
 H = cpk.analyze(S["G"], S["B"], -S["C"])
 rp, bl, lr, order, L = H["round_ptr"], H["blk_lvl"], H["lvl_row"], H["order"], H["L"]
 fcnt = np.diff(L.tocsr().indptr)[order]
@@ -25,7 +25,7 @@ bcnt = np.diff(L.indptr)[order]
 cum = lambda c: np.concatenate([[0], np.cumsum(c)])  # noqa: E731
 cf, cb = cum(fcnt), cum(bcnt)
 
-ctx = cpk.Context(device=0)
+ctx = cpk.Context(device=0, options={"no_chain": 1})  # one launch per round: stamps per round
 M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
 M.nitref, M.force_itref = 1, True
 z = np.random.default_rng(1).standard_normal(M.n)
