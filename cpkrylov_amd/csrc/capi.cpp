@@ -616,6 +616,15 @@ int cpk_debug_blk_cycles(uint64_t *out, int64_t n, int64_t *copied) {
     API_END
 }
 
+int cpk_debug_block_model(cpk_pc M, int64_t *out, int64_t n, int64_t *copied) {
+    API_BEGIN
+    need(M && copied, "NULL argument");
+    const std::vector<int64_t> &h = M->p->dF.hmodel;
+    *copied = std::min<int64_t>(n, (int64_t)h.size());
+    if (out && *copied) std::memcpy(out, h.data(), (size_t)*copied * sizeof(int64_t));
+    API_END
+}
+
 int cpk_pc_sep_info(cpk_pc M, int64_t *info) {
     API_BEGIN
     need(M && info, "NULL argument");

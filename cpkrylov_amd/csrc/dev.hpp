@@ -107,6 +107,8 @@ struct EngineOpts {
     bool no_col16 = false;        // no_col16:           round-0 forward columns as int32
     bool no_dataflow = false;     // no_dataflow:        upper rounds always on the level loop
     bool all_dataflow = false;    // all_dataflow:       upper rounds always on the dataflow loop (tests)
+    bool no_colsweep = false;     // no_colsweep:        upper rounds never on the column sweep
+    bool all_colsweep = false;    // all_colsweep:       upper blocks of <= 256 rows always on the column sweep (tests)
     bool no_sched_resid = false;  // no_sched_resid:     refinement residual in original order
     bool no_fused_resid = false;  // no_fused_resid:     refinement residual as its own SpMV
     int r0_xcd_chunk = 16;        // r0_xcd_chunk:       K > 0: runs of K consecutive round-0 blocks share an XCD
@@ -219,6 +221,7 @@ struct DFactor {
     // the upper rounds' rows [urow0, N): leading outside-term count of each row's forward and
     // backward entries, [2 (row - urow0) + bwd] (the kernels' fold_known; empty: fold_prefix)
     DBuf<int16_t> ufold;
+    DBuf<int16_t> ustep;  // the row's step in its block's column sweep, same layout
     int32_t urow0 = 0;
     DBuf<int16_t> fcol16;  // round 0 when every forward entry is local: column - block's first row (else empty)
     int64_t nnz16 = 0;     // forward entries stored in fcol16 (10 bytes each instead of 12)
@@ -235,6 +238,7 @@ struct DFactor {
     bool no_upper = false;  // upper rounds through the generic kernels (set before make_dfactor)
     bool no_col16 = false;  // no int16 round-0 forward columns (set before make_dfactor)
     int dataflow = 0;       // upper-round level loops: 0 the host model per block, 1 never, 2 always
+    int colsweep = 0;       // the column sweep (levels_colsweep): 0 the host model per block, 1 never, 2 always
     // engine options of the preconditioner's context when it was built (launch-time paths)
     bool no_fused_resid = false;
     bool fuse_last = false;  // single GPU, no entries outside the factor: the last round fwd + bwd in one launch
@@ -244,6 +248,7 @@ struct DFactor {
     // sweep launched with wdead (launch_sptrsv_bwd): the byte models drop them
     int64_t bwd_dead_w_rows() const { return pipelined && round0_rows > 0 ? round0_rows : 0; }
     std::vector<int32_t> hmeta;  // host copy of meta
+    std::vector<int64_t> hmodel; // the upper blocks' loop-cost model (mark_dataflow; diagnostic)
     // round-0 blocks assigned to the persistent launch's workgroups by modelled cost (plan_round0),
     // per kernel variant v (0 forward, 1 forward with the fused refinement residual, 2 backward):
     // workgroup g runs the BlkMeta records ameta[v][aptr[v][g] .. aptr[v][g + 1]); agrid[v] = the
@@ -262,7 +267,7 @@ struct DFactor {
     std::vector<char> round_fits;    // host: every block of round r fits (sweep_rows[1], sweep_cap[1])
     int sweep_rows[2] = {192, 1024}, sweep_cap[2] = {576, 4096}, sweep_threads[2] = {64, 512};  // round 0 / rest
     size_t bytes() const {
-        return fptr.bytes() + fcol.bytes() + fcol16.bytes() + ufold.bytes() + fval.bytes() + bptr.bytes() + bcol.bytes() + bval.bytes() + D.bytes() +
+        return fptr.bytes() + fcol.bytes() + fcol16.bytes() + ufold.bytes() + ustep.bytes() + fval.bytes() + bptr.bytes() + bcol.bytes() + bval.bytes() + D.bytes() +
                perm.bytes() + blk_lvl.bytes() + lvl_row.bytes() + meta.bytes();
     }
 };
@@ -464,7 +469,9 @@ constexpr int64_t kSepPiggy = 2;  // spare payload slots per rank in the separat
 // there with the next vector's halo (solvers.hip, cpminres)
 // block record flags (DFactor::meta, the l1 field): the dataflow level loop per direction for
 // an upper-round block (mark_dataflow, kernels.hip); every reader of l1 masks them off
-constexpr int32_t kMetaDfFwd = 1 << 30, kMetaDfBwd = 1 << 29, kMetaL1Mask = (1 << 29) - 1;
+constexpr int kBlockModelW = 8;  // fields per (upper block, direction) of DFactor::hmodel
+constexpr int32_t kMetaDfFwd = 1 << 30, kMetaDfBwd = 1 << 29, kMetaCsFwd = 1 << 28, kMetaCsBwd = 1 << 27,
+                  kMetaL1Mask = (1 << 27) - 1;
 constexpr int64_t kKrylovSpare = 2;
 struct DSep {
     int64_t nT = 0, kt = 0, nlev = 0, nsend = 0, ntdof = 0;

@@ -117,6 +117,16 @@ void make_dmat(const HCsr &a, DMat &d) {
 // branch-free ready prefix and 4 / 2 terms (profiles/r04_dataflow_alpha_ab_v11.txt: S10 +0.4 %,
 // P = 8 rank -1.2 %, the +-64 window 324 -> 357 it/s)
 constexpr double kDataflowTripCost = 1.0;
+// the column sweep (levels_colsweep): blocks of at most 256 rows (4 per lane).  The choice
+// against the other loops is made in cycles, fitted on the stamps build over every upper block of
+// the +-64 window and S10 with the column sweep forced on and off (tools/upper_cycles.py BLOCKS=,
+// profiles/r05_colsweep_calibration.txt): a step costs ~430 / 520 / 610 cycles at 1 / 2 / 3 rows
+// per lane, an outside term behind an in-block one ~40-70 more; a level-loop trip ~300 cycles, a
+// dataflow trip ~220
+constexpr int kColsweepMaxRows = 4 * 64;
+constexpr double kColsweepStepCycles[4] = {430.0, 520.0, 610.0, 700.0};
+constexpr double kColsweepOutCycles = 50.0;
+constexpr double kLevelTripCycles = 300.0, kDataflowTripCycles = 220.0;
 #ifndef CPK_UPPER_DATAFLOW
 #define CPK_UPPER_DATAFLOW 1
 #endif
@@ -188,12 +198,67 @@ int64_t dataflow_trips(const std::vector<std::vector<int>> &terms, bool bwd, int
 }
 }  // namespace
 
+// the upper rounds' row data for the block kernels (DFactor::ufold, [2 (row - urow0) + bwd]):
+//   fold: the leading outside-term count of each row and direction, the entries before the first
+//     one inside the row's block -- what fold_prefix finds by testing each column (fold_known).
+//     Capped at INT16_MAX (a shorter fold is still exact: the loops take the rest against the
+//     1.0 slot);
+//   step: the row's position in its block by ascending key (forward) / descending key (backward)
+//     -- the entry order of every row, so an order in which each row's terms are met in its own
+//     order (levels_colsweep).
+template <class Key>
+static std::vector<int16_t> build_ufold(DFactor &d, const std::vector<int32_t> &meta, const std::vector<int64_t> &round_ptr,
+                        const std::vector<uint32_t> &fptr, const std::vector<int32_t> &fcol,
+                        const std::vector<uint32_t> &bptr, const std::vector<int32_t> &bcol, const Key &key) {
+    d.ufold.release();
+    d.ustep.release();
+    d.urow0 = 0;
+    if (round_ptr.size() < 3) return {};
+    const int64_t ub0 = round_ptr[1], ub1 = round_ptr.back();
+    int64_t lo = INT64_MAX, hi = 0;
+    for (int64_t b = ub0; b < ub1; b++) lo = std::min<int64_t>(lo, meta[(size_t)b * 8]), hi = std::max<int64_t>(hi, meta[(size_t)b * 8 + 1]);
+    if (lo >= hi) return {};
+    std::vector<int16_t> uf((size_t)(2 * (hi - lo)), 0), us((size_t)(2 * (hi - lo)), 0);
+    parallel_for(ub1 - ub0, [&](int64_t a, int64_t z) {
+        std::vector<std::pair<int64_t, int32_t>> order;
+        for (int64_t b = ub0 + a; b < ub0 + z; b++) {
+            const int32_t r0 = meta[(size_t)b * 8], r1 = meta[(size_t)b * 8 + 1];
+            for (int32_t i = r0; i < r1; i++)
+                for (int dir = 0; dir < 2; dir++) {
+                    const std::vector<uint32_t> &ptr = dir ? bptr : fptr;
+                    const std::vector<int32_t> &col = dir ? bcol : fcol;
+                    uint32_t e = ptr[i];
+                    while (e < ptr[i + 1] && !(col[e] >= r0 && col[e] < r1)) e++;
+                    uf[(size_t)(2 * (i - lo) + dir)] = (int16_t)std::min<uint32_t>(e - ptr[i], INT16_MAX);
+                }
+            if (r1 - r0 > INT16_MAX) continue;
+            order.clear();
+            for (int32_t i = r0; i < r1; i++) order.push_back({key(i), i});
+            std::sort(order.begin(), order.end());
+            const int32_t nr = r1 - r0;
+            for (int32_t t = 0; t < nr; t++) {
+                const int32_t i = order[(size_t)t].second;
+                us[(size_t)(2 * (i - lo))] = (int16_t)t, us[(size_t)(2 * (i - lo) + 1)] = (int16_t)(nr - 1 - t);
+            }
+        }
+    }, 64);
+    d.urow0 = (int32_t)lo;
+    d.ufold.upload(uf);
+    d.ustep.upload(us);
+    return us;
+}
 void mark_dataflow(std::vector<int32_t> &meta, const std::vector<int64_t> &round_ptr, const std::vector<uint32_t> &fptr,
                    const std::vector<int32_t> &fcol, const std::vector<uint32_t> &bptr, const std::vector<int32_t> &bcol,
-                   int mode) {
-    if (!CPK_UPPER_DATAFLOW || round_ptr.size() < 3 || mode == 1) return;
+                   int mode, int cs_mode, const std::vector<int16_t> &ustep, int64_t urow0,
+                   std::vector<int64_t> *model) {
+    if (model) model->clear();
+    if (round_ptr.size() < 3) return;
     const int64_t b0 = round_ptr[1], b1 = round_ptr.back();  // the upper rounds
+    // per block and direction: nr, level trips, dataflow trips, outside terms behind in-block
+    // ones, column sweep valid, flags chosen (cpk_debug_block_model: the loops' cost model)
+    if (model) model->assign((size_t)(b1 - b0) * 2 * kBlockModelW, -1);
     const double alpha = kDataflowTripCost;
+    const bool df_on = CPK_UPPER_DATAFLOW && mode != 1;
     parallel_for(b1 - b0, [&](int64_t lo, int64_t hi) {
         std::vector<int32_t> lb;
         std::vector<int> nterm;
@@ -233,8 +298,42 @@ void mark_dataflow(std::vector<int32_t> &meta, const std::vector<int64_t> &round
                     for (int k = 0; k < nr; k++) byl[pos[lev[k]]++] = nterm[k];
                 }
                 const int64_t lt = level_trips(lb, byl, dir ? CPK_UPPER_CH_BWD : CPK_UPPER_CH_FWD);
-                const int64_t dt = dataflow_trips(terms, dir == 1, CPK_DF_CH(dir == 1), (int64_t)(4 * lt) + 8);
-                if (mode == 2 || alpha * (double)dt < (double)lt) m[3] |= dir ? kMetaDfBwd : kMetaDfFwd;
+                const int64_t dt = df_on ? dataflow_trips(terms, dir == 1, CPK_DF_CH(dir == 1), (int64_t)(4 * lt) + 8)
+                                         : INT64_MAX;
+                const bool df = df_on && (mode == 2 || alpha * (double)dt < (double)lt);
+                // the column sweep (levels_colsweep): one step per row, its cost per step growing
+                // with the rows each lane holds; outside terms behind in-block ones add a pass each
+                // valid only if every row meets its in-block terms at increasing steps, all before
+                // its own (the steps follow the entries' key order; checked, not assumed)
+                bool cs = false, cs_valid = cs_mode != 1 && nr <= kColsweepMaxRows && !ustep.empty();
+                auto step = [&](int k) { return (int)ustep[(size_t)(2 * (r0 + k - urow0) + dir)]; };
+                for (int k = 0; k < nr && cs_valid; k++) {
+                    int prev = -1;
+                    for (int c : terms[k])
+                        if (c >= 0) {
+                            cs_valid = cs_valid && step(c) > prev && step(c) < step(k);
+                            prev = step(c);
+                        }
+                }
+                if (cs_valid) {
+                    int64_t outs = 0;
+                    for (int k = 0; k < nr; k++)
+                        for (int c : terms[k]) outs += c < 0;
+                    const int rpl = (nr + kWave - 1) / kWave;
+                    const double ct = (double)nr * kColsweepStepCycles[std::min(rpl, 4) - 1] + kColsweepOutCycles * (double)outs;
+                    const double base = df ? kDataflowTripCycles * (double)dt : kLevelTripCycles * (double)lt;
+                    cs = cs_mode == 2 || ct < base;
+                }
+                if (cs) m[3] |= dir ? kMetaCsBwd : kMetaCsFwd;
+                else if (df) m[3] |= dir ? kMetaDfBwd : kMetaDfFwd;
+                if (model) {
+                    int64_t *o = &(*model)[(size_t)(((b - b0) * 2 + dir) * kBlockModelW)];
+                    int64_t outs = 0;
+                    for (int k = 0; k < nr; k++)
+                        for (int c : terms[k]) outs += c < 0;
+                    o[0] = b, o[1] = dir, o[2] = nr, o[3] = lt, o[4] = df_on ? dt : -1, o[5] = outs, o[6] = cs_valid,
+                    o[7] = cs ? 2 : (df ? 1 : 0);
+                }
             }
         }
     }, 4);
@@ -243,37 +342,6 @@ void mark_dataflow(std::vector<int32_t> &meta, const std::vector<int64_t> &round
 static void build_chain(DFactor &d, const std::vector<int32_t> &meta, const std::vector<uint32_t> &fptr,
                         const std::vector<int32_t> &fcol, const std::vector<uint32_t> &bptr,
                         const std::vector<int32_t> &bcol);
-// the upper rounds' leading outside-term counts (DFactor::ufold, the kernels' fold_known): per
-// row and direction, the entries before the first one inside the row's block -- what
-// fold_prefix finds by testing each column.  Capped at INT16_MAX (a shorter fold is still exact:
-// the level loop takes the rest against the 1.0 slot).
-static void build_ufold(DFactor &d, const std::vector<int32_t> &meta, const std::vector<int64_t> &round_ptr,
-                        const std::vector<uint32_t> &fptr, const std::vector<int32_t> &fcol,
-                        const std::vector<uint32_t> &bptr, const std::vector<int32_t> &bcol) {
-    d.ufold.release();
-    d.urow0 = 0;
-    if (round_ptr.size() < 3) return;
-    const int64_t ub0 = round_ptr[1], ub1 = round_ptr.back();
-    int64_t lo = INT64_MAX, hi = 0;
-    for (int64_t b = ub0; b < ub1; b++) lo = std::min<int64_t>(lo, meta[(size_t)b * 8]), hi = std::max<int64_t>(hi, meta[(size_t)b * 8 + 1]);
-    if (lo >= hi) return;
-    std::vector<int16_t> uf((size_t)(2 * (hi - lo)), 0);
-    parallel_for(ub1 - ub0, [&](int64_t a, int64_t z) {
-        for (int64_t b = ub0 + a; b < ub0 + z; b++) {
-            const int32_t r0 = meta[(size_t)b * 8], r1 = meta[(size_t)b * 8 + 1];
-            for (int32_t i = r0; i < r1; i++)
-                for (int dir = 0; dir < 2; dir++) {
-                    const std::vector<uint32_t> &ptr = dir ? bptr : fptr;
-                    const std::vector<int32_t> &col = dir ? bcol : fcol;
-                    uint32_t e = ptr[i];
-                    while (e < ptr[i + 1] && !(col[e] >= r0 && col[e] < r1)) e++;
-                    uf[(size_t)(2 * (i - lo) + dir)] = (int16_t)std::min<uint32_t>(e - ptr[i], INT16_MAX);
-                }
-        }
-    }, 64);
-    d.urow0 = (int32_t)lo;
-    d.ufold.upload(uf);
-}
 constexpr int64_t kInsertionSortMax = 32;  // rows up to this long sort by insertion (keys are distinct)
 void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vector<int64_t> *key,
                   const std::vector<std::vector<BwdExtra>> *extra, std::vector<int32_t> *fsrc,
@@ -434,8 +502,10 @@ void make_dfactor(const Factor &f, const Schedule &s, DFactor &d, const std::vec
         m[0] = (int32_t)r0, m[1] = (int32_t)r1, m[2] = (int32_t)l0, m[3] = (int32_t)l1;
         m[4] = (int32_t)fptr[r0], m[5] = (int32_t)fptr[r1], m[6] = (int32_t)bptr[r0], m[7] = (int32_t)bptr[r1];
     }
-    mark_dataflow(meta, s.round_ptr, fptr, fcol, bptr, bcol, d.dataflow);
-    build_ufold(d, meta, s.round_ptr, fptr, fcol, bptr, bcol);
+    {
+        const std::vector<int16_t> us = build_ufold(d, meta, s.round_ptr, fptr, fcol, bptr, bcol, [&](int64_t q) { return K(q); });
+        mark_dataflow(meta, s.round_ptr, fptr, fcol, bptr, bcol, d.dataflow, d.colsweep, us, d.urow0, &d.hmodel);
+    }
     d.meta.upload(meta);
     d.hmeta = meta;
     clk.lap("layout: uploads, block records, level-loop choice");
@@ -1092,6 +1162,7 @@ void dsep_sweep_setup(Ctx &c, DSep &T, const RankPlan &rp, int P) {
     for (int i = 0; i < 2; i++) d.sweep_rows[i] = sw.rows[i], d.sweep_cap[i] = sw.cap[i], d.sweep_threads[i] = sw.threads[i];
     d.pipelined = true, d.no_upper = false, d.no_col16 = true, d.fuse_last = false, d.skip0 = false;
     d.dataflow = c.opts.no_dataflow ? 1 : (c.opts.all_dataflow ? 2 : 0);
+    d.colsweep = c.opts.no_colsweep ? 1 : (c.opts.all_colsweep ? 2 : 0);
     d.N = NT;
     std::vector<uint32_t> fptr((size_t)NT + 1, 0), bptr((size_t)NT + 1, 0);
     std::vector<int32_t> fcol, bcol, perm((size_t)NT, 0);
@@ -1129,7 +1200,12 @@ void dsep_sweep_setup(Ctx &c, DSep &T, const RankPlan &rp, int P) {
         m[0] = (int32_t)r0, m[1] = (int32_t)r1, m[2] = (int32_t)S.blk_lvl[b], m[3] = (int32_t)S.blk_lvl[b + 1];
         m[4] = (int32_t)fptr[r0], m[5] = (int32_t)fptr[r1], m[6] = (int32_t)bptr[r0], m[7] = (int32_t)bptr[r1];
     }
-    mark_dataflow(meta, S.round_ptr, fptr, fcol, bptr, bcol, d.dataflow);
+    {
+        // row base + k is T row S.order[k]: its entries are in T's order (mark_dataflow checks it)
+        const std::vector<int16_t> us = build_ufold(d, meta, S.round_ptr, fptr, fcol, bptr, bcol,
+                    [&](int64_t q) { return q < base ? q - base : (int64_t)S.order[(size_t)(q - base)]; });
+        mark_dataflow(meta, S.round_ptr, fptr, fcol, bptr, bcol, d.dataflow, d.colsweep, us, d.urow0, nullptr);
+    }
     for (size_t r = 0; r < d.round_fits.size(); r++)
         for (int64_t b = S.round_ptr[r]; b < S.round_ptr[r + 1]; b++) {
             const int32_t *m = &meta[(size_t)b * 8];
@@ -1372,9 +1448,89 @@ __device__ __forceinline__ void fold_known(SweepLds &S, int nr, int tid) {
 // leading outside-term counts of the upper rounds' rows (DFactor::ufold): [2 (row - row0) + bwd]
 struct UFold {
     const int16_t *p = nullptr;
+    const int16_t *s = nullptr;  // DFactor::ustep, same layout
     int32_t row0 = 0;
 };
-static inline UFold ufold_of(const DFactor &F) { return UFold{F.ufold.n ? F.ufold.p : nullptr, F.urow0}; }
+static inline UFold ufold_of(const DFactor &F) {
+    return UFold{F.ufold.n ? F.ufold.p : nullptr, F.ustep.n ? F.ustep.p : nullptr, F.urow0};
+}
+
+// The column sweep (one wave; forward and backward alike): the block's rows in the order of
+// their keys -- step t solves the row of step t, and since every row's entries are stored in key
+// order (forward ascending, backward descending), each row meets its in-block terms at
+// increasing steps, all before its own (mark_dataflow checks this per block).  Lane L holds the
+// rows of steps L, L + 64, ... (RPL per lane) with their accumulators in registers.  Step t
+// broadcasts the finished value of its row from the owning lane (v_readlane, no LDS), and every
+// lane whose row's next term is column t subtracts it, then takes the outside terms (staged
+// products, 1.0 slot) that follow it in the row.  A dense chain (a separator clique: a level per
+// row) costs a step per row instead of a level-loop or dataflow trip per row.  Staged for it:
+// lv[t] = the local row of step t, c[e] = the step of an in-block column (R: outside).  Each row
+// keeps its next two terms in registers, so a refill's LDS latency is off the chain.
+// Same terms, same order, not-taken terms subtract +0.0 (an exact no-op): bit-identical.
+__device__ __forceinline__ double lane_bcast(double v, int lane) {  // lane: wave-uniform
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+template <int RPL>
+__device__ __forceinline__ void levels_colsweep(SweepLds &S, int nr, int R, int lane) {
+    // per row: the next two terms' staged columns (a step, or R: outside) and values, raw -- a
+    // refill is not looked at before the step after next, so its LDS latency stays off the chain
+    double acc[RPL], v0[RPL], v1[RPL];
+    int e[RPL], e1[RPL], c0[RPL], c1[RPL];
+#pragma unroll
+    for (int q = 0; q < RPL; q++) {
+        const int t = lane + q * kWave;
+        const int k = t < nr ? S.lv[t] : 0;
+        e[q] = t < nr ? S.ps[k] : 0, e1[q] = t < nr ? S.p[k + 1] : 0;
+        acc[q] = S.w[k];
+        c0[q] = (uint16_t)S.c[e[q]], v0[q] = S.v[e[q]];
+        c1[q] = (uint16_t)S.c[e[q] + 1], v1[q] = S.v[e[q] + 1];
+    }
+    // the row's next term taken: shift the pair, refill the second (entries stay inside the
+    // padded image: e + 1 <= e1 <= ne), then the outside terms that follow it
+    auto next = [&](int q) {
+        e[q]++, c0[q] = c1[q], v0[q] = v1[q];
+        c1[q] = (uint16_t)S.c[e[q] + 1], v1[q] = S.v[e[q] + 1];
+        while (e[q] < e1[q] && c0[q] == R) {
+            acc[q] -= v0[q];
+            e[q]++, c0[q] = c1[q], v0[q] = v1[q];
+            c1[q] = (uint16_t)S.c[e[q] + 1], v1[q] = S.v[e[q] + 1];
+        }
+    };
+#pragma unroll
+    for (int q = 0; q < RPL; q++)  // outside terms at a row's head (before its first in-block term)
+        if (e[q] < e1[q] && c0[q] == R) {
+            acc[q] -= v0[q];
+            next(q);
+        }
+#pragma unroll
+    for (int Q = 0; Q < RPL; Q++) {
+        const int jn = min(kWave, nr - Q * kWave);
+        for (int jj = 0; jj < jn; jj++) {
+            const int t = Q * kWave + jj;
+            const double x = lane_bcast(acc[Q], jj);  // the row of step t: every term taken
+#pragma unroll
+            for (int q = Q; q < RPL; q++) {
+                if (e[q] < e1[q] && c0[q] == t) {
+                    acc[q] -= v0[q] * x;
+                    next(q);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < RPL; q++) {
+        const int t = lane + q * kWave;
+        if (t < nr) S.w[S.lv[t]] = acc[q];
+    }
+}
+template <int R>
+__device__ __forceinline__ void colsweep_dispatch(SweepLds &S, int nr, int lane) {
+    if (nr <= kWave) levels_colsweep<1>(S, nr, R, lane);
+    else if (nr <= 2 * kWave) levels_colsweep<2>(S, nr, R, lane);
+    else levels_colsweep<4>(S, nr, R, lane);
+}
 
 // The level phase, out of LDS.  Per level every thread takes whole rows and consumes a row's
 // entries four at a time without branches: the (col, val) arrays are padded by four entries,
@@ -1879,9 +2035,11 @@ __device__ __forceinline__ void upper_block(
     const uint32_t e0 = BWD ? (uint32_t)m.be0 : (uint32_t)m.fe0;
     const int ne = BWD ? m.be1 - m.be0 : m.fe1 - m.fe0;
     const int tid = threadIdx.x;
+    // the column sweep for this block and direction (mark_dataflow); it needs the step table
+    const bool cs = uf.s != nullptr && (m.l1 & (BWD ? kMetaCsBwd : kMetaCsFwd));
     SweepLds S(smem, R, CAP);
     uint32_t q[RPU];
-    int32_t sp[RPU], fo[RPU];
+    int32_t sp[RPU], fo[RPU], st[RPU];
     double a[RPU], d[RPU];
     int32_t c[EPU];
     double v[EPU], g[EPU];
@@ -1890,6 +2048,7 @@ __device__ __forceinline__ void upper_block(
         const int i = tid + j * TPB, rr = r0 + (i < nr ? i : nr - 1);
         q[j] = ptr[rr], sp[j] = (BWD ? out != nullptr : !sched_in) ? perm[rr] : rr;
         fo[j] = uf.p ? uf.p[2 * (rr - uf.row0) + (BWD ? 1 : 0)] : 0;
+        st[j] = cs ? uf.s[2 * (rr - uf.row0) + (BWD ? 1 : 0)] : 0;
         if (BWD) d[j] = D[rr];
     }
 #pragma unroll
@@ -1898,7 +2057,15 @@ __device__ __forceinline__ void upper_block(
         const uint32_t ec = e0 + (uint32_t)(e < ne ? e : 0);
         c[u] = __builtin_nontemporal_load(col + ec), v[u] = __builtin_nontemporal_load(val + ec);
     }
-    for (int l = tid; l <= nl; l += TPB) S.lv[l] = (int16_t)(lvl_row[m.l0 + l] - r0);
+    // column sweep: an in-block column's step (static: before the wait); lv holds the rows by step
+    int32_t cl[EPU];
+#pragma unroll
+    for (int u = 0; u < EPU; u++) {
+        const bool local = c[u] >= r0 && c[u] < r1;
+        cl[u] = !local ? R : (cs ? (int32_t)uf.s[2 * (c[u] - uf.row0) + (BWD ? 1 : 0)] : c[u] - r0);
+    }
+    if (!cs)
+        for (int l = tid; l <= nl; l += TPB) S.lv[l] = (int16_t)(lvl_row[m.l0 + l] - r0);
 #pragma unroll
     for (int j = 0; j < RPU; j++) {
         if (!BWD) a[j] = xin[sp[j]];
@@ -1916,6 +2083,7 @@ __device__ __forceinline__ void upper_block(
         if (i < nr) {
             S.p[i] = (int16_t)(q[j] - e0);
             if (uf.p) S.ps[i] = (int16_t)(q[j] - e0 + fo[j]);
+            if (cs) S.lv[st[j]] = (int16_t)i;
             S.w[i] = BWD ? a[j] / d[j] : ((sp[j] >= neg_from) ? -a[j] : a[j]);
             if (!BWD && xs) xs[r0 + i] = S.w[i];
         }
@@ -1927,7 +2095,7 @@ __device__ __forceinline__ void upper_block(
         const int e = tid + u * TPB;
         if (e < ne) {
             const bool local = c[u] >= r0 && c[u] < r1;
-            S.c[e] = local ? (int16_t)(c[u] - r0) : (int16_t)R;  // outside: pre-multiplied, 1.0 slot
+            S.c[e] = (int16_t)cl[u];  // outside: R, pre-multiplied against the 1.0 slot
             S.v[e] = local ? v[u] : v[u] * g[u];
         }
     }
@@ -1940,7 +2108,8 @@ __device__ __forceinline__ void upper_block(
     // (a single wave's LDS accesses complete in program order) the chain is LDS latency only;
     // narrow levels give each row a lane group (levels_grouped)
     if (tid < kWave) {
-        if (CPK_UPPER_DATAFLOW && (m.l1 & (BWD ? kMetaDfBwd : kMetaDfFwd)))
+        if (cs) colsweep_dispatch<R>(S, nr, tid);
+        else if (CPK_UPPER_DATAFLOW && (m.l1 & (BWD ? kMetaDfBwd : kMetaDfFwd)))
             levels_dataflow<BWD, CPK_DF_CH(BWD), true, R / kWave>(S, nr, R, ne, tid);
         else if (CPK_UPPER_GROUP(BWD)) levels_grouped<CPK_UPPER_CH(BWD), BWD, true>(S, nl, false, tid);
         else sweep_levels<kWave, BWD, true, CPK_UPPER_CH(BWD), true, true>(S, nl, false, tid);
@@ -2003,9 +2172,10 @@ __device__ __forceinline__ void last_block(
     const int r0 = m.r0, r1 = m.r1, nr = r1 - r0, nl = (m.l1 & kMetaL1Mask) - m.l0;
     const int nef = m.fe1 - m.fe0, neb = m.be1 - m.be0;
     const int tid = threadIdx.x;
+    const bool csf = uf.s != nullptr && (m.l1 & kMetaCsFwd), csb = uf.s != nullptr && (m.l1 & kMetaCsBwd);
     SweepLds S(smem, R, CAP);
     uint32_t qf[RPU], qb[RPU];
-    int32_t sp[RPU], dp[RPU], fof[RPU], fob[RPU];
+    int32_t sp[RPU], dp[RPU], fof[RPU], fob[RPU], stf[RPU], stb[RPU];
     double a[RPU], d[RPU];
     int32_t cf[EPU], cb[EPU];
     double vf[EPU], vb[EPU], g[EPU];
@@ -2014,6 +2184,7 @@ __device__ __forceinline__ void last_block(
         const int i = tid + j * TPB, rr = r0 + (i < nr ? i : nr - 1);
         qf[j] = fptr[rr], qb[j] = bptr[rr], d[j] = D[rr];
         fof[j] = uf.p ? uf.p[2 * (rr - uf.row0)] : 0, fob[j] = uf.p ? uf.p[2 * (rr - uf.row0) + 1] : 0;
+        stf[j] = csf ? uf.s[2 * (rr - uf.row0)] : 0, stb[j] = csb ? uf.s[2 * (rr - uf.row0) + 1] : 0;
         sp[j] = sched_in ? rr : perm[rr];
         dp[j] = out ? perm[rr] : rr;
     }
@@ -2023,7 +2194,14 @@ __device__ __forceinline__ void last_block(
         const uint32_t ef = (uint32_t)m.fe0 + (uint32_t)(e < nef ? e : 0);
         cf[u] = __builtin_nontemporal_load(fcol + ef), vf[u] = __builtin_nontemporal_load(fval + ef);
     }
-    for (int l = tid; l <= nl; l += TPB) S.lv[l] = (int16_t)(lvl_row[m.l0 + l] - r0);
+    int32_t cl[EPU];  // staged columns: local row, or the step (column sweep); R outside
+#pragma unroll
+    for (int u = 0; u < EPU; u++) {
+        const bool local = cf[u] >= r0 && cf[u] < r1;
+        cl[u] = !local ? R : (csf ? (int32_t)uf.s[2 * (cf[u] - uf.row0)] : cf[u] - r0);
+    }
+    if (!csf)
+        for (int l = tid; l <= nl; l += TPB) S.lv[l] = (int16_t)(lvl_row[m.l0 + l] - r0);
 #pragma unroll
     for (int j = 0; j < RPU; j++) a[j] = xin[sp[j]];
     wait();
@@ -2044,6 +2222,7 @@ __device__ __forceinline__ void last_block(
         if (i < nr) {
             S.p[i] = (int16_t)(qf[j] - (uint32_t)m.fe0);
             if (uf.p) S.ps[i] = (int16_t)(qf[j] - (uint32_t)m.fe0 + fof[j]);
+            if (csf) S.lv[stf[j]] = (int16_t)i;
             S.w[i] = (sp[j] >= neg_from) ? -a[j] : a[j];
             if (xs) xs[r0 + i] = S.w[i];
         }
@@ -2055,7 +2234,7 @@ __device__ __forceinline__ void last_block(
         const int e = tid + u * TPB;
         if (e < nef) {
             const bool local = cf[u] >= r0 && cf[u] < r1;
-            S.c[e] = local ? (int16_t)(cf[u] - r0) : (int16_t)R;
+            S.c[e] = (int16_t)cl[u];
             S.v[e] = local ? vf[u] : vf[u] * g[u];
         }
     }
@@ -2063,7 +2242,8 @@ __device__ __forceinline__ void last_block(
     if (uf.p) fold_known<TPB>(S, nr, tid);
     else fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd)) levels_dataflow<false, CPK_DF_CH(false), true, R / kWave>(S, nr, R, nef, tid);
+        if (csf) colsweep_dispatch<R>(S, nr, tid);
+        else if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd)) levels_dataflow<false, CPK_DF_CH(false), true, R / kWave>(S, nr, R, nef, tid);
         else if (CPK_UPPER_GROUP(false)) levels_grouped<CPK_UPPER_CH(false), false, true>(S, nl, false, tid);
         else sweep_levels<kWave, false, true, CPK_UPPER_CH(false), true, true>(S, nl, false, tid);
     }
@@ -2079,18 +2259,20 @@ __device__ __forceinline__ void last_block(
             S.w[i] = S.w[i] / d[j];
             S.p[i] = (int16_t)(qb[j] - (uint32_t)m.be0);
             if (uf.p) S.ps[i] = (int16_t)(qb[j] - (uint32_t)m.be0 + fob[j]);
+            if (csb) S.lv[stb[j]] = (int16_t)i;
         }
     }
     if (tid == 0) S.p[nr] = (int16_t)neb;
     if (tid < kSweepPad) S.c[neb + tid] = (int16_t)R;
-    if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd) && !(m.l1 & kMetaDfBwd))  // the forward flags took lv
+    // the level loop needs the level bounds back if the forward loop took lv (flags or steps)
+    if ((csf || (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd))) && !csb && !(CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfBwd)))
         for (int l = tid; l <= nl; l += TPB) S.lv[l] = (int16_t)(lvl_row[m.l0 + l] - r0);
 #pragma unroll
     for (int u = 0; u < EPU; u++) {
         const int e = tid + u * TPB;
         if (e < neb) {
             const bool local = cb[u] >= r0 && cb[u] < r1;
-            S.c[e] = local ? (int16_t)(cb[u] - r0) : (int16_t)R;
+            S.c[e] = !local ? (int16_t)R : (int16_t)(csb ? uf.s[2 * (cb[u] - uf.row0) + 1] : cb[u] - r0);
             S.v[e] = local ? vb[u] : vb[u] * g[u];
         }
     }
@@ -2098,7 +2280,8 @@ __device__ __forceinline__ void last_block(
     if (uf.p) fold_known<TPB>(S, nr, tid);
     else fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfBwd)) levels_dataflow<true, CPK_DF_CH(true), true, R / kWave>(S, nr, R, neb, tid);
+        if (csb) colsweep_dispatch<R>(S, nr, tid);
+        else if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfBwd)) levels_dataflow<true, CPK_DF_CH(true), true, R / kWave>(S, nr, R, neb, tid);
         else if (CPK_UPPER_GROUP(true)) levels_grouped<CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
         else sweep_levels<kWave, true, true, CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
     }

@@ -58,6 +58,8 @@ const BoolOpt kBool[] = {
     {"no_col16", &EngineOpts::no_col16},
     {"no_dataflow", &EngineOpts::no_dataflow},
     {"all_dataflow", &EngineOpts::all_dataflow},
+    {"no_colsweep", &EngineOpts::no_colsweep},
+    {"all_colsweep", &EngineOpts::all_colsweep},
     {"no_sched_resid", &EngineOpts::no_sched_resid},
     {"no_fused_resid", &EngineOpts::no_fused_resid},
     {"tsolve_global", &EngineOpts::tsolve_global},

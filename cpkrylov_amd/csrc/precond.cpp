@@ -98,6 +98,7 @@ Precond *precond_create(Ctx &c, Analysis &&an, PrecondPre *pre) {
     pc->dF.pipelined = !c.opts.no_pipe, pc->dF.no_upper = c.opts.no_upper, pc->dF.no_col16 = c.opts.no_col16;
     pc->dF.no_chain = c.opts.no_chain;
     pc->dF.dataflow = c.opts.no_dataflow ? 1 : (c.opts.all_dataflow ? 2 : 0);
+    pc->dF.colsweep = c.opts.no_colsweep ? 1 : (c.opts.all_colsweep ? 2 : 0);
     pc->dF.no_fused_resid = c.opts.no_fused_resid;
     pc->dF.fuse_last = !c.opts.no_fuse_last;  // single GPU: no entries outside the factor
     pc->no_sched = c.opts.no_sched_resid;
@@ -265,6 +266,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     pc->dF.pipelined = !c.opts.no_pipe, pc->dF.no_upper = c.opts.no_upper, pc->dF.no_col16 = c.opts.no_col16;
     pc->dF.no_chain = c.opts.no_chain;
     pc->dF.dataflow = c.opts.no_dataflow ? 1 : (c.opts.all_dataflow ? 2 : 0);
+    pc->dF.colsweep = c.opts.no_colsweep ? 1 : (c.opts.all_colsweep ? 2 : 0);
     pc->dF.no_fused_resid = c.opts.no_fused_resid;
     {
         Factor Fl = relabel(rp.Fsub, S);

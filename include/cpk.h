@@ -135,7 +135,8 @@ int cpk_ctx_create_sim(int device, cpk_simgroup group, int rank, int nranks, cpk
  * once at creation; a change applies to preconditioners and solves created afterwards.
  * Names: sweep ("rows,cap,threads[,rows,cap,threads[,sub0]]"; unset, each path has its own
  * default: a distributed context reports and uses the distributed one), split_tol, host_factor,
- * no_pipe, no_upper, no_col16, no_dataflow, all_dataflow, no_sched_resid, no_fused_resid, r0_xcd_chunk, tsolve_global, tsolve_sweep,
+ * no_pipe, no_upper, no_col16, no_dataflow, all_dataflow, no_colsweep, all_colsweep, no_chain, exact_dots,
+ * no_sched_resid, no_fused_resid, r0_xcd_chunk, tsolve_global, tsolve_sweep,
  * no_piggy, no_halo_merge, no_graph, no_fuse_last, no_tkr, no_minres_fuse, dist_graph, batch,
  * dist1 (a 1-rank communicator runs the distributed kernels; set before building operators),
  * profile_fwd_sched (diagnostic), sweep_set ("0" returns sweep to the per-path default).
@@ -305,6 +306,11 @@ int cpk_debug_pipe_stamps(uint64_t *out, int npairs, int *copied);
  * out[v * 131072 + block] for v = forward, forward with the fused refinement residual, backward,
  * backward accumulating; *copied = 0 unless built with -DCPK_PIPE_STAMPS (tools/blk_cycles.py). */
 int cpk_debug_blk_cycles(uint64_t *out, int64_t n, int64_t *copied);
+/* Diagnostic: the upper-round loop-cost model of a preconditioner's sweeps, 8 int64 per (upper
+ * block, direction): block, direction (0 forward), rows, level-loop trips, dataflow trips (-1:
+ * not modelled), outside terms behind in-block ones, column sweep valid, loop chosen (0 level,
+ * 1 dataflow, 2 column sweep).  out = NULL: *copied = the total count. */
+int cpk_debug_block_model(cpk_pc M, int64_t *out, int64_t n, int64_t *copied);
 
 /* [c, s, d] = SymGivens(a, b)  (util/SymGivens.m:1-29) */
 int cpk_symgivens(double a, double b, double *c, double *s, double *d);

@@ -387,7 +387,8 @@ def test_dist_minres_fused_update_bitexact(P):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("path", ["tsolve_global", "tsolve_sweep", "tsolve_sweep,all_dataflow",
-                                  "tsolve_sweep,no_dataflow"])
+                                  "tsolve_sweep,no_dataflow", "tsolve_sweep,all_colsweep",
+                                  "tsolve_sweep,all_colsweep,no_chain"])
 @pytest.mark.parametrize("P", [2, 4])
 def test_dist_apply_separator_fallbacks_bitexact(P, path):
     """The separator solve's other paths -- records left in HBM (a separator too large for LDS),

@@ -410,9 +410,11 @@ def test_precond_apply_sweep_chain(gpu_ctx, name, props):
 @pytest.mark.parametrize("props", [dict(nitref=0), dict(nitref=1, force_itref=True),
                                    dict(nitref=2, force_itref=False, itref_tol=1e-30)])
 def test_precond_apply_dataflow_levels(gpu_ctx, name, props):
-    """The upper rounds' two level loops: the level-synchronous loop (engine option no_dataflow)
-    and the dataflow loop (levels_dataflow; all_dataflow forces it on every upper block), and the
-    default per-block choice of the host model -- with the default staging and small blocks
+    """The upper rounds' three level loops: the level-synchronous loop (engine option no_dataflow),
+    the dataflow loop (levels_dataflow; all_dataflow forces it on every upper block) and the
+    column sweep (levels_colsweep; all_colsweep forces it on every block of <= 256 rows whose
+    entries follow the key order, chained and per round), and the default per-block choice of
+    the host model -- with the default staging and small blocks
     (many upper rounds, the fused last round among them), on a system whose separators are dense
     chains (w64: the +-64 coupling window, where the model picks the dataflow loop).  Every way
     the oracle's bits."""
@@ -428,7 +430,8 @@ def test_precond_apply_dataflow_levels(gpu_ctx, name, props):
     z = np.random.default_rng(37).standard_normal(G.shape[0] + B.shape[0])
     for sweep in ("", "64,192,64,128,512,512"):
         ys = []
-        for mode in ({}, {"no_dataflow": 1}, {"all_dataflow": 1}):
+        for mode in ({}, {"no_dataflow": 1, "no_colsweep": 1}, {"all_dataflow": 1, "no_colsweep": 1},
+                     {"all_colsweep": 1}, {"all_colsweep": 1, "no_chain": 1}):
             opts = dict(mode)
             if sweep:
                 opts["sweep"] = sweep

@@ -55,3 +55,18 @@ for r in range(1, len(rp) - 1):
         out["total_mean_median_max"] = [round(float(tot.mean()), 0), round(float(np.median(tot)), 0),
                                         round(float(tot.max()), 0)]
         print(json.dumps(out), flush=True)
+
+# per-block records (BLOCKS=<path>): the loop-cost model of every upper block and direction
+# (cpk_debug_block_model) beside its measured phase cycles -- the model's calibration data
+if os.environ.get("BLOCKS"):
+    n = C.c_int64(0)
+    _lib.check(_lib.lib.cpk_debug_block_model(M.h, None, 1 << 40, C.byref(n)))
+    mod = np.zeros(max(n.value, 1), np.int64)
+    _lib.check(_lib.lib.cpk_debug_block_model(M.h, mod.ctypes.data_as(C.POINTER(C.c_int64)), n.value, C.byref(n)))
+    mod = mod[:n.value].reshape(-1, 8)
+    with open(os.environ["BLOCKS"], "w") as f:
+        for b, d, nr, lt, dt, outs, valid, choice in mod.tolist():
+            ph = cyc[4 + 4 * d: 8 + 4 * d, b].tolist() if b < KMAX else [0, 0, 0, 0]
+            f.write(json.dumps({"b": b, "dir": d, "nr": nr, "lt": lt, "dt": dt, "outs": outs, "valid": valid,
+                                "choice": choice, "cyc": ph}) + "\n")
+
