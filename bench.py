@@ -530,8 +530,10 @@ def w64_block(args):
     """SURVEY 8d's +-64 B window (nnz(L) ~ 40.9 M, elimination tree 255 deep): the same bench in
     a child process (its own cpu_baseline sample, parity, PMC traffic), embedded as a block."""
     import subprocess
+    # CPU budget: the serial leg (half of it) must run the ~17 iterations to convergence, ~1 s
+    # each here, for the parity block against the serial oracle
     cmd = [sys.executable, os.path.abspath(__file__), "--window", "64", "--steps", str(args.steps), "--warmup",
-           str(args.warmup), "--cpu-seconds", str(min(args.cpu_seconds, 10.0)), "--no-w64"]
+           str(args.warmup), "--cpu-seconds", str(max(args.cpu_seconds, 40.0)), "--no-w64"]
     if args.no_pmc:
         cmd.append("--no-pmc")
     if args.no_cpu_baseline:
