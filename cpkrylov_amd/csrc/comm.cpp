@@ -40,6 +40,23 @@ struct RcclComm : Comm {
     void allgather(const double *send, double *recv, size_t n, hipStream_t s) override {
         nccl_check(ncclAllGather(send, recv, n, ncclDouble, c, s), "ncclAllGather");
     }
+    // host bytes through a device staging buffer, in chunks (RCCL moves device memory only)
+    void broadcast_host(void *p, size_t n, int root, hipStream_t s) override {
+        if (!n) return;
+        int me = 0;
+        nccl_check(ncclCommUserRank(c, &me), "ncclCommUserRank");
+        constexpr size_t kChunk = size_t(256) << 20;
+        DBuf<char> d;
+        d.alloc(std::min(n, kChunk));
+        char *h = static_cast<char *>(p);
+        for (size_t o = 0; o < n; o += kChunk) {
+            const size_t k = std::min(kChunk, n - o);
+            if (me == root) CPK_HIP(hipMemcpyAsync(d.p, h + o, k, hipMemcpyHostToDevice, s));
+            nccl_check(ncclBroadcast(d.p, d.p, k, ncclChar, root, c, s), "ncclBroadcast");
+            if (me != root) CPK_HIP(hipMemcpyAsync(h + o, d.p, k, hipMemcpyDeviceToHost, s));
+            CPK_HIP(hipStreamSynchronize(s));
+        }
+    }
     bool capturable() const override { return true; }  // the solvers also check the dist_graph option
     int kind() const override { return CPK_COMM_RCCL; }
     int count() const override {
@@ -83,6 +100,9 @@ struct NullComm : Comm {
     void allgather(const double *send, double *recv, size_t n, hipStream_t s) override {
         if (n) CPK_HIP(hipMemcpyAsync(recv + (size_t)rank * n, send, n * sizeof(double), hipMemcpyDeviceToDevice, s));
     }
+    void broadcast_host(void *, size_t, int, hipStream_t) override {
+        throw Error(CPK_ERR_UNSUPPORTED, "internal: broadcast on the peer-less timing communicator");
+    }
     bool capturable() const override { return true; }
     bool has_peers() const override { return false; }
     int kind() const override { return CPK_COMM_NULL; }
@@ -104,6 +124,7 @@ struct SimGroup {
     // where every rank is (a mismatched collective sequence, or a rank stuck in a device wait)
     std::vector<uint64_t> seq;
     std::vector<std::string> last;
+    std::vector<char> host;  // broadcast_host's staging
     int timeout_s = 300;  // CPK_SIM_TIMEOUT_S
     explicit SimGroup(int p) : P(p), seq(p, 0), last(p) {
         if (const char *e = std::getenv("CPK_SIM_TIMEOUT_S")) timeout_s = std::max(1, std::atoi(e));
@@ -173,6 +194,14 @@ struct SimComm : Comm {
         if (n) CPK_HIP(hipMemcpyAsync(recv, g->shared.p, n * g->P * sizeof(double), hipMemcpyDeviceToDevice, s));
         CPK_HIP(hipStreamSynchronize(s));
         g->barrier(rank);
+    }
+    void broadcast_host(void *p, size_t n, int root, hipStream_t) override {
+        g->enter(rank, "broadcast_host", n);
+        if (rank == root) g->host.assign(static_cast<char *>(p), static_cast<char *>(p) + n);
+        g->barrier(rank);
+        if (rank != root) std::memcpy(p, g->host.data(), n);
+        g->barrier(rank);
+        if (rank == root) std::vector<char>().swap(g->host);
     }
     bool capturable() const override { return false; }
     int kind() const override { return CPK_COMM_SIM; }

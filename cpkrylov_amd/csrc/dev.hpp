@@ -69,6 +69,9 @@ struct Comm {
     virtual void allgather(const double *send, double *recv, size_t n, hipStream_t s) = 0;
     virtual bool capturable() const = 0;  // may be captured into a hipGraph
     virtual bool has_peers() const { return true; }  // false: the timing stand-in (no exchange)
+    // rank `root`'s n host bytes at p to every rank's p (the distributed construction's analysis,
+    // precond.cpp); n is the same on every rank.  Only where has_peers().
+    virtual void broadcast_host(void *p, size_t n, int root, hipStream_t s) = 0;
     virtual int kind() const = 0;   // CPK_COMM_RCCL / _SIM / _NULL (cpk_ctx_get_info)
     virtual int count() const = 0;  // ranks of the communicator (RCCL: ncclCommCount)
 };
@@ -121,6 +124,8 @@ struct EngineOpts {
     bool no_tkr = false;          // no_tkr:             distributed refinement residual through the Kp halo
     bool no_minres_fuse = false;  // no_minres_fuse:     cpminres update as its own pass (normalise + w, x)
     bool no_chain = false;        // no_chain:           upper rounds one launch per round (not the sweep chain)
+    bool no_bcast_analysis = false;  // no_bcast_analysis: every rank of a distributed preconditioner runs the global analysis
+    int chain_wide = 256;         // chain_wide:         rounds of at most this many blocks join the sweep chain
     bool dist_graph = true;       // dist_graph:         capture collectives in the graphs
     bool dist1 = false;           // dist1:              a 1-rank communicator runs the distributed path
                                   //                     (diagnostic; set before building operators)
@@ -263,6 +268,7 @@ struct DFactor {
     DChain chain[3];
     int64_t chain_first = 1;  // the first chained round (the chains cover [chain_first, R))
     bool no_chain = false;  // engine option no_chain (set before make_dfactor)
+    int chain_wide = 256;   // engine option chain_wide
     std::vector<int64_t> round_ptr;  // host copy: blocks per round
     std::vector<char> round_fits;    // host: every block of round r fits (sweep_rows[1], sweep_cap[1])
     int sweep_rows[2] = {192, 1024}, sweep_cap[2] = {576, 4096}, sweep_threads[2] = {64, 512};  // round 0 / rest
@@ -453,6 +459,7 @@ struct Analysis {
     bool device_numeric = false;
     LdlSymbolic sym;
     std::vector<int32_t> rsrc;  // F's entry t came from F0's entry rsrc[t]
+    uint64_t input_hash = 0;    // this rank's own A11, B, C22 (pattern and values): the plan agreement
 };
 // on_symbolic (optional) runs on a second host thread as soon as the symbolic factor exists,
 // beside the schedule and the relabelling (which only read it), and is joined before analyze

@@ -2360,11 +2360,10 @@ static void launch_last(Ctx &c, const DFactor &F, const FwdIn &in, double *w, do
 // the epoch.  Every spin is bounded: a wait that outlives kChainSpinCap sets the error word, every
 // other waiter then gives up, and the host raises CPK_ERR_HIP (check_chain).
 constexpr uint32_t kChainSpinCap = 1u << 20;
-// the rounds a chain covers: the narrow top of the tree (rounds of at most kChainWide blocks,
+// the rounds a chain covers: the narrow top of the tree (rounds of at most chain_wide blocks,
 // and at least two of them).  A wide round's blocks are all ready at once -- a launch of their
 // own costs nothing there -- and in a chain hundreds of its blocks would sit polling the few
 // flags of the round above: the guide's warning, many pollers cut the chip's bandwidth.
-constexpr int64_t kChainWide = 256;
 struct ChainArgs {
     const int32_t *task, *dptr, *didx;
     uint32_t *flag, *ctrl;
@@ -2518,7 +2517,7 @@ static void build_chain(DFactor &d, const std::vector<int32_t> &meta, const std:
     // the chained rounds: the narrow top [first, R), two rounds at least, every one through the
     // block kernel
     int64_t first = R;
-    while (first > 1 && d.round_ptr[first] - d.round_ptr[first - 1] <= kChainWide) first--;
+    while (first > 1 && d.round_ptr[first] - d.round_ptr[first - 1] <= d.chain_wide) first--;
     if (R - first < 2) return;
     for (int64_t r = first; r < R; r++)
         if (r >= (int64_t)d.round_fits.size() || !d.round_fits[r]) return;

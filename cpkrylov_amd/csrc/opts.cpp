@@ -74,6 +74,7 @@ const BoolOpt kBool[] = {
     {"dist1", &EngineOpts::dist1},
     {"exact_dots", &EngineOpts::exact_dots},
     {"no_chain", &EngineOpts::no_chain},
+    {"no_bcast_analysis", &EngineOpts::no_bcast_analysis},
     {"profile_fwd_sched", &EngineOpts::profile_fwd_sched},
 };
 
@@ -112,6 +113,12 @@ void set_engine_option(EngineOpts &o, const std::string &name, const std::string
         if (end == value.c_str() || *end != '\0' || v < 0 || v > 4096)
             throw Error(CPK_ERR_ARGS, "engine option " + name + " must be an integer in [0, 4096], got '" + value + "'");
         (name == "batch" ? o.batch : o.r0_xcd_chunk) = (int)v;
+    } else if (name == "chain_wide") {
+        char *end = nullptr;
+        const long v = strtol(value.c_str(), &end, 10);
+        if (end == value.c_str() || *end != '\0' || v < 1 || v > (1L << 24))
+            throw Error(CPK_ERR_ARGS, "engine option chain_wide must be an integer in [1, 2^24], got '" + value + "'");
+        o.chain_wide = (int)v;
     } else {
         throw Error(CPK_ERR_ARGS, "unknown engine option '" + name + "'");
     }
@@ -129,6 +136,7 @@ std::string get_engine_option(const EngineOpts &o, const std::string &name, bool
     }
     if (name == "batch") return std::to_string(o.batch);
     if (name == "r0_xcd_chunk") return std::to_string(o.r0_xcd_chunk);
+    if (name == "chain_wide") return std::to_string(o.chain_wide);
     throw Error(CPK_ERR_ARGS, "unknown engine option '" + name + "'");
 }
 
@@ -144,6 +152,7 @@ EngineOpts engine_opts_from_env() {
     from("split_tol");
     from("batch");
     from("r0_xcd_chunk");
+    from("chain_wide");
     return o;
 }
 
@@ -156,6 +165,7 @@ std::string engine_opts_string(const EngineOpts &o, bool dist) {
     put("split_tol");
     put("batch");
     put("r0_xcd_chunk");
+    put("chain_wide");
     return s;
 }
 
@@ -189,6 +199,7 @@ uint64_t engine_opts_hash(const EngineOpts &o) {
     mix(get_engine_option(o, "split_tol"));
     mix(std::to_string(o.batch));
     mix(std::to_string(o.r0_xcd_chunk));
+    mix(std::to_string(o.chain_wide));
     return h;
 }
 

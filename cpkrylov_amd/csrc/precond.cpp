@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -97,6 +98,7 @@ Precond *precond_create(Ctx &c, Analysis &&an, PrecondPre *pre) {
         pc->dF.sweep_threads[i] = an.sweep.threads[i];
     pc->dF.pipelined = !c.opts.no_pipe, pc->dF.no_upper = c.opts.no_upper, pc->dF.no_col16 = c.opts.no_col16;
     pc->dF.no_chain = c.opts.no_chain;
+    pc->dF.chain_wide = c.opts.chain_wide;
     pc->dF.dataflow = c.opts.no_dataflow ? 1 : (c.opts.all_dataflow ? 2 : 0);
     pc->dF.colsweep = c.opts.no_colsweep ? 1 : (c.opts.all_colsweep ? 2 : 0);
     pc->dF.no_fused_resid = c.opts.no_fused_resid;
@@ -194,6 +196,7 @@ uint64_t plan_hash(const Ctx &c, const Analysis &an, const TreeSplit &ts) {
     uint64_t h = engine_opts_hash(c.opts);
     auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
     mix((uint64_t)c.nranks), mix((uint64_t)an.n), mix((uint64_t)an.m), mix((uint64_t)an.Kp.nnz());
+    mix(an.input_hash);
     for (int32_t v : an.F0.perm) mix((uint32_t)v);
     for (int64_t v : an.F0.Lp) mix((uint64_t)v);
     for (int32_t v : ts.node_rank) mix((uint32_t)v);
@@ -265,6 +268,7 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
         pc->dF.sweep_rows[i] = sw.rows[i], pc->dF.sweep_cap[i] = sw.cap[i], pc->dF.sweep_threads[i] = sw.threads[i];
     pc->dF.pipelined = !c.opts.no_pipe, pc->dF.no_upper = c.opts.no_upper, pc->dF.no_col16 = c.opts.no_col16;
     pc->dF.no_chain = c.opts.no_chain;
+    pc->dF.chain_wide = c.opts.chain_wide;
     pc->dF.dataflow = c.opts.no_dataflow ? 1 : (c.opts.all_dataflow ? 2 : 0);
     pc->dF.colsweep = c.opts.no_colsweep ? 1 : (c.opts.all_colsweep ? 2 : 0);
     pc->dF.no_fused_resid = c.opts.no_fused_resid;
@@ -513,10 +517,108 @@ Precond *precond_create_dist(Ctx &c, Analysis &&an, const HCsr *Akry) {
     return pc.release();
 }
 
+// FNV-1a over the dimensions, the pattern and the value bits of the three blocks
+static uint64_t input_hash(const HCsr &A11, const HCsr &B, const HCsr &C22) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+    for (const HCsr *a : {&A11, &B, &C22}) {
+        mix((uint64_t)a->nrows), mix((uint64_t)a->ncols);
+        for (int64_t v : a->ptr) mix((uint64_t)v);
+        for (int32_t v : a->ind) mix((uint32_t)v);
+        for (double v : a->val) {
+            uint64_t u;
+            std::memcpy(&u, &v, sizeof u);
+            mix(u);
+        }
+    }
+    return h;
+}
+
+// The global analysis of a distributed preconditioner, once: rank 0 runs it and broadcasts the
+// parts every rank's plan and device factorization read (Kp, the exported factor's structure,
+// the device phase's symbolic data), field by field straight from and into the vectors; the
+// other ranks skip the ordering and the symbolic factorization (S50 at P = 8: ~3.9 s of host
+// work and its memory peak, 8 times over on one node's cores).  Each rank still hashes its own
+// inputs into the plan agreement, so ranks given different matrices fail as before.  A failure
+// on rank 0 travels with the broadcast: every rank throws its message.
+namespace {
+struct AnalysisBcast {
+    Comm &cm;
+    hipStream_t s;
+    template <class T>
+    void pod(T &v) { cm.broadcast_host(&v, sizeof v, 0, s); }
+    template <class T>
+    void vec(std::vector<T> &v) {
+        uint64_t n = v.size();
+        pod(n);
+        v.resize((size_t)n);
+        if (n) cm.broadcast_host(v.data(), (size_t)n * sizeof(T), 0, s);
+    }
+    void run(Analysis &an) {
+        pod(an.n), pod(an.m), pod(an.N), pod(an.ordering), pod(an.seconds), pod(an.sweep);
+        uint8_t dn = an.device_numeric ? 1 : 0;
+        pod(dn);
+        an.device_numeric = dn != 0;
+        pod(an.Kp.nrows), pod(an.Kp.ncols), vec(an.Kp.ptr), vec(an.Kp.ind), vec(an.Kp.val);
+        pod(an.F0.N), vec(an.F0.perm), vec(an.F0.Lp), vec(an.F0.Li), vec(an.F0.Lx), vec(an.F0.D), vec(an.F0.parent);
+        LdlSymbolic &y = an.sym;
+        pod(y.N), vec(y.Rp), vec(y.Rc), vec(y.Rcsc), vec(y.kp_ptr), vec(y.kp_tgt), vec(y.kp_src), vec(y.lev_ptr),
+            vec(y.lev_rows);
+        vec(an.rsrc);
+    }
+};
+}  // namespace
+
+// every rank's vote (all must agree to broadcast: a rank that analyzes on its own while the
+// others wait in a broadcast would never meet them)
+static bool all_ranks(Ctx &c, bool mine) {
+    DBuf<double> snd, rcv;
+    snd.alloc(1), rcv.alloc((size_t)c.nranks);
+    const double v = mine ? 1.0 : 0.0;
+    CPK_HIP(hipMemcpy(snd.p, &v, sizeof v, hipMemcpyHostToDevice));
+    c.comm->allgather(snd.p, rcv.p, 1, c.stream);
+    std::vector<double> all((size_t)c.nranks);
+    CPK_HIP(hipMemcpyAsync(all.data(), rcv.p, rcv.bytes(), hipMemcpyDeviceToHost, c.stream));
+    CPK_HIP(hipStreamSynchronize(c.stream));
+    for (double a : all)
+        if (a != 1.0) return false;
+    return true;
+}
+
+static Analysis analyze_dist(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22, bool dev) {
+    Analysis an;
+    if (c.nranks <= 1 || !c.comm->has_peers() || !all_ranks(c, !c.opts.no_bcast_analysis)) {
+        an = analyze(A11, B, C22, c.opts, dev, {}, false);
+    } else {
+        const auto t0 = std::chrono::steady_clock::now();
+        PhaseClock pcl("precond_create_dist");
+        std::string err;
+        if (c.rank == 0) {
+            try {
+                an = analyze(A11, B, C22, c.opts, dev, {}, false);
+            } catch (const std::exception &e) {
+                err = e.what();
+                if (err.empty()) err = "analysis failed";
+            }
+        }
+        AnalysisBcast bc{*c.comm, c.stream};
+        std::vector<char> msg(err.begin(), err.end());
+        bc.vec(msg);
+        err.assign(msg.begin(), msg.end());
+        if (!err.empty()) throw Error(CPK_ERR_ARGS, "distributed preconditioner (analysis on rank 0): " + err);
+        pcl.lap(c.rank == 0 ? "global analysis (rank 0)" : "rank 0's global analysis (waiting)");
+        bc.run(an);
+        if (c.rank != 0) an.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        pcl.lap("analysis broadcast from rank 0");
+    }
+    an.input_hash = input_hash(A11, B, C22);
+    return an;
+}
+
 Precond *precond_create_dist(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr &C22, const HCsr *Akry) {
     const bool dev = !c.opts.host_factor;
     // each rank schedules its own subtrees: no schedule of the whole system
-    Precond *pc = precond_create_dist(c, analyze(A11, B, C22, c.opts, dev, {}, false), Akry);
+    Precond *pc = precond_create_dist(c, analyze_dist(c, A11, B, C22, dev), Akry);
     pc->pattern_hash = pattern_hash(A11, B, C22);
     if (dev) pc->dl.kp_from.upload(kp_value_sources(A11, B, C22));
     return pc;

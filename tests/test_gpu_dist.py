@@ -528,6 +528,62 @@ def test_dist_plan_mismatch_fails_on_every_rank(option, value):
     assert _run_ranks(2, work, {option: value}) == [None, None]
 
 
+@pytest.mark.parametrize("P", [2, 4])
+def test_dist_analysis_broadcast_bitexact(P):
+    """The global analysis run once on rank 0 and broadcast (default) against every rank running
+    it on its own (engine option no_bcast_analysis): the same factors and the same applies, bit
+    for bit, and the oracle's; one rank alone asking for its own analysis takes every rank there
+    (and the plan agreement then names it)."""
+    import cpkrylov_amd as cpk
+    S = _system("synthetic20k")
+    z = np.random.default_rng(17).standard_normal(S["n"] + S["m"])
+
+    def work(ctx, r):
+        M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+        M.nitref, M.force_itref = 1, True
+        return M * z, M.export_factors() if r == 0 else None
+
+    res_b = _run_ranks(P, work)
+    res_l = _run_ranks(P, work, {"no_bcast_analysis": 1})
+    L, D, perm = res_b[0][1]
+    L2, D2, perm2 = res_l[0][1]
+    assert np.array_equal(perm, perm2) and np.array_equal(L.data, L2.data) and np.array_equal(D, D2)
+    Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=(L, D, perm))
+    Mo.set(nitref=1.0, force_itref=1.0)
+    yo = Mo @ z
+    for (yb, _), (yl, _) in zip(res_b, res_l):
+        assert np.array_equal(yb, yo) and np.array_equal(yl, yo)
+
+    def work_err(ctx, r):
+        try:
+            cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
+        except cpk.CpkError as e:
+            return str(e)
+        return None
+
+    res = _run_ranks(P, work_err, lambda r: {"no_bcast_analysis": 1} if r == 1 else {})
+    assert all(m is not None and "plan of rank(s) 1 differs" in m for m in res), res
+
+
+def test_dist_inputs_differ_fail_on_every_rank():
+    """With the analysis broadcast from rank 0, a rank given other matrix values than rank 0's
+    would build its plan on rank 0's analysis: every rank hashes its own inputs (pattern and value
+    bits) into the plan agreement, so all of them fail with the same clean error."""
+    import cpkrylov_amd as cpk
+    S = _system("synthetic20k")
+
+    def work(ctx, r):
+        C = S["C"] * (2.0 if r == 1 else 1.0)
+        try:
+            cpk.opLDL2(S["G"], S["B"], -C, ctx=ctx)
+        except cpk.CpkError as e:
+            return str(e)
+        return None
+
+    res = _run_ranks(3, work)
+    assert all(m is not None and "plan of rank(s) 1 differs" in m for m in res), res
+
+
 def _new_values(S, seed):
     """IPM-like new values with the same sparsity: G rescaled, B and C scaled."""
     rng = np.random.default_rng(seed)
