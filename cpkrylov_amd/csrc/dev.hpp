@@ -254,6 +254,8 @@ struct DFactor {
     int64_t bwd_dead_w_rows() const { return pipelined && round0_rows > 0 ? round0_rows : 0; }
     std::vector<int32_t> hmeta;  // host copy of meta
     std::vector<int64_t> hmodel; // the upper blocks' loop-cost model (mark_dataflow; diagnostic)
+    // (first, last) block of a launch -> its blocks' largest rows / entries (the LDS image, kernels.hip)
+    mutable std::map<std::pair<int64_t, int64_t>, std::pair<int, int>> img_cache;
     // round-0 blocks assigned to the persistent launch's workgroups by modelled cost (plan_round0),
     // per kernel variant v (0 forward, 1 forward with the fused refinement residual, 2 backward):
     // workgroup g runs the BlkMeta records ameta[v][aptr[v][g] .. aptr[v][g + 1]); agrid[v] = the

@@ -1445,12 +1445,32 @@ __device__ __forceinline__ void fold_known(SweepLds &S, int nr, int tid) {
     __syncthreads();
 }
 
+// the LDS image of an upper-round launch: rows (the 1.0 slot's index) and entries it holds
+struct Img {
+    int R, CAP;
+};
 // leading outside-term counts of the upper rounds' rows (DFactor::ufold): [2 (row - row0) + bwd]
 struct UFold {
     const int16_t *p = nullptr;
     const int16_t *s = nullptr;  // DFactor::ustep, same layout
     int32_t row0 = 0;
 };
+// the image of a launch over blocks [b0, b1): their largest row count and entry count (either
+// direction), capped by the kernel's R / CAP.  A smaller image than the kernel's maximum lets
+// more workgroups share a CU's LDS (the +-64 window's first upper round: 5 per CU instead of 4)
+static Img launch_img(const DFactor &F, int64_t b0, int64_t b1, int rmax, int capmax) {
+    auto it = F.img_cache.find({b0, b1});
+    if (it == F.img_cache.end()) {
+        int R = 1, CAP = 1;
+        for (int64_t b = b0; b < b1; b++) {
+            const int32_t *m = &F.hmeta[(size_t)b * 8];
+            R = std::max(R, m[1] - m[0]), CAP = std::max({CAP, m[5] - m[4], m[7] - m[6]});
+        }
+        it = F.img_cache.emplace(std::make_pair(b0, b1), std::make_pair(R, CAP)).first;
+    }
+    return Img{std::min(it->second.first, rmax), std::min(it->second.second, capmax)};
+}
+static size_t img_bytes(const Img &g) { return sweep_lds_bytes(g.R, g.CAP); }
 static inline UFold ufold_of(const DFactor &F) {
     return UFold{F.ufold.n ? F.ufold.p : nullptr, F.ustep.n ? F.ustep.p : nullptr, F.urow0};
 }
@@ -1525,8 +1545,7 @@ __device__ __forceinline__ void levels_colsweep(SweepLds &S, int nr, int R, int 
         if (t < nr) S.w[S.lv[t]] = acc[q];
     }
 }
-template <int R>
-__device__ __forceinline__ void colsweep_dispatch(SweepLds &S, int nr, int lane) {
+__device__ __forceinline__ void colsweep_dispatch(SweepLds &S, int nr, int R, int lane) {
     if (nr <= kWave) levels_colsweep<1>(S, nr, R, lane);
     else if (nr <= 2 * kWave) levels_colsweep<2>(S, nr, R, lane);
     else levels_colsweep<4>(S, nr, R, lane);
@@ -2024,8 +2043,10 @@ __device__ __forceinline__ void upper_block(
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
     double *w, double *out, int sched_in, double *ys, double *xs, const PackArgs &pk, const UFold &uf, int64_t b,
-    const Wait &wait = Wait{}) {
-    constexpr int R = RPU * TPB, CAP = EPU * TPB;
+    const Img &img, const Wait &wait = Wait{}) {
+    // the LDS image of this launch (Img: its blocks' largest rows / entries, <= the kernel's R / CAP)
+    constexpr int RMAX = RPU * TPB;
+    const int R = img.R, CAP = img.CAP;
 #ifdef CPK_PIPE_STAMPS
     uint64_t tp = (uint64_t)clock64();
 #else
@@ -2038,6 +2059,7 @@ __device__ __forceinline__ void upper_block(
     // the column sweep for this block and direction (mark_dataflow); it needs the step table
     const bool cs = uf.s != nullptr && (m.l1 & (BWD ? kMetaCsBwd : kMetaCsFwd));
     SweepLds S(smem, R, CAP);
+    (void)CAP;
     uint32_t q[RPU];
     int32_t sp[RPU], fo[RPU], st[RPU];
     double a[RPU], d[RPU];
@@ -2108,9 +2130,9 @@ __device__ __forceinline__ void upper_block(
     // (a single wave's LDS accesses complete in program order) the chain is LDS latency only;
     // narrow levels give each row a lane group (levels_grouped)
     if (tid < kWave) {
-        if (cs) colsweep_dispatch<R>(S, nr, tid);
+        if (cs) colsweep_dispatch(S, nr, R, tid);
         else if (CPK_UPPER_DATAFLOW && (m.l1 & (BWD ? kMetaDfBwd : kMetaDfFwd)))
-            levels_dataflow<BWD, CPK_DF_CH(BWD), true, R / kWave>(S, nr, R, ne, tid);
+            levels_dataflow<BWD, CPK_DF_CH(BWD), true, RMAX / kWave>(S, nr, R, ne, tid);
         else if (CPK_UPPER_GROUP(BWD)) levels_grouped<CPK_UPPER_CH(BWD), BWD, true>(S, nl, false, tid);
         else sweep_levels<kWave, BWD, true, CPK_UPPER_CH(BWD), true, true>(S, nl, false, tid);
     }
@@ -2146,11 +2168,11 @@ __global__ __launch_bounds__(TPB) void sptrsv_upper_kernel(
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
     double *w, double *out, const int *run, const int *active, int sched_in, double *ys, double *xs, PackArgs pk,
-    UFold uf) {
+    UFold uf, Img img) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
     upper_block<TPB, RPU, EPU, BWD, ADD>(smem, meta[blk0 + blockIdx.x], lvl_row, ptr, col, val, D, perm, xin, neg_from,
-                                         w, out, sched_in, ys, xs, pk, uf, blk0 + blockIdx.x);
+                                         w, out, sched_in, ys, xs, pk, uf, blk0 + blockIdx.x, img);
 }
 
 // The last round's forward and backward sweeps in one launch (single GPU).  The sweeps meet at
@@ -2167,13 +2189,16 @@ __device__ __forceinline__ void last_block(
     const uint32_t *__restrict__ fptr, const int32_t *__restrict__ fcol, const double *__restrict__ fval,
     const uint32_t *__restrict__ bptr, const int32_t *__restrict__ bcol, const double *__restrict__ bval,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
-    int sched_in, double *xs, double *w, double *out, double *ys, const UFold &uf, const Wait &wait = Wait{}) {
-    constexpr int R = RPU * TPB, CAP = EPU * TPB;
+    int sched_in, double *xs, double *w, double *out, double *ys, const UFold &uf, const Img &img,
+    const Wait &wait = Wait{}) {
+    constexpr int RMAX = RPU * TPB;
+    const int R = img.R, CAP = img.CAP;
     const int r0 = m.r0, r1 = m.r1, nr = r1 - r0, nl = (m.l1 & kMetaL1Mask) - m.l0;
     const int nef = m.fe1 - m.fe0, neb = m.be1 - m.be0;
     const int tid = threadIdx.x;
     const bool csf = uf.s != nullptr && (m.l1 & kMetaCsFwd), csb = uf.s != nullptr && (m.l1 & kMetaCsBwd);
     SweepLds S(smem, R, CAP);
+    (void)CAP;
     uint32_t qf[RPU], qb[RPU];
     int32_t sp[RPU], dp[RPU], fof[RPU], fob[RPU], stf[RPU], stb[RPU];
     double a[RPU], d[RPU];
@@ -2242,8 +2267,8 @@ __device__ __forceinline__ void last_block(
     if (uf.p) fold_known<TPB>(S, nr, tid);
     else fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (csf) colsweep_dispatch<R>(S, nr, tid);
-        else if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd)) levels_dataflow<false, CPK_DF_CH(false), true, R / kWave>(S, nr, R, nef, tid);
+        if (csf) colsweep_dispatch(S, nr, R, tid);
+        else if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd)) levels_dataflow<false, CPK_DF_CH(false), true, RMAX / kWave>(S, nr, R, nef, tid);
         else if (CPK_UPPER_GROUP(false)) levels_grouped<CPK_UPPER_CH(false), false, true>(S, nl, false, tid);
         else sweep_levels<kWave, false, true, CPK_UPPER_CH(false), true, true>(S, nl, false, tid);
     }
@@ -2280,8 +2305,8 @@ __device__ __forceinline__ void last_block(
     if (uf.p) fold_known<TPB>(S, nr, tid);
     else fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (csb) colsweep_dispatch<R>(S, nr, tid);
-        else if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfBwd)) levels_dataflow<true, CPK_DF_CH(true), true, R / kWave>(S, nr, R, neb, tid);
+        if (csb) colsweep_dispatch(S, nr, R, tid);
+        else if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfBwd)) levels_dataflow<true, CPK_DF_CH(true), true, RMAX / kWave>(S, nr, R, neb, tid);
         else if (CPK_UPPER_GROUP(true)) levels_grouped<CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
         else sweep_levels<kWave, true, true, CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
     }
@@ -2304,11 +2329,12 @@ __global__ __launch_bounds__(TPB) void sptrsv_last_kernel(
     const uint32_t *__restrict__ fptr, const int32_t *__restrict__ fcol, const double *__restrict__ fval,
     const uint32_t *__restrict__ bptr, const int32_t *__restrict__ bcol, const double *__restrict__ bval,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
-    int sched_in, double *xs, double *w, double *out, const int *run, const int *active, double *ys, UFold uf) {
+    int sched_in, double *xs, double *w, double *out, const int *run, const int *active, double *ys, UFold uf,
+    Img img) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip(run, active)) return;
     last_block<TPB, RPU, EPU, ADD>(smem, meta[blk0 + blockIdx.x], lvl_row, fptr, fcol, fval, bptr, bcol, bval, D, perm,
-                                   xin, neg_from, sched_in, xs, w, out, ys, uf);
+                                   xin, neg_from, sched_in, xs, w, out, ys, uf, img);
 }
 
 // the last round fused (fwd + bwd) when it is an upper round whose blocks fit sptrsv_last_kernel
@@ -2326,6 +2352,7 @@ static void launch_last(Ctx &c, const DFactor &F, const FwdIn &in, double *w, do
     const int64_t b0 = F.round_ptr[R - 1], nb = F.round_ptr[R] - b0;
     if (!nb) return;
     const size_t lds = sweep_lds_bytes(RPU * TPB, EPU * TPB);
+    const Img img{RPU * TPB, EPU * TPB};
     static const bool lds_ok = lds <= 64 * 1024 ||
         (hipFuncSetAttribute((const void *)sptrsv_last_kernel<TPB, RPU, EPU, false>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
@@ -2334,13 +2361,13 @@ static void launch_last(Ctx &c, const DFactor &F, const FwdIn &in, double *w, do
     if (!lds_ok) throw Error(CPK_ERR_HIP, "sptrsv_last_kernel: LDS image not admitted");
     const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
     if (add)
-        hipLaunchKernelGGL((sptrsv_last_kernel<TPB, RPU, EPU, true>), dim3((unsigned)nb), dim3(TPB), lds, c.stream, b0,
+        hipLaunchKernelGGL((sptrsv_last_kernel<TPB, RPU, EPU, true>), dim3((unsigned)nb), dim3(TPB), img_bytes(img), c.stream, b0,
                            meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p,
-                           in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, ufold_of(F));
+                           in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, ufold_of(F), img);
     else
-        hipLaunchKernelGGL((sptrsv_last_kernel<TPB, RPU, EPU, false>), dim3((unsigned)nb), dim3(TPB), lds, c.stream, b0,
+        hipLaunchKernelGGL((sptrsv_last_kernel<TPB, RPU, EPU, false>), dim3((unsigned)nb), dim3(TPB), img_bytes(img), c.stream, b0,
                            meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p,
-                           in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, ufold_of(F));
+                           in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, ufold_of(F), img);
     CPK_HIP(hipGetLastError());
 }
 
@@ -2383,7 +2410,7 @@ __global__ __launch_bounds__(TPB) void sptrsv_chain_kernel(
     const uint32_t *__restrict__ bptr, const int32_t *__restrict__ bcol, const double *__restrict__ bval,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
     int sched_in, double *xs, double *w, double *out, const int *run, const int *active, double *ys, PackArgs pk,
-    UFold uf) {
+    UFold uf, Img img) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ uint32_t s_epoch;
     if (skip(run, active)) return;
@@ -2417,13 +2444,13 @@ __global__ __launch_bounds__(TPB) void sptrsv_chain_kernel(
     };
     if (kind == 0)
         upper_block<TPB, RPU, EPU, false, false, true>(smem, meta[b], lvl_row, fptr, fcol, fval, D, perm, xin, neg_from, w,
-                                                       nullptr, sched_in, nullptr, xs, pk, uf, b, wait);
+                                                       nullptr, sched_in, nullptr, xs, pk, uf, b, img, wait);
     else if (kind == 1)
         last_block<TPB, RPU, EPU, ADD, true>(smem, meta[b], lvl_row, fptr, fcol, fval, bptr, bcol, bval, D, perm, xin,
-                                             neg_from, sched_in, xs, w, out, ys, uf, wait);
+                                             neg_from, sched_in, xs, w, out, ys, uf, img, wait);
     else
         upper_block<TPB, RPU, EPU, true, ADD, true>(smem, meta[b], lvl_row, bptr, bcol, bval, D, perm, nullptr, 0, w, out,
-                                                    0, ys, nullptr, pk, uf, b, wait);
+                                                    0, ys, nullptr, pk, uf, b, img, wait);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w stores done
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2547,15 +2574,16 @@ static void launch_chain_t(Ctx &c, const DFactor &F, int kind, const FwdIn &in, 
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess);
     if (!lds_ok) throw Error(CPK_ERR_HIP, "sptrsv_chain_kernel: LDS image not admitted");
     const ChainArgs ch{h.task.p, h.dptr.p, h.didx.p, h.flag.p, h.ctrl.p, (int)h.ntask};
+    const Img img{RPU * TPB, EPU * TPB};  // narrow rounds: every task resident at the kernel's image
     const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
     if (add)
-        hipLaunchKernelGGL((sptrsv_chain_kernel<TPB, RPU, EPU, true>), dim3((unsigned)h.ntask), dim3(TPB), lds, c.stream,
+        hipLaunchKernelGGL((sptrsv_chain_kernel<TPB, RPU, EPU, true>), dim3((unsigned)h.ntask), dim3(TPB), img_bytes(img), c.stream,
                            ch, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
-                           F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, pk, ufold_of(F));
+                           F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, pk, ufold_of(F), img);
     else
-        hipLaunchKernelGGL((sptrsv_chain_kernel<TPB, RPU, EPU, false>), dim3((unsigned)h.ntask), dim3(TPB), lds,
+        hipLaunchKernelGGL((sptrsv_chain_kernel<TPB, RPU, EPU, false>), dim3((unsigned)h.ntask), dim3(TPB), img_bytes(img),
                            c.stream, ch, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p,
-                           F.D.p, F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, pk, ufold_of(F));
+                           F.D.p, F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, pk, ufold_of(F), img);
     CPK_HIP(hipGetLastError());
 }
 static void launch_chain(Ctx &c, const DFactor &F, int kind, const FwdIn &in, double *w, double *out, bool add,
@@ -2595,18 +2623,30 @@ static bool upper_round_t(Ctx &c, const DFactor &F, int64_t r, bool bwd, bool ad
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess);
     if (!lds_ok) return false;
     const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
+    // the round's own image only where it raises residency for a round that needs it: a round of
+    // at most (kernel-image blocks per CU) x CUs workgroups is resident at once already, and a
+    // smaller image would let some CUs take more of its blocks than others (S10's first upper
+    // round, 1024 blocks: 4 per CU on every CU, or 5 on some and 3 on others)
+    static const int64_t resident = [] {
+        int cus = 256, dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return (int64_t)cus * (int64_t)std::max<size_t>(1, (160 * 1024) / sweep_lds_bytes(RPU * TPB, EPU * TPB));
+    }();
+    const Img img = nb > resident ? launch_img(F, b0, b0 + nb, RPU * TPB, EPU * TPB) : Img{RPU * TPB, EPU * TPB};
+    const size_t ldsr = img_bytes(img);
     if (!bwd)
-        hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, false, false>), dim3((unsigned)nb), dim3(TPB), lds,
+        hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, false, false>), dim3((unsigned)nb), dim3(TPB), ldsr,
                            c.stream, b0, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active, sched_in, ys, xs, pk, ufold_of(F));
+                           neg_from, w, out, run, active, sched_in, ys, xs, pk, ufold_of(F), img);
     else if (add)
-        hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, true>), dim3((unsigned)nb), dim3(TPB), lds,
+        hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, true>), dim3((unsigned)nb), dim3(TPB), ldsr,
                            c.stream, b0, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active, sched_in, ys, xs, pk, ufold_of(F));
+                           neg_from, w, out, run, active, sched_in, ys, xs, pk, ufold_of(F), img);
     else
-        hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, false>), dim3((unsigned)nb), dim3(TPB), lds,
+        hipLaunchKernelGGL((sptrsv_upper_kernel<TPB, RPU, EPU, true, false>), dim3((unsigned)nb), dim3(TPB), ldsr,
                            c.stream, b0, meta, F.lvl_row.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p, F.perm.p, xin,
-                           neg_from, w, out, run, active, sched_in, ys, xs, pk, ufold_of(F));
+                           neg_from, w, out, run, active, sched_in, ys, xs, pk, ufold_of(F), img);
     return true;
 }
 
