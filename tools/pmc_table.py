@@ -18,6 +18,7 @@ import sys
 # sptrsv_pipe_kernel<TPB, RPT, EPT, BWD, ADD, SPLIT, LOC, RES>, sptrsv_upper_kernel<TPB, RPU, EPU, BWD, ADD>
 PIPE = re.compile(r"sptrsv_pipe_kernel<(\d+), (\d+), (\d+), (\w+), (\w+), (\d+), (\w+), (\w+)>")
 UPPER = re.compile(r"sptrsv_upper_kernel<(\d+), (\d+), (\d+), (\w+), (\w+)>")
+CHAIN = re.compile(r"sptrsv_chain_kernel<(\d+), (\d+), (\d+), (\w+)>")
 
 
 def label(name):
@@ -30,6 +31,9 @@ def label(name):
     if m:
         bwd, add = m.group(4) == "true", m.group(5) == "true"
         return f"upper {'bwd' if bwd else 'fwd'}{' +add' if add else ''} <{m.group(1)},{m.group(2)},{m.group(3)}>"
+    m = CHAIN.search(name)
+    if m:
+        return f"chain{' +add' if m.group(4) == 'true' else ''} <{m.group(1)},{m.group(2)},{m.group(3)}>"
     return re.sub(r"\(.*", "", name).replace("cpk::", "").replace("(anonymous namespace)::", "")[:48]
 
 
