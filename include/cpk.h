@@ -135,7 +135,9 @@ int cpk_ctx_create_sim(int device, cpk_simgroup group, int rank, int nranks, cpk
  * once at creation; a change applies to preconditioners and solves created afterwards.
  * Names: sweep ("rows,cap,threads[,rows,cap,threads[,sub0]]"; unset, each path has its own
  * default: a distributed context reports and uses the distributed one), split_tol, host_factor,
- * no_pipe, no_upper, no_col16, no_dataflow, all_dataflow, no_colsweep, all_colsweep, no_chain, exact_dots,
+ * no_pipe, no_upper, no_col16, no_dataflow, all_dataflow, no_colsweep, all_colsweep, no_chain, chain_wide
+ * (rounds of at most this many blocks join the sweep chain, default 256), exact_dots, no_bcast_analysis
+ * (every rank of a distributed preconditioner runs the global analysis instead of receiving rank 0's),
  * no_sched_resid, no_fused_resid, r0_xcd_chunk, tsolve_global, tsolve_sweep,
  * no_piggy, no_halo_merge, no_graph, no_fuse_last, no_tkr, no_minres_fuse, dist_graph, batch,
  * dist1 (a 1-rank communicator runs the distributed kernels; set before building operators),
