@@ -2387,6 +2387,17 @@ static void launch_last(Ctx &c, const DFactor &F, const FwdIn &in, double *w, do
 // the epoch.  Every spin is bounded: a wait that outlives kChainSpinCap sets the error word, every
 // other waiter then gives up, and the host raises CPK_ERR_HIP (check_chain).
 constexpr uint32_t kChainSpinCap = 1u << 20;
+// polling back-off of a waiting task: CPK_CHAIN_FAST_POLLS polls s_sleep CPK_CHAIN_SLEEP0 apart,
+// then CPK_CHAIN_SLEEP1 (units of 64 cycles)
+#ifndef CPK_CHAIN_FAST_POLLS
+#define CPK_CHAIN_FAST_POLLS 16
+#endif
+#ifndef CPK_CHAIN_SLEEP0
+#define CPK_CHAIN_SLEEP0 2
+#endif
+#ifndef CPK_CHAIN_SLEEP1
+#define CPK_CHAIN_SLEEP1 16
+#endif
 // the rounds a chain covers: the narrow top of the tree (rounds of at most chain_wide blocks,
 // and at least two of them).  A wide round's blocks are all ready at once -- a launch of their
 // own costs nothing there -- and in a chain hundreds of its blocks would sit polling the few
@@ -2436,8 +2447,8 @@ __global__ __launch_bounds__(TPB) void sptrsv_chain_kernel(
                     break;
                 }
                 // back off: a few quick polls, then ~1000 cycles apart (poll traffic stays low)
-                if (spins < 16) __builtin_amdgcn_s_sleep(2);
-                else __builtin_amdgcn_s_sleep(16);
+                if (spins < CPK_CHAIN_FAST_POLLS) __builtin_amdgcn_s_sleep(CPK_CHAIN_SLEEP0);
+                else __builtin_amdgcn_s_sleep(CPK_CHAIN_SLEEP1);
             }
         }
         __syncthreads();
