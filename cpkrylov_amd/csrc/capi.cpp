@@ -444,8 +444,9 @@ int cpk_pc_apply(cpk_pc M, const double *x, double *y) {
     } else {
         CPK_HIP(hipMemcpyAsync(y, dy.p, p.N * sizeof(double), hipMemcpyDeviceToHost, c.stream));
         CPK_HIP(hipStreamSynchronize(c.stream));
-        check_chain(p.dF);
     }
+    check_chain(p.dF);
+    check_chain(p.sep.tsw);
     API_END
 }
 

@@ -1220,6 +1220,10 @@ void dsep_sweep_setup(Ctx &c, DSep &T, const RankPlan &rp, int P) {
     d.round_ptr = S.round_ptr;
     d.round0_rows = -1;
     plan_round0(c, d, nullptr);
+    // the T sweep's upper rounds as sweep chains (forward, backward): on the +-64 window at P = 8
+    // T is 6128 rows in 8 rounds, 14 upper-round launches per T solve
+    d.no_chain = c.opts.no_chain, d.chain_wide = c.opts.chain_wide;
+    build_chain(d, meta, fptr, fcol, bptr, bcol);
     T.tsw_q.upload(q);
     T.tsw_base = base;
     T.tsweep = true;
@@ -2551,7 +2555,7 @@ static void build_chain(DFactor &d, const std::vector<int32_t> &meta, const std:
                         const std::vector<int32_t> &bcol) {
     for (DChain &c : d.chain) c.ntask = 0;
     const int64_t R = (int64_t)d.round_ptr.size() - 1;
-    if (d.no_chain || d.no_upper || R < 3 || d.round0_rows < 0 || !chain_tpb(d)) return;
+    if (d.no_chain || d.no_upper || R < 3 || !chain_tpb(d)) return;
     // the chained rounds: the narrow top [first, R), two rounds at least, every one through the
     // block kernel
     int64_t first = R;

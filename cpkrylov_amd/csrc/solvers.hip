@@ -2097,6 +2097,7 @@ void method_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, 
     CPK_HIP(hipEventRecord(c.ev1, c.stream));
     CPK_HIP(hipEventSynchronize(c.ev1));
     check_chain(M.dF);
+    check_chain(M.sep.tsw);
     if (stats) {
         float ms = 0;
         CPK_HIP(hipEventElapsedTime(&ms, c.ev0, c.ev1));
