@@ -228,6 +228,11 @@ struct DFactor {
     DBuf<int16_t> ufold;
     DBuf<int16_t> ustep;  // the row's step in its block's column sweep, same layout
     int32_t urow0 = 0;
+    // the column sweep's staged column of every entry of the upper rounds' rows, per direction
+    // (kernels.hip kCsOut / kCsStep): in-block, the column's step | the run of outside entries
+    // behind it << 8; outside, kCsOut.  ucode[dir][e - ucode0[dir]] for entry e of fcol / bcol
+    DBuf<int16_t> ucode[2];
+    uint32_t ucode0[2] = {0, 0};
     DBuf<int16_t> fcol16;  // round 0 when every forward entry is local: column - block's first row (else empty)
     int64_t nnz16 = 0;     // forward entries stored in fcol16 (10 bytes each instead of 12)
     DBuf<double> fval;
@@ -275,7 +280,7 @@ struct DFactor {
     std::vector<char> round_fits;    // host: every block of round r fits (sweep_rows[1], sweep_cap[1])
     int sweep_rows[2] = {192, 1024}, sweep_cap[2] = {576, 4096}, sweep_threads[2] = {64, 512};  // round 0 / rest
     size_t bytes() const {
-        return fptr.bytes() + fcol.bytes() + fcol16.bytes() + ufold.bytes() + ustep.bytes() + fval.bytes() + bptr.bytes() + bcol.bytes() + bval.bytes() + D.bytes() +
+        return fptr.bytes() + fcol.bytes() + fcol16.bytes() + ufold.bytes() + ustep.bytes() + ucode[0].bytes() + ucode[1].bytes() + fval.bytes() + bptr.bytes() + bcol.bytes() + bval.bytes() + D.bytes() +
                perm.bytes() + blk_lvl.bytes() + lvl_row.bytes() + meta.bytes();
     }
 };
@@ -480,7 +485,7 @@ constexpr int64_t kSepPiggy = 2;  // spare payload slots per rank in the separat
 // an upper-round block (mark_dataflow, kernels.hip); every reader of l1 masks them off
 constexpr int kBlockModelW = 8;  // fields per (upper block, direction) of DFactor::hmodel
 constexpr int32_t kMetaDfFwd = 1 << 30, kMetaDfBwd = 1 << 29, kMetaCsFwd = 1 << 28, kMetaCsBwd = 1 << 27,
-                  kMetaL1Mask = (1 << 27) - 1;
+                  kMetaCoFwd = 1 << 26, kMetaCoBwd = 1 << 25, kMetaL1Mask = (1 << 25) - 1;
 constexpr int64_t kKrylovSpare = 2;
 struct DSep {
     int64_t nT = 0, kt = 0, nlev = 0, nsend = 0, ntdof = 0;

@@ -120,12 +120,15 @@ constexpr double kDataflowTripCost = 1.0;
 // the column sweep (levels_colsweep): blocks of at most 256 rows (4 per lane).  The choice
 // against the other loops is made in cycles, fitted on the stamps build over every upper block of
 // the +-64 window and S10 with the column sweep forced on and off (tools/upper_cycles.py BLOCKS=,
-// profiles/r05_colsweep_calibration.txt): a step costs ~430 / 520 / 610 cycles at 1 / 2 / 3 rows
-// per lane, an outside term behind an in-block one ~40-70 more; a level-loop trip ~300 cycles, a
-// dataflow trip ~220
+// profiles/r05_colsweep_calibration.txt): cycles per step at 1 / 2 / 3 / 4 rows per lane; a
+// level-loop trip ~300 cycles, a dataflow trip ~220
 constexpr int kColsweepMaxRows = 4 * 64;
-constexpr double kColsweepStepCycles[4] = {430.0, 520.0, 610.0, 700.0};
-constexpr double kColsweepOutCycles = 50.0;
+constexpr double kColsweepStepCycles[4] = {150.0, 200.0, 280.0, 360.0};
+// the column sweep's staged columns (DFactor::ucode): an in-block entry holds its column's step |
+// the run of outside entries behind it (up to the next in-block entry or the row's end) << 8, an
+// outside entry kCsOut
+constexpr int kCsOut = 0x8000, kCsStep = 0x80ff, kCsRunMax = 127;
+constexpr double kColsweepDrainCycles[4] = {150.0, 250.0, 350.0, 450.0};  // a drain trip (four terms a row)
 constexpr double kLevelTripCycles = 300.0, kDataflowTripCycles = 220.0;
 #ifndef CPK_UPPER_DATAFLOW
 #define CPK_UPPER_DATAFLOW 1
@@ -212,13 +215,16 @@ static std::vector<int16_t> build_ufold(DFactor &d, const std::vector<int32_t> &
                         const std::vector<uint32_t> &bptr, const std::vector<int32_t> &bcol, const Key &key) {
     d.ufold.release();
     d.ustep.release();
-    d.urow0 = 0;
+    d.ucode[0].release(), d.ucode[1].release();
+    d.urow0 = 0, d.ucode0[0] = d.ucode0[1] = 0;
     if (round_ptr.size() < 3) return {};
     const int64_t ub0 = round_ptr[1], ub1 = round_ptr.back();
     int64_t lo = INT64_MAX, hi = 0;
     for (int64_t b = ub0; b < ub1; b++) lo = std::min<int64_t>(lo, meta[(size_t)b * 8]), hi = std::max<int64_t>(hi, meta[(size_t)b * 8 + 1]);
     if (lo >= hi) return {};
     std::vector<int16_t> uf((size_t)(2 * (hi - lo)), 0), us((size_t)(2 * (hi - lo)), 0);
+    std::vector<int16_t> code[2] = {std::vector<int16_t>((size_t)(fptr[hi] - fptr[lo]), 0),
+                                    std::vector<int16_t>((size_t)(bptr[hi] - bptr[lo]), 0)};
     parallel_for(ub1 - ub0, [&](int64_t a, int64_t z) {
         std::vector<std::pair<int64_t, int32_t>> order;
         for (int64_t b = ub0 + a; b < ub0 + z; b++) {
@@ -240,11 +246,33 @@ static std::vector<int16_t> build_ufold(DFactor &d, const std::vector<int32_t> &
                 const int32_t i = order[(size_t)t].second;
                 us[(size_t)(2 * (i - lo))] = (int16_t)t, us[(size_t)(2 * (i - lo) + 1)] = (int16_t)(nr - 1 - t);
             }
+            if (nr > kColsweepMaxRows) continue;
+            // staged columns of the column sweep: in-block steps with the outside run behind each
+            for (int32_t i = r0; i < r1; i++)
+                for (int dir = 0; dir < 2; dir++) {
+                    const std::vector<uint32_t> &ptr = dir ? bptr : fptr;
+                    const std::vector<int32_t> &col = dir ? bcol : fcol;
+                    int16_t *cd = code[dir].data() - (dir ? bptr[lo] : fptr[lo]);
+                    int64_t last = -1;
+                    int run = 0;
+                    for (uint32_t e = ptr[i]; e < ptr[i + 1]; e++) {
+                        const int32_t c = col[e];
+                        if (c >= r0 && c < r1) {
+                            if (last >= 0) cd[last] = (int16_t)(cd[last] | (std::min(run, kCsRunMax) << 8));
+                            cd[e] = us[(size_t)(2 * (c - lo) + dir)], last = e, run = 0;
+                        } else {
+                            cd[e] = (int16_t)kCsOut, run += last >= 0;
+                        }
+                    }
+                    if (last >= 0) cd[last] = (int16_t)(cd[last] | (std::min(run, kCsRunMax) << 8));
+                }
         }
     }, 64);
     d.urow0 = (int32_t)lo;
     d.ufold.upload(uf);
     d.ustep.upload(us);
+    d.ucode[0].upload(code[0]), d.ucode[1].upload(code[1]);
+    d.ucode0[0] = fptr[lo], d.ucode0[1] = bptr[lo];
     return us;
 }
 void mark_dataflow(std::vector<int32_t> &meta, const std::vector<int64_t> &round_ptr, const std::vector<uint32_t> &fptr,
@@ -305,26 +333,44 @@ void mark_dataflow(std::vector<int32_t> &meta, const std::vector<int64_t> &round
                 // with the rows each lane holds; outside terms behind in-block ones add a pass each
                 // valid only if every row meets its in-block terms at increasing steps, all before
                 // its own (the steps follow the entries' key order; checked, not assumed)
-                bool cs = false, cs_valid = cs_mode != 1 && nr <= kColsweepMaxRows && !ustep.empty();
+                // valid only if the kernel's schedule takes every term of every row before the
+                // row's own step, one term per step: an in-block term at its column's step, an
+                // outside term at the first step after the row's previous term (the steps follow
+                // the entries' key order; checked, not assumed)
+                // Without drains (one term per step) it needs every outside term to find a free
+                // step before the row's next in-block term and its own step; with drains it needs
+                // the in-block terms at increasing steps before the row's own, and costs a drain
+                // trip per step and outside term behind that step's in-block ones (the longest run)
+                bool cs = false, drain = false, cs_valid = cs_mode != 1 && nr <= kColsweepMaxRows && !ustep.empty();
                 auto step = [&](int k) { return (int)ustep[(size_t)(2 * (r0 + k - urow0) + dir)]; };
+                std::vector<int> run(cs_valid ? (size_t)nr : 0, 0);  // per step: longest outside run behind it
+                int maxrun = 0;
                 for (int k = 0; k < nr && cs_valid; k++) {
-                    int prev = -1;
-                    for (int c : terms[k])
-                        if (c >= 0) {
+                    int t = 0, prev = -1, out = 0;  // t: the first step free for the row's next term
+                    for (int c : terms[k]) {
+                        if (c < 0) {
+                            t++, out++;
+                            if (prev >= 0) run[(size_t)prev] = std::max(run[(size_t)prev], out);
+                            maxrun = std::max(maxrun, out);
+                        } else {
                             cs_valid = cs_valid && step(c) > prev && step(c) < step(k);
-                            prev = step(c);
+                            drain = drain || step(c) < t;
+                            t = step(c) + 1, prev = step(c), out = 0;
                         }
+                    }
+                    drain = drain || t > step(k);
                 }
+                cs_valid = cs_valid && !(drain && maxrun > 127);  // kCsRunMax: a run's length in its staged column
                 if (cs_valid) {
-                    int64_t outs = 0;
-                    for (int k = 0; k < nr; k++)
-                        for (int c : terms[k]) outs += c < 0;
-                    const int rpl = (nr + kWave - 1) / kWave;
-                    const double ct = (double)nr * kColsweepStepCycles[std::min(rpl, 4) - 1] + kColsweepOutCycles * (double)outs;
+                    const int rpl = std::min((nr + kWave - 1) / kWave, 4);
+                    int64_t trips = 0;  // drain trips: four terms of every row's run per trip
+                    if (drain)
+                        for (int x : run) trips += (x + 3) / 4;
+                    const double ct = (double)nr * kColsweepStepCycles[rpl - 1] + (double)trips * kColsweepDrainCycles[rpl - 1];
                     const double base = df ? kDataflowTripCycles * (double)dt : kLevelTripCycles * (double)lt;
                     cs = cs_mode == 2 || ct < base;
                 }
-                if (cs) m[3] |= dir ? kMetaCsBwd : kMetaCsFwd;
+                if (cs) m[3] |= (dir ? kMetaCsBwd : kMetaCsFwd) | (drain ? (dir ? kMetaCoBwd : kMetaCoFwd) : 0);
                 else if (df) m[3] |= dir ? kMetaDfBwd : kMetaDfFwd;
                 if (model) {
                     int64_t *o = &(*model)[(size_t)(((b - b0) * 2 + dir) * kBlockModelW)];
@@ -332,7 +378,7 @@ void mark_dataflow(std::vector<int32_t> &meta, const std::vector<int64_t> &round
                     for (int k = 0; k < nr; k++)
                         for (int c : terms[k]) outs += c < 0;
                     o[0] = b, o[1] = dir, o[2] = nr, o[3] = lt, o[4] = df_on ? dt : -1, o[5] = outs, o[6] = cs_valid,
-                    o[7] = cs ? 2 : (df ? 1 : 0);
+                    o[7] = cs ? (drain ? 3 : 2) : (df ? 1 : 0);
                 }
             }
         }
@@ -1458,6 +1504,8 @@ struct UFold {
     const int16_t *p = nullptr;
     const int16_t *s = nullptr;  // DFactor::ustep, same layout
     int32_t row0 = 0;
+    const int16_t *cf = nullptr, *cb = nullptr;  // DFactor::ucode, forward / backward
+    uint32_t cf0 = 0, cb0 = 0;
 };
 // the image of a launch over blocks [b0, b1): their largest row count and entry count (either
 // direction), capped by the kernel's R / CAP.  A smaller image than the kernel's maximum lets
@@ -1476,83 +1524,132 @@ static Img launch_img(const DFactor &F, int64_t b0, int64_t b1, int rmax, int ca
 }
 static size_t img_bytes(const Img &g) { return sweep_lds_bytes(g.R, g.CAP); }
 static inline UFold ufold_of(const DFactor &F) {
-    return UFold{F.ufold.n ? F.ufold.p : nullptr, F.ustep.n ? F.ustep.p : nullptr, F.urow0};
+    const bool cs = F.ustep.n && F.ucode[0].n && F.ucode[1].n;
+    return UFold{F.ufold.n ? F.ufold.p : nullptr, cs ? F.ustep.p : nullptr, F.urow0, cs ? F.ucode[0].p : nullptr,
+                 cs ? F.ucode[1].p : nullptr, F.ucode0[0], F.ucode0[1]};
 }
 
 // The column sweep (one wave; forward and backward alike): the block's rows in the order of
 // their keys -- step t solves the row of step t, and since every row's entries are stored in key
 // order (forward ascending, backward descending), each row meets its in-block terms at
-// increasing steps, all before its own (mark_dataflow checks this per block).  Lane L holds the
-// rows of steps L, L + 64, ... (RPL per lane) with their accumulators in registers.  Step t
-// broadcasts the finished value of its row from the owning lane (v_readlane, no LDS), and every
-// lane whose row's next term is column t subtracts it, then takes the outside terms (staged
-// products, 1.0 slot) that follow it in the row.  A dense chain (a separator clique: a level per
-// row) costs a step per row instead of a level-loop or dataflow trip per row.  Staged for it:
-// lv[t] = the local row of step t, c[e] = the step of an in-block column (R: outside).  Each row
-// keeps its next two terms in registers, so a refill's LDS latency is off the chain.
-// Same terms, same order, not-taken terms subtract +0.0 (an exact no-op): bit-identical.
+// increasing steps, all before its own.  Lane L holds the rows of steps L, L + 64, ... (RPL per
+// lane) with their accumulators in registers.  Step t broadcasts the finished value of its row
+// from the owning lane (v_readlane, no LDS), and every row takes at most ONE term per step: its
+// next term if that is column t, or if it is an outside term (a staged product against the 1.0
+// slot: column R), which any step may take.  So a step has no branches and no data-dependent
+// register shifts: per row a compare, a select, a multiply-subtract and the load of the row's next
+// entry, whose LDS latency the next step's broadcast and the other rows cover.  mark_dataflow
+// checks per block that this schedule is complete -- every in-block term found at its own step,
+// every outside term behind it taken before the row's next in-block term and before the row's own
+// step -- and keeps the other loops for a block that fails.  A dense chain (a separator clique: a
+// level per row) costs a step per row instead of a level-loop or dataflow trip per row.  Staged
+// for it: lv[t] = the local row of step t, c[e] = the step of an in-block column (R: outside).
+// DRAIN (blocks whose rows hold outside terms between in-block ones that the steps cannot absorb
+// one at a time -- the +-64 window's forward separator rows): a row takes only in-block terms at
+// the steps, and right after one it takes the run of outside terms behind it.  The run's length
+// is in the in-block entry's staged column (DFactor::ucode, counted at layout), so a drain issues
+// its values' loads four at a time, with no LDS round trip per term.
+// Same terms, same order; an outside term subtracts v * 1.0 = v: bit-identical.
 __device__ __forceinline__ double lane_bcast(double v, int lane) {  // lane: wave-uniform
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
     return __hiloint2double(hi, lo);
 }
+// the sweep's per-row state (registers): accumulator, next entry (staged column c, value v), its
+// index e and the row's end e1
 template <int RPL>
-__device__ __forceinline__ void levels_colsweep(SweepLds &S, int nr, int R, int lane) {
-    // per row: the next two terms' staged columns (a step, or R: outside) and values, raw -- a
-    // refill is not looked at before the step after next, so its LDS latency stays off the chain
-    double acc[RPL], v0[RPL], v1[RPL];
-    int e[RPL], e1[RPL], c0[RPL], c1[RPL];
+struct ColState {
+    double acc[RPL], v[RPL];
+    int e[RPL], e1[RPL], c[RPL], k[RPL];
+};
+// the outside runs behind this step's in-block terms (k[q] terms of row q >= Q0), four loads per
+// row in flight per trip, subtracted in the row's order
+template <int Q, int RPL>
+__device__ __forceinline__ void colsweep_run_chunk(ColState<RPL> &st, const SweepLds &S, int j0) {
+    if constexpr (Q < RPL) {
+        double u[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) u[i] = S.v[j0 + i < st.k[Q] ? st.e[Q] + j0 + i : st.e[Q]];
+#pragma unroll
+        for (int i = 0; i < 4; i++) st.acc[Q] = j0 + i < st.k[Q] ? st.acc[Q] - u[i] : st.acc[Q];
+    }
+}
+template <int Q0, int RPL>
+__device__ __forceinline__ void colsweep_drain(ColState<RPL> &st, const SweepLds &S) {
+    static_assert(RPL <= 4, "four rows per lane at most");
+    int km = 0;
+#pragma unroll
+    for (int q = Q0; q < RPL; q++) km = max(km, st.k[q]);
+    // (a #pragma unroll loop over the rows inside the trip loop is not unrolled by this compiler)
+    for (int j0 = 0; __any(j0 < km); j0 += 4) {
+        colsweep_run_chunk<Q0, RPL>(st, S, j0);
+        colsweep_run_chunk<Q0 + 1, RPL>(st, S, j0);
+        colsweep_run_chunk<Q0 + 2, RPL>(st, S, j0);
+        colsweep_run_chunk<Q0 + 3, RPL>(st, S, j0);
+    }
+#pragma unroll
+    for (int q = Q0; q < RPL; q++) {
+        st.e[q] += st.k[q];
+        st.c[q] = (uint16_t)S.c[st.e[q]], st.v[q] = S.v[st.e[q]];
+    }
+}
+// steps Q * 64 .. (the rows lane + Q * 64 broadcast), rows q >= Q taking terms
+template <int Q, int RPL, bool DRAIN>
+__device__ __forceinline__ void colsweep_steps(ColState<RPL> &st, const SweepLds &S, int nr) {
+    if constexpr (Q < RPL) {
+        const int jn = min(kWave, nr - Q * kWave);
+        for (int jj = 0; jj < jn; jj++) {
+            const int t = Q * kWave + jj;
+            const double x = lane_bcast(st.acc[Q], jj);  // the row of step t: every term taken
+#pragma unroll
+            for (int q = Q; q < RPL; q++) {
+                const bool in = (st.c[q] & kCsStep) == t;
+                if (DRAIN) {
+                    const bool tk = in && st.e[q] < st.e1[q];
+                    st.acc[q] = tk ? st.acc[q] - st.v[q] * x : st.acc[q];
+                    st.e[q] += tk ? 1 : 0;
+                    st.k[q] = tk ? min((st.c[q] >> 8) & kCsRunMax, st.e1[q] - st.e[q]) : 0;
+                } else {  // an outside term at the head: taken by any step
+                    const bool tk = (in || (st.c[q] & kCsOut)) && st.e[q] < st.e1[q];
+                    const double xs = in ? x : 1.0;
+                    st.acc[q] = tk ? st.acc[q] - st.v[q] * xs : st.acc[q];
+                    st.e[q] += tk ? 1 : 0;
+                    st.c[q] = (uint16_t)S.c[st.e[q]], st.v[q] = S.v[st.e[q]];
+                }
+            }
+            if (DRAIN) colsweep_drain<Q, RPL>(st, S);
+        }
+        colsweep_steps<Q + 1, RPL, DRAIN>(st, S, nr);
+    }
+}
+template <int RPL, bool DRAIN>
+__device__ __forceinline__ void levels_colsweep(SweepLds &S, int nr, int lane) {
+    ColState<RPL> st;
 #pragma unroll
     for (int q = 0; q < RPL; q++) {
         const int t = lane + q * kWave;
         const int k = t < nr ? S.lv[t] : 0;
-        e[q] = t < nr ? S.ps[k] : 0, e1[q] = t < nr ? S.p[k + 1] : 0;
-        acc[q] = S.w[k];
-        c0[q] = (uint16_t)S.c[e[q]], v0[q] = S.v[e[q]];
-        c1[q] = (uint16_t)S.c[e[q] + 1], v1[q] = S.v[e[q] + 1];
+        st.e[q] = t < nr ? S.ps[k] : 0, st.e1[q] = t < nr ? S.p[k + 1] : 0, st.k[q] = 0;
+        st.acc[q] = S.w[k];
+        st.c[q] = (uint16_t)S.c[st.e[q]], st.v[q] = S.v[st.e[q]];  // e <= e1 <= ne: inside the padded image
     }
-    // the row's next term taken: shift the pair, refill the second (entries stay inside the
-    // padded image: e + 1 <= e1 <= ne), then the outside terms that follow it
-    auto next = [&](int q) {
-        e[q]++, c0[q] = c1[q], v0[q] = v1[q];
-        c1[q] = (uint16_t)S.c[e[q] + 1], v1[q] = S.v[e[q] + 1];
-        while (e[q] < e1[q] && c0[q] == R) {
-            acc[q] -= v0[q];
-            e[q]++, c0[q] = c1[q], v0[q] = v1[q];
-            c1[q] = (uint16_t)S.c[e[q] + 1], v1[q] = S.v[e[q] + 1];
-        }
-    };
-#pragma unroll
-    for (int q = 0; q < RPL; q++)  // outside terms at a row's head (before its first in-block term)
-        if (e[q] < e1[q] && c0[q] == R) {
-            acc[q] -= v0[q];
-            next(q);
-        }
-#pragma unroll
-    for (int Q = 0; Q < RPL; Q++) {
-        const int jn = min(kWave, nr - Q * kWave);
-        for (int jj = 0; jj < jn; jj++) {
-            const int t = Q * kWave + jj;
-            const double x = lane_bcast(acc[Q], jj);  // the row of step t: every term taken
-#pragma unroll
-            for (int q = Q; q < RPL; q++) {
-                if (e[q] < e1[q] && c0[q] == t) {
-                    acc[q] -= v0[q] * x;
-                    next(q);
-                }
-            }
-        }
-    }
+    colsweep_steps<0, RPL, DRAIN>(st, S, nr);
 #pragma unroll
     for (int q = 0; q < RPL; q++) {
         const int t = lane + q * kWave;
-        if (t < nr) S.w[S.lv[t]] = acc[q];
+        if (t < nr) S.w[S.lv[t]] = st.acc[q];
     }
 }
-__device__ __forceinline__ void colsweep_dispatch(SweepLds &S, int nr, int R, int lane) {
-    if (nr <= kWave) levels_colsweep<1>(S, nr, R, lane);
-    else if (nr <= 2 * kWave) levels_colsweep<2>(S, nr, R, lane);
-    else levels_colsweep<4>(S, nr, R, lane);
+__device__ __forceinline__ void colsweep_dispatch(SweepLds &S, int nr, int lane, bool drain) {
+    if (drain) {
+        if (nr <= kWave) levels_colsweep<1, true>(S, nr, lane);
+        else if (nr <= 2 * kWave) levels_colsweep<2, true>(S, nr, lane);
+        else levels_colsweep<4, true>(S, nr, lane);
+    } else {
+        if (nr <= kWave) levels_colsweep<1, false>(S, nr, lane);
+        else if (nr <= 2 * kWave) levels_colsweep<2, false>(S, nr, lane);
+        else levels_colsweep<4, false>(S, nr, lane);
+    }
 }
 
 // The level phase, out of LDS.  Per level every thread takes whole rows and consumes a row's
@@ -2083,12 +2180,14 @@ __device__ __forceinline__ void upper_block(
         const uint32_t ec = e0 + (uint32_t)(e < ne ? e : 0);
         c[u] = __builtin_nontemporal_load(col + ec), v[u] = __builtin_nontemporal_load(val + ec);
     }
-    // column sweep: an in-block column's step (static: before the wait); lv holds the rows by step
+    // staged columns (static: before the wait): local row, or the layout's code (column sweep; lv
+    // holds the rows by step); R outside
     int32_t cl[EPU];
 #pragma unroll
     for (int u = 0; u < EPU; u++) {
         const bool local = c[u] >= r0 && c[u] < r1;
-        cl[u] = !local ? R : (cs ? (int32_t)uf.s[2 * (c[u] - uf.row0) + (BWD ? 1 : 0)] : c[u] - r0);
+        const uint32_t ec = e0 + (uint32_t)(tid + u * TPB < ne ? tid + u * TPB : 0);
+        cl[u] = cs ? (int32_t)(uint16_t)(BWD ? uf.cb[ec - uf.cb0] : uf.cf[ec - uf.cf0]) : (!local ? R : c[u] - r0);
     }
     if (!cs)
         for (int l = tid; l <= nl; l += TPB) S.lv[l] = (int16_t)(lvl_row[m.l0 + l] - r0);
@@ -2134,7 +2233,7 @@ __device__ __forceinline__ void upper_block(
     // (a single wave's LDS accesses complete in program order) the chain is LDS latency only;
     // narrow levels give each row a lane group (levels_grouped)
     if (tid < kWave) {
-        if (cs) colsweep_dispatch(S, nr, R, tid);
+        if (cs) colsweep_dispatch(S, nr, tid, m.l1 & (BWD ? kMetaCoBwd : kMetaCoFwd));
         else if (CPK_UPPER_DATAFLOW && (m.l1 & (BWD ? kMetaDfBwd : kMetaDfFwd)))
             levels_dataflow<BWD, CPK_DF_CH(BWD), true, RMAX / kWave>(S, nr, R, ne, tid);
         else if (CPK_UPPER_GROUP(BWD)) levels_grouped<CPK_UPPER_CH(BWD), BWD, true>(S, nl, false, tid);
@@ -2223,11 +2322,12 @@ __device__ __forceinline__ void last_block(
         const uint32_t ef = (uint32_t)m.fe0 + (uint32_t)(e < nef ? e : 0);
         cf[u] = __builtin_nontemporal_load(fcol + ef), vf[u] = __builtin_nontemporal_load(fval + ef);
     }
-    int32_t cl[EPU];  // staged columns: local row, or the step (column sweep); R outside
+    int32_t cl[EPU];  // staged columns: local row, or the layout's code (column sweep); R outside
 #pragma unroll
     for (int u = 0; u < EPU; u++) {
         const bool local = cf[u] >= r0 && cf[u] < r1;
-        cl[u] = !local ? R : (csf ? (int32_t)uf.s[2 * (cf[u] - uf.row0)] : cf[u] - r0);
+        const uint32_t ef = (uint32_t)m.fe0 + (uint32_t)(tid + u * TPB < nef ? tid + u * TPB : 0);
+        cl[u] = csf ? (int32_t)(uint16_t)uf.cf[ef - uf.cf0] : (!local ? R : cf[u] - r0);
     }
     if (!csf)
         for (int l = tid; l <= nl; l += TPB) S.lv[l] = (int16_t)(lvl_row[m.l0 + l] - r0);
@@ -2271,7 +2371,7 @@ __device__ __forceinline__ void last_block(
     if (uf.p) fold_known<TPB>(S, nr, tid);
     else fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (csf) colsweep_dispatch(S, nr, R, tid);
+        if (csf) colsweep_dispatch(S, nr, tid, m.l1 & kMetaCoFwd);
         else if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd)) levels_dataflow<false, CPK_DF_CH(false), true, RMAX / kWave>(S, nr, R, nef, tid);
         else if (CPK_UPPER_GROUP(false)) levels_grouped<CPK_UPPER_CH(false), false, true>(S, nl, false, tid);
         else sweep_levels<kWave, false, true, CPK_UPPER_CH(false), true, true>(S, nl, false, tid);
@@ -2301,7 +2401,7 @@ __device__ __forceinline__ void last_block(
         const int e = tid + u * TPB;
         if (e < neb) {
             const bool local = cb[u] >= r0 && cb[u] < r1;
-            S.c[e] = !local ? (int16_t)R : (int16_t)(csb ? uf.s[2 * (cb[u] - uf.row0) + 1] : cb[u] - r0);
+            S.c[e] = csb ? uf.cb[(uint32_t)m.be0 + (uint32_t)e - uf.cb0] : (int16_t)(!local ? R : cb[u] - r0);
             S.v[e] = local ? vb[u] : vb[u] * g[u];
         }
     }
@@ -2309,7 +2409,7 @@ __device__ __forceinline__ void last_block(
     if (uf.p) fold_known<TPB>(S, nr, tid);
     else fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (csb) colsweep_dispatch(S, nr, R, tid);
+        if (csb) colsweep_dispatch(S, nr, tid, m.l1 & kMetaCoBwd);
         else if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfBwd)) levels_dataflow<true, CPK_DF_CH(true), true, RMAX / kWave>(S, nr, R, neb, tid);
         else if (CPK_UPPER_GROUP(true)) levels_grouped<CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
         else sweep_levels<kWave, true, true, CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
