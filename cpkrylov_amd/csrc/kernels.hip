@@ -119,17 +119,19 @@ void make_dmat(const HCsr &a, DMat &d) {
 constexpr double kDataflowTripCost = 1.0;
 // the column sweep (levels_colsweep): blocks of at most 256 rows (4 per lane).  The choice
 // against the other loops is made in cycles, fitted on the stamps build over every upper block of
-// the +-64 window and S10 with the column sweep forced on and off (tools/upper_cycles.py BLOCKS=,
-// profiles/r05_colsweep_calibration.txt): cycles per step at 1 / 2 / 3 / 4 rows per lane; a
-// level-loop trip ~300 cycles, a dataflow trip ~220
+// the +-64 window with the column sweep forced on and off (tools/upper_cycles.py BLOCKS=,
+// profiles/r05_colsweep_calibration.txt): cycles per step at 1 / 2 / 3 / 4 rows per lane, without
+// and with drains, and per drain trip; a level-loop trip ~290 cycles, a dataflow trip ~270
+// forward / ~190 backward (3 and 4 rows per lane: extrapolated, no such block measured)
 constexpr int kColsweepMaxRows = 4 * 64;
-constexpr double kColsweepStepCycles[4] = {150.0, 200.0, 280.0, 360.0};
+constexpr double kColsweepStepCycles[4] = {220.0, 257.0, 340.0, 420.0};
+constexpr double kColsweepStepDrainCycles[4] = {297.0, 353.0, 430.0, 500.0};
 // the column sweep's staged columns (DFactor::ucode): an in-block entry holds its column's step |
 // the run of outside entries behind it (up to the next in-block entry or the row's end) << 8, an
 // outside entry kCsOut
 constexpr int kCsOut = 0x8000, kCsStep = 0x80ff, kCsRunMax = 127;
-constexpr double kColsweepDrainCycles[4] = {150.0, 250.0, 350.0, 450.0};  // a drain trip (four terms a row)
-constexpr double kLevelTripCycles = 300.0, kDataflowTripCycles = 220.0;
+constexpr double kColsweepDrainCycles[4] = {261.0, 617.0, 800.0, 1000.0};  // a drain trip (four terms a row)
+constexpr double kLevelTripCycles = 290.0, kDataflowTripCycles[2] = {272.0, 190.0};
 #ifndef CPK_UPPER_DATAFLOW
 #define CPK_UPPER_DATAFLOW 1
 #endif
@@ -366,8 +368,9 @@ void mark_dataflow(std::vector<int32_t> &meta, const std::vector<int64_t> &round
                     int64_t trips = 0;  // drain trips: four terms of every row's run per trip
                     if (drain)
                         for (int x : run) trips += (x + 3) / 4;
-                    const double ct = (double)nr * kColsweepStepCycles[rpl - 1] + (double)trips * kColsweepDrainCycles[rpl - 1];
-                    const double base = df ? kDataflowTripCycles * (double)dt : kLevelTripCycles * (double)lt;
+                    const double ct = (double)nr * (drain ? kColsweepStepDrainCycles : kColsweepStepCycles)[rpl - 1] +
+                                      (double)trips * kColsweepDrainCycles[rpl - 1];
+                    const double base = df ? kDataflowTripCycles[dir] * (double)dt : kLevelTripCycles * (double)lt;
                     cs = cs_mode == 2 || ct < base;
                 }
                 if (cs) m[3] |= (dir ? kMetaCsBwd : kMetaCsFwd) | (drain ? (dir ? kMetaCoBwd : kMetaCoFwd) : 0);
