@@ -268,6 +268,17 @@ void launch_krylov_spmv(Ctx &c, const DMat &AC, DState *st, double *y, int64_t n
 // ----------------------------------------------------------------------------------------------
 // vkp1 = vprec(1:n) - alpha*vk - beta*vkm1 ; qkp1 = qk - vprec(n+1:N); qkp1 = qkp1 - alpha*qk - beta*qkm1
 // + beta_new = dot(u, vkp1) + dot(t, qkp1)      (cpminres.m:191-194, identical in the others)
+// the fused Lanczos + MINRES pass streams its vectors: nontemporal loads and stores (A/B: CPK_LANCZOS_NT)
+#ifndef CPK_LANCZOS_NT
+#define CPK_LANCZOS_NT 1
+#endif
+#if CPK_LANCZOS_NT
+#define NTL(p) __builtin_nontemporal_load(p)
+#define NTS(p, v) __builtin_nontemporal_store((v), (p))
+#else
+#define NTL(p) (*(p))
+#define NTS(p, v) (*(p) = (v))
+#endif
 template <int KIND>
 struct LanczosStep {
     DState *st;
@@ -392,8 +403,8 @@ struct LanczosStep {
 #pragma unroll
         for (int e = 0; e < kTile; e++) {
             const int64_t i = i0 + e * kBlock;
-            p[e] = vprec[i], a[e] = vk[i], b[e] = vkm1[i], u[e] = ut[i];
-            w1[e] = u_w1[i], w2[e] = u_w2[i], x[e] = xy[i];
+            p[e] = NTL(vprec + i), a[e] = vk[i], b[e] = NTL(vkm1 + i), u[e] = NTL(ut + i);
+            w1[e] = NTL(u_w1 + i), w2[e] = NTL(u_w2 + i), x[e] = NTL(xy + i);
         }
 #pragma unroll
         for (int e = 0; e < kTile; e++) {
@@ -407,8 +418,10 @@ struct LanczosStep {
                 v = t - alpha * a[e] - beta * b[e];
                 dadd(acc[1], u[e], v);
             }
-            vkp1[i] = v;
-            minres_wx(i, b[e], w1[e], w2[e], x[e]);
+            NTS(vkp1 + i, v);
+            const double w = (b[e] - u_oldeps * w1[e] - u_delta * w2[e]) / u_gamma;  // minres_wx
+            NTS(u_wn + i, w);
+            NTS(xy + i, (i < n) ? x[e] + u_tau * w : x[e] - u_tau * w);
         }
     }
     __device__ void fin(const double *tot);
