@@ -1568,32 +1568,56 @@ struct ColState {
 // the outside runs behind this step's in-block terms (k[q] terms of row q >= Q0), four loads per
 // row in flight per trip, subtracted in the row's order
 template <int Q, int RPL>
-__device__ __forceinline__ void colsweep_run_chunk(ColState<RPL> &st, const SweepLds &S, int j0) {
+__device__ __forceinline__ void colsweep_run_load(const ColState<RPL> &st, const SweepLds &S, int j0, double (&u)[4][4]) {
     if constexpr (Q < RPL) {
-        double u[4];
 #pragma unroll
-        for (int i = 0; i < 4; i++) u[i] = S.v[j0 + i < st.k[Q] ? st.e[Q] + j0 + i : st.e[Q]];
-#pragma unroll
-        for (int i = 0; i < 4; i++) st.acc[Q] = j0 + i < st.k[Q] ? st.acc[Q] - u[i] : st.acc[Q];
+        for (int i = 0; i < 4; i++) u[Q][i] = S.v[j0 + i < st.k[Q] ? st.e[Q] + j0 + i : st.e[Q]];
     }
 }
+template <int Q, int RPL>
+__device__ __forceinline__ void colsweep_run_sub(ColState<RPL> &st, int j0, const double (&u)[4][4]) {
+    if constexpr (Q < RPL) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) st.acc[Q] = j0 + i < st.k[Q] ? st.acc[Q] - u[Q][i] : st.acc[Q];
+    }
+}
+template <int Q, int RPL>
+__device__ __forceinline__ void colsweep_next_load(const ColState<RPL> &st, const SweepLds &S, int (&cn)[4], double (&vn)[4]) {
+    if constexpr (Q < RPL) {
+        const int e = st.e[Q] + st.k[Q];
+        cn[Q] = (uint16_t)S.c[e], vn[Q] = S.v[e];
+    }
+}
+// a trip issues every row's four loads before its subtractions; the rows' next entries (behind
+// their runs) are loaded first, in flight across the trips
 template <int Q0, int RPL>
 __device__ __forceinline__ void colsweep_drain(ColState<RPL> &st, const SweepLds &S) {
     static_assert(RPL <= 4, "four rows per lane at most");
+    int cn[4];
+    double vn[4];
+    colsweep_next_load<Q0, RPL>(st, S, cn, vn);
+    colsweep_next_load<Q0 + 1, RPL>(st, S, cn, vn);
+    colsweep_next_load<Q0 + 2, RPL>(st, S, cn, vn);
+    colsweep_next_load<Q0 + 3, RPL>(st, S, cn, vn);
     int km = 0;
 #pragma unroll
     for (int q = Q0; q < RPL; q++) km = max(km, st.k[q]);
     // (a #pragma unroll loop over the rows inside the trip loop is not unrolled by this compiler)
     for (int j0 = 0; __any(j0 < km); j0 += 4) {
-        colsweep_run_chunk<Q0, RPL>(st, S, j0);
-        colsweep_run_chunk<Q0 + 1, RPL>(st, S, j0);
-        colsweep_run_chunk<Q0 + 2, RPL>(st, S, j0);
-        colsweep_run_chunk<Q0 + 3, RPL>(st, S, j0);
+        double u[4][4];
+        colsweep_run_load<Q0, RPL>(st, S, j0, u);
+        colsweep_run_load<Q0 + 1, RPL>(st, S, j0, u);
+        colsweep_run_load<Q0 + 2, RPL>(st, S, j0, u);
+        colsweep_run_load<Q0 + 3, RPL>(st, S, j0, u);
+        colsweep_run_sub<Q0, RPL>(st, j0, u);
+        colsweep_run_sub<Q0 + 1, RPL>(st, j0, u);
+        colsweep_run_sub<Q0 + 2, RPL>(st, j0, u);
+        colsweep_run_sub<Q0 + 3, RPL>(st, j0, u);
     }
 #pragma unroll
     for (int q = Q0; q < RPL; q++) {
         st.e[q] += st.k[q];
-        st.c[q] = (uint16_t)S.c[st.e[q]], st.v[q] = S.v[st.e[q]];
+        st.c[q] = cn[q], st.v[q] = vn[q];
     }
 }
 // steps Q * 64 .. (the rows lane + Q * 64 broadcast), rows q >= Q taking terms
