@@ -2866,10 +2866,11 @@ __global__ __launch_bounds__(TPB * SPLIT) __attribute__((amdgpu_waves_per_eu(SPL
         for (int j = 0; j < RPT; j++) {
             const int i = tid + j * TPB;
             const int rr = m.r0 + (i < nr ? i : nr - 1);  // clamped: later gathers need no predicate
-            q[j] = ptr[rr];
-            sp[j] = need_perm ? perm[rr] : rr;
-            if (BWD) wr[j] = w[rr], dr[j] = D[rr];
-            if (i < nl) lvr[j] = lvl_row[m.l0 + i];
+            // the row arrays are streamed once per sweep too
+            q[j] = __builtin_nontemporal_load(ptr + rr);
+            sp[j] = need_perm ? __builtin_nontemporal_load(perm + rr) : rr;
+            if (BWD) wr[j] = w[rr], dr[j] = __builtin_nontemporal_load(D + rr);
+            if (i < nl) lvr[j] = __builtin_nontemporal_load(lvl_row + m.l0 + i);
         }
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
