@@ -1,7 +1,11 @@
 #!/usr/bin/env python
-"""Krylov iters/sec of CP-MINRES on the synthetic 10M-dof saddle-point system (S10).
+"""Krylov iters/sec of CP-MINRES on the synthetic 10M-dof saddle-point system of SURVEY.md 8d.
 
 Metric (BASELINE.json): "Krylov iters/sec + SpMV GB/s (% HBM peak), cpminres 10M-dof".
+  system    SURVEY 8d's S10 generator with its +-64 B coupling window (nnz(L) 40.9 M, elimination
+            tree 255 deep): the headline (round 6; rounds 1-5 quoted the +-4 window, now the `w4`
+            block).  The `s50` block is config 5 (cpdqgmres(40) at 50 M dofs); both blocks are
+            child runs of this script with their own timing, parity and CPU sample.
   step      one converging cpminres solve (the method call, kernels/cpminres.m) with the
             example options (cpk_exprog1.m:79-90: atol = rtol = 1e-6, itmax = 500, nitref = 1,
             force_itref, residual_update); b1 (the shifted rhs, reg_cpkrylov.m:152-160) and the
@@ -52,11 +56,13 @@ def parse(argv=None):
                     help="s10: symmetric 10M cpminres (the headline metric); s50: nonsymmetric 3x3-block "
                          "50M cpdqgmres(40) (SURVEY.md section 8d config 5)")
     ap.add_argument("--size", type=int, default=None, help="total dofs N (default 10M for s10, 50M for s50)")
-    ap.add_argument("--window", type=int, default=4,
-                    help="s10: the B coupling window (+-W columns; SURVEY.md 8d sketches 64, the headline system uses 4)")
+    ap.add_argument("--window", type=int, default=64,
+                    help="s10: the B coupling window (+-W columns; SURVEY.md 8d's 64 is the headline, 4 the w4 block)")
     ap.add_argument("--method", default=None)
     ap.add_argument("--itmax", type=int, default=None, help="s50: iterations per step (default 120)")
-    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=None,
+                    help="budget of the CPU-baseline sample (default 40 s for the +-64 system, whose serial leg "
+                         "must converge for the parity block; 20 s otherwise)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-reps", type=int, default=20)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE passes")
@@ -68,8 +74,10 @@ def parse(argv=None):
     ap.add_argument("--no-exact", action="store_true",
                     help="skip the exact_dots block (the same solve with order-independent inner products, "
                          "timed, and compared bit for bit with the oracle's exact mode)")
-    ap.add_argument("--no-w64", action="store_true",
-                    help="skip the w64 block (the S10 system with SURVEY 8d's +-64 B window, measured by a child run)")
+    ap.add_argument("--no-sub", action="store_true",
+                    help="skip the w4 and s50 blocks (child runs: the +-4 window system and config 5)")
+    ap.add_argument("--no-w4", action="store_true", help="skip the w4 block")
+    ap.add_argument("--no-s50", action="store_true", help="skip the s50 block")
     ap.add_argument("--rhs-perturb", type=float, default=0.0,
                     help="scale the rhs by (1 + eps*u), u uniform in [-1, 1] (sensitivity runs; never the bench line)")
     ap.add_argument("--perturb-seed", type=int, default=1)
@@ -79,6 +87,8 @@ def parse(argv=None):
         a.size = 50_000_000 if s50 else 10_000_000
     if a.method is None:
         a.method = "dqgmres" if s50 else "minres"
+    if a.cpu_seconds is None:
+        a.cpu_seconds = 40.0 if (not s50 and a.window >= 64) else 20.0
     a.opts = dict(EXPROG_OPTS)
     if s50:
         a.opts.update(mem=40, restart=40, itmax=a.itmax or 120)
@@ -291,10 +301,16 @@ def main(argv=None):
                                 "GBps": round(gbs(prof.fwd_resid_bytes, prof.fwd_resid_ms), 1),
                                 "replaces_ms": round(prof.resid_ms + prof.fwd_ms, 5)}
 
+    passes = None
+    if rank == 0 and world == 1 and not distributed and args.config == "s50":
+        passes = s50_passes(ctx, step, M, N, n, m, args, prof, gbs)
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not distributed:
-        cpu, parity = cpu_baseline(S, b1.cpu().numpy(), M, args, hist_gpu, niters_last)
+        if args.config == "s50":
+            cpu = cpu_baseline_s50(S, b1.cpu().numpy(), M, args)
+        else:
+            cpu, parity = cpu_baseline(S, b1.cpu().numpy(), M, args, hist_gpu, niters_last)
     exact = None
     if rank == 0 and world == 1 and not distributed and not args.no_exact:
         exact = exact_block(ctx, S, M, step, st, hist, xy, b1, xy0, args, iters / dt)
@@ -319,7 +335,8 @@ def main(argv=None):
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": (f"S10 synthetic symmetric saddle-point system{'' if args.window == 4 else f' (B window +-{args.window})'}, "
+            "config": {"workload": (f"S10 synthetic symmetric saddle-point system, SURVEY 8d generator with B window "
+                                    f"+-{args.window}{' (the headline system)' if args.window == 64 else ''}, "
                                     f"cp{args.method} to convergence (cpk_exprog1 options), step = one method call"
                                     if args.config == "s10" else
                                     f"S50 synthetic nonsymmetric 3x3-block saddle-point system, cp{args.method}"
@@ -349,8 +366,13 @@ def main(argv=None):
             "parity": parity,
             "exact_dots": exact,
         }
-        if world == 1 and not distributed and args.config == "s10" and args.window == 4 and not args.no_w64:
-            line["w64"] = w64_block(args)
+        if passes is not None:
+            line["passes"] = passes
+        if world == 1 and not distributed and args.config == "s10" and args.window == 64 and not args.no_sub:
+            if not args.no_w4:
+                line["w4"] = sub_block(args, ["--window", "4"], "the S10 system with the +-4 B window (rounds 1-5's headline)")
+            if not args.no_s50:
+                line["s50"] = sub_block(args, ["--config", "s50"], "config 5: S50, cpdqgmres(40), 120 iterations")
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
@@ -526,29 +548,92 @@ def exact_block(ctx, S, M, step, st, hist, xy, b1, xy0, args, value_default):
     return out
 
 
-def w64_block(args):
-    """SURVEY 8d's +-64 B window (nnz(L) ~ 40.9 M, elimination tree 255 deep): the same bench in
-    a child process (its own cpu_baseline sample, parity, PMC traffic), embedded as a block."""
+def sub_block(args, extra, what):
+    """A secondary configuration measured by a child run of this script (its own setup, timing,
+    CPU sample, parity, exact-mode and PMC blocks), embedded in the headline line."""
     import subprocess
-    # CPU budget: the serial leg (half of it) must run the ~17 iterations to convergence, ~1 s
-    # each here, for the parity block against the serial oracle
-    cmd = [sys.executable, os.path.abspath(__file__), "--window", "64", "--steps", str(args.steps), "--warmup",
-           str(args.warmup), "--cpu-seconds", str(max(args.cpu_seconds, 40.0)), "--no-w64"]
-    if args.no_pmc:
-        cmd.append("--no-pmc")
-    if args.no_cpu_baseline:
-        cmd.append("--no-cpu-baseline")
-    if args.no_exact:
-        cmd.append("--no-exact")
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=420)
+    cmd = [sys.executable, os.path.abspath(__file__), "--steps", str(args.steps), "--warmup", str(args.warmup),
+           "--no-sub"] + extra
+    for flag in ("no_pmc", "no_cpu_baseline", "no_exact"):
+        if getattr(args, flag):
+            cmd.append("--" + flag.replace("_", "-"))
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=420)
+    except subprocess.TimeoutExpired:
+        return {"error": "child timed out (420 s)", "what": what}
     if r.returncode != 0:
-        return {"error": f"child exited {r.returncode}: {r.stderr[-400:]}"}
+        return {"error": f"child exited {r.returncode}: {r.stderr[-400:]}", "what": what}
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    keep = ("value", "unit", "ms_per_step", "iters_per_step", "solved", "roofline", "spmv_roofline", "kernels",
-            "cpu_baseline", "pmc", "parity", "exact_dots", "setup_s")
-    out = {k: d.get(k) for k in keep}
+    keep = ("metric", "value", "unit", "ms_per_step", "iters_per_step", "solved", "roofline", "spmv_roofline",
+            "kernels", "cpu_baseline", "pmc", "parity", "exact_dots", "setup_s", "passes")
+    out = {"what": what}
+    out.update({k: d.get(k) for k in keep if k in d})
     out["config"] = d["config"]
     return out
+
+
+def s50_passes(ctx, step, M, N, n, m, args, prof, gbs):
+    """Config 5's per-pass rates: one more 120-iteration cpdqgmres(40) call with engine option
+    profile_passes (eager batches, HIP events between the passes; cpk_debug_pass_times), each
+    pass's algorithmic bytes summed over the iterations at their own window sizes nv (kernels/
+    cpdqgmres.m:194-275; solvers.hip):
+      window dots   arnoldi_dots_kernel: nv basis vectors, ut, w read, the new vector written,
+                    the old one read for its y part: (nv + 3) 8N + 8m
+      orthogonal.   ArnoldiOrth: nv basis vectors, the new vector read and written, ut:
+                    (nv + 3) 8N
+      direction     DqgmresDirection: nv' directions, v_k, the new vector read and written, the
+                    new direction written, xy read and written: (nv' + 6) 8N
+      M*z           Precond::apply_bytes per iteration; Krylov SpMV as cpk_profile_kernels."""
+    from cpkrylov_amd import _lib
+    ctx.set_option("profile_passes", 1)
+    try:
+        step()
+        v = (C.c_double * 8)()
+        _lib.check(_lib.lib.cpk_debug_pass_times(ctx.h, v))
+    finally:
+        ctx.set_option("profile_passes", 0)
+    its, spmv_ms, apply_ms, dots_ms, orth_ms, dir_ms, wd, wr = list(v)
+    if its <= 0:
+        return None
+    its_i = int(its)
+    byts = {"krylov_spmv": prof.spmv_bytes * its, "mz": prof.apply_bytes * its,
+            "dots": (wd + 3 * its) * 8.0 * N + 8.0 * m * its, "orth": (wd + 3 * its) * 8.0 * N,
+            "direction": (wr + 6 * its) * 8.0 * N}
+    ms = {"krylov_spmv": spmv_ms, "mz": apply_ms, "dots": dots_ms, "orth": orth_ms, "direction": dir_ms}
+    out = {"iterations": its_i, "mean_window": round(wd / its, 2),
+           "method": "one extra call with engine option profile_passes (eager, HIP events between passes); "
+                     "bytes: the byte model in bench.py s50_passes at each iteration's window size"}
+    for k in ms:
+        a = gbs(byts[k], ms[k]) if ms[k] > 0 else 0.0
+        out[k] = {"ms_per_iter": round(ms[k] / its, 4), "bytes_per_iter": round(byts[k] / its),
+                  "GBps": round(a, 1), "frac": round(a / HBM_PEAK_GBS, 4)}
+    out["iteration_ms_eager"] = round(sum(ms.values()) / its, 4)
+    return out
+
+
+def cpu_baseline_s50(S, b1, M_gpu, args):
+    """Config 5's CPU sample: the oracle's cpdqgmres(40) on the same system and shifted rhs with
+    the product's factors, OpenMP on the granted cores, a few iterations (the serial window
+    loops take ~10 s per iteration at 50 M dofs)."""
+    from oracle import oracle as O
+    host = host_cpu()
+    L, D, perm = M_gpu.export_factors()
+    Mo = O.LDL2(S["G"], S["B"], -S["C"], factors=(L, D, perm))
+    Mo.set(nitref=args.opts["nitref"], itref_tol=args.opts["itref_tol"], force_itref=1.0, residual_update=1.0)
+    T = O.set_threads(host["threads"])
+    try:
+        itmax = 3
+        t = time.perf_counter()
+        _, _, st = O.method(args.method, b1, S["Q"], S["C"], Mo, dict(args.opts, itmax=itmax))
+        dt = time.perf_counter() - t
+    finally:
+        O.set_threads(1)
+    it = int(st["niters"])
+    return {"value": round(it / dt, 4), "unit": "iters/s", "cores": T, "kind": "port",
+            "sample": f"oracle cp{args.method}(mem 40) on S50 (same b1, the product's factors), {it} iterations "
+                      f"(the initial M*b included) in {dt:.1f} s, OpenMP on {T} threads, gcc -O3 -ffp-contract=off "
+                      "(no serial leg: ~10 s per iteration)",
+            "host": host}
 
 
 PMC_REPS = 5

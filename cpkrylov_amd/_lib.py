@@ -100,6 +100,7 @@ _SIGS = {
     "cpk_debug_pipe_stamps": ([P(C.c_uint64), C.c_int, P(C.c_int)], C.c_int),
     "cpk_debug_blk_cycles": ([P(C.c_uint64), C.c_int64, P(C.c_int64)], C.c_int),
     "cpk_debug_block_model": ([vp, P(C.c_int64), C.c_int64, P(C.c_int64)], C.c_int),
+    "cpk_debug_pass_times": ([vp, P(C.c_double)], C.c_int),
     "cpk_ctx_set_option": ([C.c_void_p, C.c_char_p, C.c_char_p], C.c_int),
     "cpk_pc_sweep_info": ([C.c_void_p, P(C.c_int64)], C.c_int),
     "cpk_ctx_get_option": ([C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t], C.c_int),

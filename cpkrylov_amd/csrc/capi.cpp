@@ -617,6 +617,13 @@ int cpk_debug_blk_cycles(uint64_t *out, int64_t n, int64_t *copied) {
     API_END
 }
 
+int cpk_debug_pass_times(cpk_ctx ctx, double *out) {
+    API_BEGIN
+    need(ctx && out, "NULL argument");
+    std::memcpy(out, ctx->c.pass_ms, sizeof ctx->c.pass_ms);
+    API_END
+}
+
 int cpk_debug_block_model(cpk_pc M, int64_t *out, int64_t n, int64_t *copied) {
     API_BEGIN
     need(M && copied, "NULL argument");

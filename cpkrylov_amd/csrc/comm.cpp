@@ -15,6 +15,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "dev.hpp"
 
@@ -40,23 +41,29 @@ struct RcclComm : Comm {
     void allgather(const double *send, double *recv, size_t n, hipStream_t s) override {
         nccl_check(ncclAllGather(send, recv, n, ncclDouble, c, s), "ncclAllGather");
     }
-    // host bytes through a device staging buffer, in chunks (RCCL moves device memory only)
+    void allreduce_max_i64(int64_t *buf, size_t n, hipStream_t s) override {
+        nccl_check(ncclAllReduce(buf, buf, n, ncclInt64, ncclMax, c, s), "ncclAllReduce(max)");
+    }
+    // host bytes through a device staging buffer, in chunks (RCCL moves device memory only).  The
+    // staging buffer is kept across calls (the analysis broadcast makes ~40 of them) and released
+    // by release_staging(); it only grows, up to one chunk
+    DBuf<char> stage;
     void broadcast_host(void *p, size_t n, int root, hipStream_t s) override {
         if (!n) return;
         int me = 0;
         nccl_check(ncclCommUserRank(c, &me), "ncclCommUserRank");
         constexpr size_t kChunk = size_t(256) << 20;
-        DBuf<char> d;
-        d.alloc(std::min(n, kChunk));
+        if (stage.n < std::min(n, kChunk)) stage.alloc(std::min(n, kChunk));
         char *h = static_cast<char *>(p);
         for (size_t o = 0; o < n; o += kChunk) {
             const size_t k = std::min(kChunk, n - o);
-            if (me == root) CPK_HIP(hipMemcpyAsync(d.p, h + o, k, hipMemcpyHostToDevice, s));
-            nccl_check(ncclBroadcast(d.p, d.p, k, ncclChar, root, c, s), "ncclBroadcast");
-            if (me != root) CPK_HIP(hipMemcpyAsync(h + o, d.p, k, hipMemcpyDeviceToHost, s));
+            if (me == root) CPK_HIP(hipMemcpyAsync(stage.p, h + o, k, hipMemcpyHostToDevice, s));
+            nccl_check(ncclBroadcast(stage.p, stage.p, k, ncclChar, root, c, s), "ncclBroadcast");
+            if (me != root && h) CPK_HIP(hipMemcpyAsync(h + o, stage.p, k, hipMemcpyDeviceToHost, s));
             CPK_HIP(hipStreamSynchronize(s));
         }
     }
+    void release_staging() override { stage.release(); }
     bool capturable() const override { return true; }  // the solvers also check the dist_graph option
     int kind() const override { return CPK_COMM_RCCL; }
     int count() const override {
@@ -100,6 +107,7 @@ struct NullComm : Comm {
     void allgather(const double *send, double *recv, size_t n, hipStream_t s) override {
         if (n) CPK_HIP(hipMemcpyAsync(recv + (size_t)rank * n, send, n * sizeof(double), hipMemcpyDeviceToDevice, s));
     }
+    void allreduce_max_i64(int64_t *, size_t, hipStream_t) override {}
     void broadcast_host(void *, size_t, int, hipStream_t) override {
         throw Error(CPK_ERR_UNSUPPORTED, "internal: broadcast on the peer-less timing communicator");
     }
@@ -166,8 +174,6 @@ struct SimComm : Comm {
     }
     void allreduce_sum(double *buf, size_t n, hipStream_t s) override {
         g->enter(rank, "allreduce_sum", n);
-        g->enter(rank, "allreduce_sum_i64", n);
-        g->enter(rank, "allgather", n);
         check(n);
         CPK_HIP(hipMemcpyAsync(g->shared.p + rank * n, buf, n * sizeof(double), hipMemcpyDeviceToDevice, s));
         CPK_HIP(hipStreamSynchronize(s));
@@ -177,6 +183,7 @@ struct SimComm : Comm {
         g->barrier(rank);
     }
     void allreduce_sum_i64(int64_t *buf, size_t n, hipStream_t s) override {
+        g->enter(rank, "allreduce_sum_i64", n);
         check(n);  // the shared buffer holds 8-byte words: the digits travel as their bits
         int64_t *sh = reinterpret_cast<int64_t *>(g->shared.p);
         CPK_HIP(hipMemcpyAsync(sh + rank * n, buf, n * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
@@ -186,7 +193,26 @@ struct SimComm : Comm {
         CPK_HIP(hipStreamSynchronize(s));
         g->barrier(rank);
     }
+    void allreduce_max_i64(int64_t *buf, size_t n, hipStream_t s) override {
+        g->enter(rank, "allreduce_max_i64", n);
+        check(n);
+        int64_t *sh = reinterpret_cast<int64_t *>(g->shared.p);
+        CPK_HIP(hipMemcpyAsync(sh + rank * n, buf, n * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+        CPK_HIP(hipStreamSynchronize(s));
+        g->barrier(rank);
+        std::vector<int64_t> all(n * (size_t)g->P), mx(n);
+        CPK_HIP(hipMemcpyAsync(all.data(), sh, all.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        CPK_HIP(hipStreamSynchronize(s));
+        g->barrier(rank);
+        for (size_t i = 0; i < n; i++) {
+            mx[i] = all[i];
+            for (int q = 1; q < g->P; q++) mx[i] = std::max(mx[i], all[(size_t)q * n + i]);
+        }
+        CPK_HIP(hipMemcpyAsync(buf, mx.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        CPK_HIP(hipStreamSynchronize(s));
+    }
     void allgather(const double *send, double *recv, size_t n, hipStream_t s) override {
+        g->enter(rank, "allgather", n);
         check(n);
         if (n) CPK_HIP(hipMemcpyAsync(g->shared.p + rank * n, send, n * sizeof(double), hipMemcpyDeviceToDevice, s));
         CPK_HIP(hipStreamSynchronize(s));
@@ -199,7 +225,7 @@ struct SimComm : Comm {
         g->enter(rank, "broadcast_host", n);
         if (rank == root) g->host.assign(static_cast<char *>(p), static_cast<char *>(p) + n);
         g->barrier(rank);
-        if (rank != root) std::memcpy(p, g->host.data(), n);
+        if (rank != root && p) std::memcpy(p, g->host.data(), n);
         g->barrier(rank);
         if (rank == root) std::vector<char>().swap(g->host);
     }

@@ -67,11 +67,17 @@ struct Comm {
     // integer sums (exact_dots: the superaccumulator digits of every rank, xacc.hpp)
     virtual void allreduce_sum_i64(int64_t *buf, size_t n, hipStream_t s) = 0;
     virtual void allgather(const double *send, double *recv, size_t n, hipStream_t s) = 0;
+    // elementwise maximum over the ranks, in place on device memory: the status agreement of a
+    // distributed solve (solvers.hip, agree_status) -- a rank-local failure reaches every rank
+    virtual void allreduce_max_i64(int64_t *buf, size_t n, hipStream_t s) = 0;
     virtual bool capturable() const = 0;  // may be captured into a hipGraph
     virtual bool has_peers() const { return true; }  // false: the timing stand-in (no exchange)
     // rank `root`'s n host bytes at p to every rank's p (the distributed construction's analysis,
-    // precond.cpp); n is the same on every rank.  Only where has_peers().
+    // precond.cpp); n is the same on every rank.  Only where has_peers().  A receiver that passes
+    // p = nullptr takes part and discards the bytes (a receiver that could not allocate keeps the
+    // broadcast sequence, so the root never waits for it; the construction then fails everywhere).
     virtual void broadcast_host(void *p, size_t n, int root, hipStream_t s) = 0;
+    virtual void release_staging() {}  // broadcast_host's device staging, kept across calls
     virtual int kind() const = 0;   // CPK_COMM_RCCL / _SIM / _NULL (cpk_ctx_get_info)
     virtual int count() const = 0;  // ranks of the communicator (RCCL: ncclCommCount)
 };
@@ -135,6 +141,13 @@ struct EngineOpts {
                                   //                     one option that changes results (last bits)
     int batch = 0;                // batch:              fixed iterations per graph (0: adaptive)
     bool profile_fwd_sched = false;     // profile_fwd_sched: diagnostic, the profiled forward reads its input in schedule order
+    bool profile_passes = false;  // profile_passes:     diagnostic, cpdqgmres runs eagerly with HIP events around its
+                                  //                     passes (cpk_debug_pass_times: the bench's s50 block)
+    // fail_inject: test hook, "R:site" -- rank R of a distributed solve fails locally at `site`:
+    // "setup" (before the solve's first collective), "batch:K" (a host error after its K-th graph
+    // batch) or "chain:K" (the sweep chain's device error word set after batch K).  Rank-local by
+    // design, so it is NOT part of the plan agreement's hash (tests/test_gpu_dist.py)
+    std::string fail_inject;
 };
 EngineOpts engine_opts_from_env();
 // name as in the comments above; throws CPK_ERR_ARGS on an unknown name or a bad value
@@ -167,6 +180,10 @@ struct Ctx {
     // dist1 asks for the distributed kernels (tests; DESIGN.md section 7's 1-rank comparison).
     // The timing stand-in (NullComm) declares nranks > 1.
     bool dist() const { return comm != nullptr && (nranks > 1 || opts.dist1); }
+    // profile_passes: the last profiled solve's per-pass sums (cpk_debug_pass_times):
+    // [iterations, Krylov SpMV ms, M*z ms, window dots ms, orthogonalisation ms, direction ms,
+    //  sum of the dots' window sizes, sum of the direction's window sizes]
+    double pass_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     bool exact() const { return opts.exact_dots; }
     // reduction workspace for grids of up to `count` partial sums (and, in exact mode, the
     // sub-accumulators of at least 4 sums); ensure_xacc: room for `nsums` exact sums per launch
@@ -338,6 +355,10 @@ struct FwdIn {
 };
 // the sweep chain's error word (a producer wait timed out): CPK_ERR_HIP, cleared
 void check_chain(const DFactor &F);
+// the distributed solve's status word: host_code, raised to chain_code if a chain error word of
+// any of the nf factors is set (kernels.hip, solve_status_kernel)
+void launch_solve_status(Ctx &c, const DFactor *const *F, int nf, int64_t host_code, int64_t chain_code, int64_t *out);
+bool debug_set_chain_error(Ctx &c, const DFactor &F);
 bool fuse_last_ok(const DFactor &F);
 // defer (optional): the last round is left to the backward sweep (sptrsv_last_kernel solves it
 // forward and backward in one launch); *defer then says how, for launch_sptrsv_bwd's last

@@ -29,8 +29,6 @@ namespace cpk {
 // ascending (the serial loop's order).
 static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &perm, LdlSymbolic &sym) {
     const int64_t N = Kp.nrows;
-    auto T0 = std::chrono::steady_clock::now();
-    auto lap = [&](const char *w) { if (getenv("CPK_SYMT")) { auto t = std::chrono::steady_clock::now(); fprintf(stderr, "%s %.3f\n", w, std::chrono::duration<double>(t - T0).count()); T0 = t; } };
     Factor f;
     f.N = N;
     f.perm = perm;
@@ -52,7 +50,6 @@ static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &
             }
         }
     }
-    lap("etree");
     // row patterns and seeds, rows in parallel chunks
     const int T = std::max(1, std::min<int>(host_threads(), (int)((N + 65535) / 65536)));
     struct Chunk {
@@ -95,7 +92,6 @@ static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &
     for (int t = 1; t < T; t++) th.emplace_back(work, t);
     work(0);
     for (auto &x : th) x.join();
-    lap("rows");
     sym.N = N;
     sym.Rp.assign(N + 1, 0);
     sym.kp_ptr.assign(N + 1, 0);
@@ -107,7 +103,6 @@ static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &
         }
     if ((int64_t)sym.Rp[N] > INT32_MAX || sym.kp_ptr[N] < 0)
         throw Error(CPK_ERR_NOMEM, "factor too large for 32-bit entry offsets");
-    lap("prefix");
     const int64_t nnz = sym.Rp[N];
     {
         // the large outputs are zero-filled on threads of their own: the first touch of fresh
@@ -121,7 +116,6 @@ static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &
         sym.Rcsc.resize(nnz);
         for (auto &x : al) x.join();
     }
-    lap("alloc");
     {
         std::vector<std::thread> cp;
         auto copy = [&](int t) {
@@ -144,13 +138,11 @@ static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &
         copy(0);
         for (auto &x : cp) x.join();
     }
-    lap("concat");
     // columns of L: rows in ascending order within each column (the serial loop's lnz[i]++ order)
     parallel_for(nnz, [&](int64_t lo, int64_t hi) {  // column counts: a histogram, order-free
         for (int64_t q = lo; q < hi; q++) __atomic_fetch_add(&f.Lp[sym.Rc[q] + 1], (int64_t)1, __ATOMIC_RELAXED);
     }, 1 << 18);
     for (int64_t i = 0; i < N; i++) f.Lp[i + 1] += f.Lp[i];
-    lap("column counts");
     {
         // a parallel transpose: thread t owns the row range rcut[t] .. rcut[t+1) and the column
         // range ccut[t] .. ccut[t+1) (equal entry counts each).  Every thread sorts its rows'
@@ -196,13 +188,11 @@ static Factor ldl_symbolic_threaded(const HCsr &Kp, const std::vector<int32_t> &
         for (int t = 1; t < T; t++) cth.emplace_back(bucket, t);
         bucket(0);
         for (auto &x : cth) x.join();
-        lap("column buckets");
         cth.clear();
         for (int u = 1; u < T; u++) cth.emplace_back(place, u);
         place(0);
         for (auto &x : cth) x.join();
     }
-    lap("columns");
     return f;
 }
 

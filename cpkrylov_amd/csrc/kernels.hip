@@ -804,6 +804,7 @@ void launch_spmv_resid_norm(Ctx &c, const DMat &A, const double *xin, int64_t ne
         else
             spmv_launch(c, A, y, 0, EpiResidNorm<>{xin, neg_from, r, tol, active_out, rb, run, active});
     } else if (dist) {  // no rows here: zero local sums
+        c.ensure_partials(1);  // (and the exact digits, if exact_dots was switched on after the buffers were sized)
         if (c.exact()) CPK_HIP(hipMemsetAsync(c.xred.p, 0, 2 * kXW * sizeof(int64_t), c.stream));
         else CPK_HIP(hipMemsetAsync(c.red.p, 0, 2 * sizeof(double), c.stream));
     }
@@ -2516,8 +2517,19 @@ static void launch_last(Ctx &c, const DFactor &F, const FwdIn &in, double *w, do
 // (vmcnt(0)) before the workgroup barrier, one lane stores the flag sc1, and consumers poll it
 // sc1.  Flags hold the launch's epoch + 1 (no reset pass); the last workgroup (ticket) advances
 // the epoch.  Every spin is bounded: a wait that outlives kChainSpinCap sets the error word, every
-// other waiter then gives up, and the host raises CPK_ERR_HIP (check_chain).
-constexpr uint32_t kChainSpinCap = 1u << 20;
+// other waiter of that launch then gives up, and the host raises CPK_ERR_HIP (check_chain).
+constexpr uint32_t kChainSpinCap = 1u << 20;  // polls (2^20: with the back-off below, ~0.5 s)
+// CPK_CHAIN_ACQUIRE (default 1): an agent-scope acquire after each task's polls.  Row 1 of the
+// guide's table (sc1 loads in place of the acquire) is measured for one workgroup per CU; the
+// chain runs up to four, so the acquire stays (round 6, profiles/r06_chain_handoff_ab.txt).
+// CPK_CHAIN_LDS_MIN: a floor on the launch's LDS (bytes); > 80 KB admits one workgroup per CU,
+// the table row's residency (the A/B's third arm).
+#ifndef CPK_CHAIN_ACQUIRE
+#define CPK_CHAIN_ACQUIRE 1
+#endif
+#ifndef CPK_CHAIN_LDS_MIN
+#define CPK_CHAIN_LDS_MIN 0
+#endif
 // polling back-off of a waiting task: CPK_CHAIN_FAST_POLLS polls s_sleep CPK_CHAIN_SLEEP0 apart,
 // then CPK_CHAIN_SLEEP1 (units of 64 cycles)
 #ifndef CPK_CHAIN_FAST_POLLS
@@ -2572,9 +2584,13 @@ __global__ __launch_bounds__(TPB) void sptrsv_chain_kernel(
             const uint32_t *f = flag + didx[k];
             uint32_t spins = 0;
             while (ld_agent32(f) != want) {
-                if (ld_agent32(err) != 0) break;  // a wait timed out somewhere: give up
+                // a wait of THIS launch timed out somewhere: give up.  The word holds the epoch of
+                // the launch that timed out, so a word left set (until the host's next check,
+                // check_chain or the distributed solve's status agreement) never disables the
+                // waits of a later launch
+                if (ld_agent32(err) == want) break;
                 if (++spins > kChainSpinCap) {
-                    st_agent32(err, 1);
+                    st_agent32(err, want);
                     break;
                 }
                 // back off: a few quick polls, then ~1000 cycles apart (poll traffic stays low)
@@ -2583,6 +2599,16 @@ __global__ __launch_bounds__(TPB) void sptrsv_chain_kernel(
             }
         }
         __syncthreads();
+#if CPK_CHAIN_ACQUIRE
+        // the consumer's agent acquire after the polls (MI355X_MICROARCH.md "Valid forms":
+        // poll -> acquire -> s_waitcnt vmcnt(0) -> barrier -> loads).  The sc1 loads alone replace
+        // it only for one workgroup per CU (the table's row 1); this kernel runs up to four
+        if (k1 > k0 && threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+#endif
     };
     if (kind == 0)
         upper_block<TPB, RPU, EPU, false, false, true>(smem, meta[b], lvl_row, fptr, fcol, fval, D, perm, xin, neg_from, w,
@@ -2603,6 +2629,42 @@ __global__ __launch_bounds__(TPB) void sptrsv_chain_kernel(
             st_agent32(ch.ctrl, want);  // the next launch's epoch
         }
     }
+}
+
+// the distributed solve's status word (solvers.hip, agree_status): a host-side code of this rank
+// (0: none) and every sweep chain's device error word of the preconditioner, as one int64 --
+// (code << 16) | (0xffff - rank), so the ranks' maximum names the largest code and, among equal
+// codes, the lowest failing rank
+__global__ void solve_status_kernel(int64_t *out, int64_t host, const uint32_t *e0, const uint32_t *e1,
+                                    const uint32_t *e2, const uint32_t *e3, const uint32_t *e4, const uint32_t *e5,
+                                    int64_t chain_code) {
+    int64_t v = host;
+    const uint32_t *e[6] = {e0, e1, e2, e3, e4, e5};
+    for (int i = 0; i < 6; i++)
+        if (e[i] && ld_agent32(e[i]) != 0) v = max(v, chain_code);
+    out[0] = v;
+}
+void launch_solve_status(Ctx &c, const DFactor *const *F, int nf, int64_t host_code, int64_t chain_code, int64_t *out) {
+    const uint32_t *e[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    int k = 0;
+    for (int i = 0; i < nf; i++)
+        for (const DChain &h : F[i]->chain)
+            if (h.ntask > 0 && k < 6) e[k++] = h.ctrl.p + 2;
+    hipLaunchKernelGGL(solve_status_kernel, dim3(1), dim3(1), 0, c.stream, out, host_code, e[0], e[1], e[2], e[3], e[4],
+                       e[5], chain_code);
+    CPK_HIP(hipGetLastError());
+}
+// test hook (engine option fail_inject "R:chain:K"): set a chain's device error word, as a wait
+// that timed out would; false if the factor has no chain
+bool debug_set_chain_error(Ctx &c, const DFactor &F) {
+    for (const DChain &h : F.chain)
+        if (h.ntask > 0) {
+            const uint32_t one = 1;
+            CPK_HIP(hipMemcpyAsync(h.ctrl.p + 2, &one, sizeof one, hipMemcpyHostToDevice, c.stream));
+            CPK_HIP(hipStreamSynchronize(c.stream));
+            return true;
+        }
+    return false;
 }
 
 // the block kernel a chain runs: 256 threads (blocks of <= 512 rows / 3072 entries, the single-
@@ -2708,7 +2770,7 @@ template <int TPB, int RPU, int EPU>
 static void launch_chain_t(Ctx &c, const DFactor &F, int kind, const FwdIn &in, double *w, double *out, bool add,
                            const int *run, const int *active, double *ys, const PackArgs &pk) {
     const DChain &h = F.chain[kind];
-    const size_t lds = sweep_lds_bytes(RPU * TPB, EPU * TPB);
+    const size_t lds = std::max<size_t>(sweep_lds_bytes(RPU * TPB, EPU * TPB), (size_t)CPK_CHAIN_LDS_MIN);
     static const bool lds_ok = lds <= 64 * 1024 ||
         (hipFuncSetAttribute((const void *)sptrsv_chain_kernel<TPB, RPU, EPU, false>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
@@ -2718,12 +2780,13 @@ static void launch_chain_t(Ctx &c, const DFactor &F, int kind, const FwdIn &in, 
     const ChainArgs ch{h.task.p, h.dptr.p, h.didx.p, h.flag.p, h.ctrl.p, (int)h.ntask};
     const Img img{RPU * TPB, EPU * TPB};  // narrow rounds: every task resident at the kernel's image
     const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
+    const size_t ldsb = std::max<size_t>(img_bytes(img), (size_t)CPK_CHAIN_LDS_MIN);
     if (add)
-        hipLaunchKernelGGL((sptrsv_chain_kernel<TPB, RPU, EPU, true>), dim3((unsigned)h.ntask), dim3(TPB), img_bytes(img), c.stream,
+        hipLaunchKernelGGL((sptrsv_chain_kernel<TPB, RPU, EPU, true>), dim3((unsigned)h.ntask), dim3(TPB), ldsb, c.stream,
                            ch, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,
                            F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, pk, ufold_of(F), img);
     else
-        hipLaunchKernelGGL((sptrsv_chain_kernel<TPB, RPU, EPU, false>), dim3((unsigned)h.ntask), dim3(TPB), img_bytes(img),
+        hipLaunchKernelGGL((sptrsv_chain_kernel<TPB, RPU, EPU, false>), dim3((unsigned)h.ntask), dim3(TPB), ldsb,
                            c.stream, ch, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p,
                            F.D.p, F.perm.p, in.xin, in.neg_from, in.sched_in, in.xs, w, out, run, active, ys, pk, ufold_of(F), img);
     CPK_HIP(hipGetLastError());

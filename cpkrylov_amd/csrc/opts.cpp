@@ -76,6 +76,7 @@ const BoolOpt kBool[] = {
     {"no_chain", &EngineOpts::no_chain},
     {"no_bcast_analysis", &EngineOpts::no_bcast_analysis},
     {"profile_fwd_sched", &EngineOpts::profile_fwd_sched},
+    {"profile_passes", &EngineOpts::profile_passes},
 };
 
 }  // namespace
@@ -113,6 +114,15 @@ void set_engine_option(EngineOpts &o, const std::string &name, const std::string
         if (end == value.c_str() || *end != '\0' || v < 0 || v > 4096)
             throw Error(CPK_ERR_ARGS, "engine option " + name + " must be an integer in [0, 4096], got '" + value + "'");
         (name == "batch" ? o.batch : o.r0_xcd_chunk) = (int)v;
+    } else if (name == "fail_inject") {  // test hook (dev.hpp): "R:setup", "R:batch:K" or "R:chain:K"
+        int r = -1, k = 0;
+        char site[16] = {0};
+        const bool ok = value.empty() ||
+                        (sscanf(value.c_str(), "%d:%15[a-z]:%d", &r, site, &k) >= 2 && r >= 0 &&
+                         (std::string(site) == "setup" || std::string(site) == "batch" || std::string(site) == "chain"));
+        if (!ok)
+            throw Error(CPK_ERR_ARGS, "engine option fail_inject: expected R:setup, R:batch:K or R:chain:K, got '" + value + "'");
+        o.fail_inject = value;
     } else if (name == "chain_wide") {
         char *end = nullptr;
         const long v = strtol(value.c_str(), &end, 10);
@@ -137,6 +147,7 @@ std::string get_engine_option(const EngineOpts &o, const std::string &name, bool
     if (name == "batch") return std::to_string(o.batch);
     if (name == "r0_xcd_chunk") return std::to_string(o.r0_xcd_chunk);
     if (name == "chain_wide") return std::to_string(o.chain_wide);
+    if (name == "fail_inject") return o.fail_inject;
     throw Error(CPK_ERR_ARGS, "unknown engine option '" + name + "'");
 }
 
@@ -153,6 +164,7 @@ EngineOpts engine_opts_from_env() {
     from("batch");
     from("r0_xcd_chunk");
     from("chain_wide");
+    from("fail_inject");
     return o;
 }
 
@@ -166,6 +178,7 @@ std::string engine_opts_string(const EngineOpts &o, bool dist) {
     put("batch");
     put("r0_xcd_chunk");
     put("chain_wide");
+    put("fail_inject");
     return s;
 }
 
@@ -200,6 +213,7 @@ uint64_t engine_opts_hash(const EngineOpts &o) {
     mix(std::to_string(o.batch));
     mix(std::to_string(o.r0_xcd_chunk));
     mix(std::to_string(o.chain_wide));
+    // fail_inject is rank-local by design (a test hook): not hashed, so the plan agreement passes
     return h;
 }
 

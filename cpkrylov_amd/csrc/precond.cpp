@@ -545,14 +545,26 @@ namespace {
 struct AnalysisBcast {
     Comm &cm;
     hipStream_t s;
+    // a receiver that cannot hold a field (allocation failure) keeps taking part in every later
+    // broadcast, discarding the bytes, so rank 0 never waits for it; the ranks then agree
+    // (analyze_dist) and every one of them fails with the same error
+    bool failed = false;
+    std::string why;
     template <class T>
     void pod(T &v) { cm.broadcast_host(&v, sizeof v, 0, s); }
     template <class T>
     void vec(std::vector<T> &v) {
         uint64_t n = v.size();
         pod(n);
-        v.resize((size_t)n);
-        if (n) cm.broadcast_host(v.data(), (size_t)n * sizeof(T), 0, s);
+        if (!failed) {
+            try {
+                v.resize((size_t)n);
+            } catch (const std::exception &e) {
+                failed = true, why = e.what();
+                std::vector<T>().swap(v);
+            }
+        }
+        if (n) cm.broadcast_host(failed ? nullptr : v.data(), (size_t)n * sizeof(T), 0, s);
     }
     void run(Analysis &an) {
         pod(an.n), pod(an.m), pod(an.N), pod(an.ordering), pod(an.seconds), pod(an.sweep);
@@ -607,7 +619,16 @@ static Analysis analyze_dist(Ctx &c, const HCsr &A11, const HCsr &B, const HCsr 
         err.assign(msg.begin(), msg.end());
         if (!err.empty()) throw Error(CPK_ERR_ARGS, "distributed preconditioner (analysis on rank 0): " + err);
         pcl.lap(c.rank == 0 ? "global analysis (rank 0)" : "rank 0's global analysis (waiting)");
-        bc.run(an);
+        try {
+            bc.run(an);
+        } catch (...) {
+            c.comm->release_staging();
+            throw;
+        }
+        c.comm->release_staging();
+        if (!all_ranks(c, !bc.failed))
+            throw Error(CPK_ERR_NOMEM, "distributed preconditioner: a rank could not hold rank 0's analysis" +
+                                           (bc.failed ? " (this rank: " + bc.why + ")" : std::string()));
         if (c.rank != 0) an.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         pcl.lap("analysis broadcast from rank 0");
     }

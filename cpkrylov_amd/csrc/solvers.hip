@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <functional>
 #include <memory>
 #include <string>
@@ -1611,6 +1612,57 @@ struct SolveCore {
         CPK_HIP(hipStreamSynchronize(c.stream));
     }
 
+    // ---- the distributed solve's status agreement -------------------------------------------
+    // At each agreement point every rank contributes a status word (0, or its error code and
+    // rank: solve_status_kernel, which also reads every sweep chain's device error word), the
+    // ranks take the maximum (Comm::allreduce_max_i64), and if it is not 0 every rank throws:
+    // the failing rank its own error, the others the same code naming that rank.  Points: before
+    // the solve's first collective (method_solve_device) and after every graph batch, where the
+    // host synchronises anyway (the word travels with the state read-back).  A failure between
+    // collectives of a batch enqueued eagerly cannot be contained this way (the other ranks are
+    // already inside that batch's collectives); a captured batch fails before it starts.
+    DBuf<int64_t> status;
+    int64_t status_h = 0;
+    int64_t nbatch = 0;
+    bool agreeing() const { return c.dist() && c.comm->has_peers(); }
+    int64_t status_word(int code) const { return code ? ((int64_t)code << 16) | (0xffff - (c.rank & 0xffff)) : 0; }
+    // engine option fail_inject "R:site[:K]" (test hook): does this rank fail at `site` / batch k?
+    int injected(const char *site, int64_t k = 0) const {
+        if (c.opts.fail_inject.empty()) return 0;
+        int r = -1, kk = 0;
+        char st[16] = {0};
+        if (sscanf(c.opts.fail_inject.c_str(), "%d:%15[a-z]:%d", &r, st, &kk) < 2 || r != c.rank) return 0;
+        if (std::string(st) != site) return 0;
+        return (std::string(site) == "setup" || kk == k) ? CPK_ERR_HIP : 0;
+    }
+    void status_enqueue(int code) {
+        ensure(status, 1);
+        const DFactor *fs[2] = {&M.dF, &M.sep.tsw};
+        launch_solve_status(c, fs, 2, status_word(code), status_word(CPK_ERR_HIP), status.p);
+        c.comm->allreduce_max_i64(status.p, 1, c.stream);
+        CPK_HIP(hipMemcpyAsync(&status_h, status.p, sizeof status_h, hipMemcpyDeviceToHost, c.stream));
+    }
+    void status_check(std::exception_ptr local) {  // after the stream synchronised
+        if (!status_h) return;
+        const int code = (int)(status_h >> 16), who = 0xffff - (int)(status_h & 0xffff);
+        // the chains' error words are read (and cleared) by check_chain on the rank that set them
+        try {
+            check_chain(M.dF);
+            check_chain(M.sep.tsw);
+        } catch (const Error &) {
+            if (!local) local = std::current_exception();
+        }
+        if (local) std::rethrow_exception(local);
+        throw Error(code, "distributed solve stopped: rank " + std::to_string(who) + " failed (status " +
+                              std::to_string(code) + "); every rank returns its error");
+    }
+    // the agreement before the solve's first collective
+    void agree_setup(std::exception_ptr local, int code) {
+        status_enqueue(code);
+        CPK_HIP(hipStreamSynchronize(c.stream));
+        status_check(local);
+    }
+
     // replay `body` (one iteration) in batches until the device sets `stop`.  A batch is a
     // captured graph of b iterations (b a power of two <= batch), captured once per loop site
     // and size and replayed by later calls with the same key.  After the first batch the size
@@ -1661,11 +1713,34 @@ struct SolveCore {
         for (;;) {
             const double res0 = h.residNorm;
             const int64_t k0 = h.k;
-            hipGraphExec_t exec = use_graph ? graph_for(site, b, body) : nullptr;
-            if (exec) CPK_HIP(hipGraphLaunch(exec, c.stream));
-            else
-                for (int i = 0; i < b; i++) body();
+            // distributed: a rank-local failure of this batch (a host error, a sweep chain's
+            // timed-out wait) joins the batch's status agreement instead of leaving the other
+            // ranks in the next collective (kernels/cpminres.m:195-199: the caller sees the error)
+            std::exception_ptr local;
+            int code = 0;
+            try {
+                hipGraphExec_t exec = use_graph ? graph_for(site, b, body) : nullptr;
+                if (exec) CPK_HIP(hipGraphLaunch(exec, c.stream));
+                else
+                    for (int i = 0; i < b; i++) body();
+                nbatch++;
+                code = injected("batch", nbatch);
+                if (injected("chain", nbatch) && !debug_set_chain_error(c, M.dF) && !debug_set_chain_error(c, M.sep.tsw))
+                    code = CPK_ERR_HIP;  // no chain to fail: the host error instead
+                if (code) throw Error(code, "fail_inject: rank " + std::to_string(c.rank) + " failed after batch " +
+                                                std::to_string(nbatch));
+            } catch (const Error &e) {
+                local = std::current_exception(), code = e.code;
+            } catch (...) {
+                local = std::current_exception(), code = CPK_ERR_HIP;
+            }
+            if (!agreeing()) {
+                if (local) std::rethrow_exception(local);
+            } else {
+                status_enqueue(code);
+            }
             pull();
+            if (agreeing()) status_check(local);
             if (print && printer) printer();
             if (h.stop) break;
             if (h.k > guard) throw Error(CPK_ERR_HIP, "solver loop did not terminate");
@@ -2048,15 +2123,62 @@ void SolveCore::dqgmres(const double *b, double *xy, cpk_stats *stats) {
         printf("stopTol = %e\n", h.stopTol);
         printf("%5s  %9s\n", "iter", "|resid|");
     }
+    // profile_passes (diagnostic): events between the passes of every iteration, eager batches
+    const bool prof = c.opts.profile_passes;
+    std::vector<hipEvent_t> evs;
+    size_t ev_used = 0;
+    const int64_t k_start = h.k;
+    int64_t kh = h.k;  // the host's copy of the iteration counter (window sizes of the byte model)
+    std::vector<double> wdots, wdir;
+    auto mark = [&]() {
+        if (ev_used == evs.size()) {
+            hipEvent_t e;
+            CPK_HIP(hipEventCreate(&e));
+            evs.push_back(e);
+        }
+        CPK_HIP(hipEventRecord(evs[ev_used++], c.stream));
+    };
+    if (prof) use_graph = false;
     auto body = [&]() {
+        if (prof) mark();
         launch_krylov_spmv(c, AC, st, UT, n, PolArnoldiSpmv{V, N, M1});
+        if (prof) mark();
         M.apply(UT, n, Wv, &st->running);
+        if (prof) mark();
         launch_arnoldi_dots(c, st, V, Wv, UT, n, N, M1, Mm);
+        if (prof) mark();
         launch_ewtred<2>(c, N, ArnoldiOrth{st, V, UT, n, N, M1, Window{}, nullptr});
+        if (prof) mark();
         launch_ewt(c, N, DqgmresDirection{st, V, PV, xy, n, N});
+        if (prof) {
+            mark();
+            // window sizes of this iteration (kernels: window(st, M1) and DqgmresDirection::setup)
+            const int64_t kk = kh + 1, mem_ = (int64_t)h.mem;
+            wdots.push_back((double)(kk - std::max<int64_t>(1, kk - mem_ + 1) + 1));
+            wdir.push_back((double)(kk - std::max<int64_t>(1, kk - mem_)));
+            kh++;
+        }
     };
     if (print) print_hist_lines("%5lld  %14.7e\n");
     loop(body, [&]() { print_hist_lines("%5lld  %14.7e\n"); });
+    if (prof) {
+        CPK_HIP(hipStreamSynchronize(c.stream));
+        // the iterations that ran (a batch's no-op iterations past the stop are not counted)
+        const size_t its = (size_t)std::min<int64_t>(std::max<int64_t>(h.k - k_start, 0), (int64_t)(ev_used / 6));
+        double ms[5] = {0, 0, 0, 0, 0}, wd = 0, wr = 0;
+        for (size_t it = 0; it < its; it++) {
+            for (int q = 0; q < 5; q++) {
+                float t = 0;
+                CPK_HIP(hipEventElapsedTime(&t, evs[6 * it + q], evs[6 * it + q + 1]));
+                ms[q] += t;
+            }
+            wd += wdots[it], wr += wdir[it];
+        }
+        c.pass_ms[0] = (double)its;
+        for (int q = 0; q < 5; q++) c.pass_ms[1 + q] = ms[q];
+        c.pass_ms[6] = wd, c.pass_ms[7] = wr;
+        for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+    }
     if (h.err) raise_error();
     if (stats) stats->solved = h.residNorm <= h.stopTol;
     finish_stats(stats);
@@ -2099,6 +2221,19 @@ void method_solve_device(Ctx &c, int method, const double *d_b, const DMat &AC, 
     if (method < CPK_CG || method > CPK_DQGMRES) throw Error(CPK_ERR_ARGS, "unknown method");
     CPK_HIP(hipEventRecord(c.ev0, c.stream));
     SolveCore &s = solver_for(c, M, AC, method, opts, d_b, d_xy);
+    s.nbatch = 0;
+    if (s.agreeing()) {  // a rank that fails before the solve's first collective stops every rank
+        std::exception_ptr local;
+        int code = s.injected("setup");
+        if (code) {
+            try {
+                throw Error(code, "fail_inject: rank " + std::to_string(c.rank) + " failed at the solve's setup");
+            } catch (const Error &) {
+                local = std::current_exception();
+            }
+        }
+        s.agree_setup(local, code);
+    }
     switch (method) {
     case CPK_MINRES: s.minres_like(0, d_b, d_xy, stats); break;
     case CPK_CGLANCZOS: s.minres_like(1, d_b, d_xy, stats); break;

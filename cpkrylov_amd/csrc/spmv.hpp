@@ -39,7 +39,10 @@ __device__ __forceinline__ double halo_gather(const Epi &epi, const double *x, c
                                               int32_t c) {
     if constexpr (!HALO) return gathered(epi, x[c]);
     const bool loc = c < nloc;
-    const double v = (loc ? x : xg - nloc)[c];
+    // a selected base and a selected index (no pointer before xg is ever formed)
+    const double *base = loc ? x : xg;
+    const int64_t k = loc ? (int64_t)c : (int64_t)c - nloc;
+    const double v = base[k];
     return loc ? gathered(epi, v) : v;
 }
 

@@ -313,6 +313,11 @@ int cpk_debug_blk_cycles(uint64_t *out, int64_t n, int64_t *copied);
  * not modelled), outside terms behind in-block ones, column sweep valid, loop chosen (0 level,
  * 1 dataflow, 2 column sweep).  out = NULL: *copied = the total count. */
 int cpk_debug_block_model(cpk_pc M, int64_t *out, int64_t n, int64_t *copied);
+/* Diagnostic: the last cpdqgmres solve of this context run with engine option profile_passes
+ * (eager batches, HIP events between its passes): out[8] = {iterations, Krylov SpMV ms, M*z ms,
+ * window dots ms, orthogonalisation ms, direction ms, sum over the iterations of the dots'
+ * window size, the same for the direction pass} (bench.py's s50 block: per-pass GB/s). */
+int cpk_debug_pass_times(cpk_ctx ctx, double *out);
 
 /* [c, s, d] = SymGivens(a, b)  (util/SymGivens.m:1-29) */
 int cpk_symgivens(double a, double b, double *c, double *s, double *d);

@@ -15,8 +15,9 @@ run uses the OpenMP leg for time and checks its first iterations against the ser
 
   python tests/golden/make_exact_golden.py s10   # ~1 minute, ~10 GB
   python tests/golden/make_exact_golden.py s50   # ~15 minutes on 8 cores, ~45 GB
+  python tests/golden/make_exact_golden.py w64   # the +-64 window system, ~3 minutes, ~14 GB
 
-Output: tests/golden/{s10,s50}_exact_golden.npz (data only).
+Output: tests/golden/{s10,s50,w64}_exact_golden.npz (data only).
 """
 import hashlib
 import os
@@ -40,6 +41,8 @@ CONFIGS = {
     # S10: the bench's converging cpminres (config 4); S50: the bench's truncated cpdqgmres(40)
     "s10": dict(N=10_000_000, gen=saddle_system, method="minres", opts=EXPROG),
     "s50": dict(N=50_000_000, gen=nonsym_system, method="dqgmres", opts=dict(EXPROG, itmax=120, mem=40)),
+    # SURVEY 8d's +-64 coupling window at 10 M dofs: the bench's headline system since round 6
+    "w64": dict(N=10_000_000, gen=lambda N: saddle_system(N=N, window=64), method="minres", opts=EXPROG),
 }
 PC = ("nitref", "itref_tol", "force_itref", "residual_update")
 

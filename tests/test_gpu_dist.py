@@ -670,3 +670,45 @@ def test_dist_refactor_failure_leaves_preconditioner_intact():
     for y0, y1, err in _run_ranks(2, work):
         assert err is not None and "pivot" in err
         assert np.array_equal(y0, y1)
+
+
+@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("site", ["setup", "batch:1", "chain:1"])
+def test_dist_rank_failure_reaches_every_rank(P, site):
+    """A failure local to one rank of a distributed solve -- before the solve's first collective,
+    a host error after a graph batch, or a sweep chain's timed-out wait (its device error word) --
+    reaches every rank through the solve's status agreement (solvers.hip, agree_status): every
+    rank returns the SAME error code promptly, none waits in a collective its peer never enters
+    (kernels/cpminres.m:195-199: the caller sees error(...); SURVEY 8b's status codes).  The
+    injected failure is engine option fail_inject (rank 1 only).  The contexts stay usable: the
+    same solve without the hook then matches on every rank."""
+    import time
+    import cpkrylov_amd as cpk
+    S = _system("synthetic20k")
+    opts = dict(F.EXPROG_OPTS)
+
+    def work(ctx, r):
+        t0 = time.perf_counter()
+        err = None
+        try:
+            cpk.reg_cpkrylov(cpk.cpminres, S["rhs"], S["Q"], S["B"], S["C"], S["G"], opts, ctx=ctx)
+        except cpk.CpkError as e:
+            err = (e.code, str(e))
+        dt = time.perf_counter() - t0
+        ctx.set_option("fail_inject", "")
+        x, stats, flag = cpk.reg_cpkrylov(cpk.cpminres, S["rhs"], S["Q"], S["B"], S["C"], S["G"], opts, ctx=ctx)
+        return err, dt, x, stats["niters"], flag["solved"]
+
+    res = _run_ranks(P, work, {"fail_inject": f"1:{site}", "batch": 1})
+    errs = [e for e, *_ in res]
+    assert all(e is not None for e in errs), errs
+    assert len({e[0] for e in errs}) == 1, errs
+    assert "fail_inject" in errs[1][1] or "timed out" in errs[1][1], errs[1]
+    for r, e in enumerate(errs):
+        if r != 1:
+            assert "rank 1 failed" in e[1], e
+    assert max(dt for _, dt, *_ in res) < 60.0, [dt for _, dt, *_ in res]
+    x0, it0, ok0 = res[0][2], res[0][3], res[0][4]
+    assert ok0
+    for _, _, x, it, ok in res[1:]:
+        assert np.array_equal(x, x0) and it == it0 and ok == ok0

@@ -359,15 +359,18 @@ def test_precond_apply_fused_last_round(gpu_ctx, name, props):
 _W64 = {}
 
 
+@pytest.mark.parametrize("wide", [0, 1 << 24])
 @pytest.mark.parametrize("name", ["cvxqp1_m", "synthetic", "w64"])
 @pytest.mark.parametrize("props", [dict(nitref=0), dict(nitref=1, force_itref=True),
                                    dict(nitref=2, force_itref=False, itref_tol=1e-30)])
-def test_precond_apply_sweep_chain(gpu_ctx, name, props):
-    """Every upper round of a solve in one launch whose blocks wait for their own producers
+def test_precond_apply_sweep_chain(gpu_ctx, name, props, wide):
+    """The narrow upper rounds of a solve in one launch whose blocks wait for their own producers
     (sptrsv_chain_kernel, the default when the upper rounds use the 256-thread blocks) against
     one launch per round (engine option no_chain) and the oracle: the default staging and small
     upper blocks (many rounds), in every apply path (plain, forced refinement with the fused
-    residual, data-dependent refinement), repeated applies (the flags' epochs)."""
+    residual, data-dependent refinement), repeated applies (the flags' epochs).  wide = 2^24
+    (engine option chain_wide): EVERY upper round in the chain -- the configuration that failed
+    in round 5 before the chain was narrowed (the chain's hand-off)."""
     import cpkrylov_amd as cpk
     if name == "w64":
         from cpkrylov_amd.synthetic import saddle_system
@@ -384,6 +387,8 @@ def test_precond_apply_sweep_chain(gpu_ctx, name, props):
         ys, chains = [], []
         for off in (False, True):
             opts = dict(no_chain=off)
+            if wide:
+                opts["chain_wide"] = wide
             if sweep:
                 opts["sweep"] = sweep
             with cpk.engine_options(**opts):
@@ -391,7 +396,10 @@ def test_precond_apply_sweep_chain(gpu_ctx, name, props):
             for k, v in props.items():
                 setattr(M, k, v)
             ys.append([M * z for z in zs])
-            chains.append(M.sweep_info()["chain_tasks"])
+            info = M.sweep_info()
+            chains.append(info["chain_tasks"])
+            if wide and not off and info["chain_tasks"]:  # every upper block forward and backward
+                assert info["chain_tasks"] >= info["upper_blocks"], info
         assert chains[1] == 0
         used.append(chains[0])
         L, D, perm = M.export_factors()

@@ -59,7 +59,10 @@ def _threads():
 @functools.lru_cache(maxsize=None)
 def _system(which):
     t = time.perf_counter()
-    S = saddle_system(N=S10_N) if which == "s10" else nonsym_system(N=S50_N)
+    if which == "w64":  # SURVEY 8d's +-64 coupling window (the bench's headline system since round 6)
+        S = saddle_system(N=S10_N, window=64)
+    else:
+        S = saddle_system(N=S10_N) if which == "s10" else nonsym_system(N=S50_N)
     _log(f"{which}: generated N={S['N']} in {time.perf_counter() - t:.1f} s")
     return S
 
@@ -280,7 +283,7 @@ def test_s50_eight_ranks():
 
 # ---- exact mode (engine option exact_dots): the serial oracle's bits -------------------------
 GOLDEN_EXACT = {w: os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"{w}_exact_golden.npz")
-                for w in ("s10", "s50")}
+                for w in ("s10", "s50", "w64")}
 
 
 def _sha(a):
@@ -292,8 +295,8 @@ def _check_exact(which, x, stats, flag, factors=None):
     """niters, solved, every history entry and x (a sample and a hash of all of it) against the
     exact-mode golden (tests/golden/make_exact_golden.py: the serial oracle in exact mode on the
     product's host-analysis factors), with ==; factors (optional) against its hashes"""
-    N = S10_N if which == "s10" else S50_N
-    if N != (10_000_000 if which == "s10" else 50_000_000) or (which == "s50" and S50_ITMAX != 120):
+    N = S50_N if which == "s50" else S10_N
+    if N != (50_000_000 if which == "s50" else 10_000_000) or (which == "s50" and S50_ITMAX != 120):
         pytest.skip("the exact goldens are for the headline sizes")
     g = np.load(GOLDEN_EXACT[which])
     if factors is not None:
@@ -313,7 +316,7 @@ def _check_exact(which, x, stats, flag, factors=None):
 def _one_gpu_exact(which):
     import cpkrylov_amd as cpk
     S = _system(which)
-    method, opts = ("minres", EXPROG_OPTS) if which == "s10" else ("dqgmres", S50_OPTS)
+    method, opts = ("dqgmres", S50_OPTS) if which == "s50" else ("minres", EXPROG_OPTS)
     with cpk.engine_options(exact_dots=1):
         t = time.perf_counter()
         x, stats, flag = cpk.reg_cpkrylov(getattr(cpk, "cp" + method), S["rhs"], S["Q"], S["B"], S["C"], S["G"],
@@ -328,6 +331,15 @@ def _one_gpu_exact(which):
 def test_s10_exact_one_gpu():
     """S10 cpminres to convergence in exact mode on one GPU: the serial oracle's bits"""
     _one_gpu_exact("s10")
+
+
+@pytest.mark.timeout(900)
+def test_w64_exact_one_gpu():
+    """SURVEY 8d's +-64 window system (10 M dofs, nnz(L) 40.9 M, elimination tree 255 deep: the
+    bench's headline since round 6) to convergence in exact mode on one GPU: niters, every history
+    entry and all of x bit for bit with the serial oracle's exact-mode record
+    (tests/golden/w64_exact_golden.npz), and the factors' hashes"""
+    _one_gpu_exact("w64")
 
 
 @pytest.mark.timeout(900)
