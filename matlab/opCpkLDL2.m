@@ -56,8 +56,26 @@ classdef opCpkLDL2 < opSpot
       function opOut = transpose(op)
          opOut = op;
       end
+      % conj / ctranspose (opLDL2.m:127-137): P*inv(conj(L)')*inv(conj(D))*inv(conj(L))*P'.  The
+      % factors are real (complex systems are out of scope, opLDL2.m:80's cflag), so conj of the
+      % operator is the operator and its conjugate transpose is its transpose: itself
+      function opOut = conj(op)
+         opOut = op;
+      end
       function opOut = ctranspose(op)
          opOut = op;
+      end
+      % double (opLDL2.m:138-149): the dense matrix, one column op * e_i at a time -- the same
+      % products the reference forms (each a device apply with the current properties)
+      function x = double(op)
+         n = op.nA + op.nC;
+         e = zeros(n, 1);
+         x = zeros(n);
+         for i = 1 : n
+            e(i) = 1;
+            x(:, i) = op * e;
+            e(i) = 0;
+         end
       end
    end
 
