@@ -1421,15 +1421,6 @@ constexpr int kSweepPad = 8;
 #define CPK_UPPER_CH(bwd) ((bwd) ? CPK_UPPER_CH_BWD : CPK_UPPER_CH_FWD)
 #ifndef CPK_PIPE_CH
 #define CPK_PIPE_CH 2  // entries per LDS round trip in the round-0 level loop
-#endif
-#ifndef CPK_COLSWEEP_V2
-#define CPK_COLSWEEP_V2 0  // 1: round 5's column sweep (A/B)
-#endif
-#ifndef CPK_COLSWEEP_BRANCH
-#define CPK_COLSWEEP_BRANCH 0  // 1: v3's takes as exec-masked regions (A/B)
-#endif
-#ifndef CPK_FOLD_V1
-#define CPK_FOLD_V1 0  // 1: round 5's fold_known, one batch in flight (A/B)
 #endif  // entry arrays padded for the branchless 8-entry chunks
 struct SweepLds {
     double *w, *v;
@@ -1488,45 +1479,13 @@ __device__ __forceinline__ void fold_prefix(SweepLds &S, int nr, int tid = -1, i
 // test and its select chain (~140 cycles per term on the ±64 window's separator rows of ~190
 // leading outside terms, r05 stamps); here a term is a load and a subtraction.  Same terms, same
 // order: bit-identical.
-// Round 6: the batches are double-buffered -- batch b + 1's loads are in flight while batch b is
-// subtracted (two register sets, the loop unrolled by two so neither is copied), so a row's
-// chain of dependent subtractions no longer stops for an LDS round trip every 16 terms (the
-// +-64 window's chained forward tasks: ~5 K fold cycles for ~160 leading terms per row).  The
-// loads of a batch past the row's last full one are clamped into the row (never used).
 template <int TPB>
 __device__ __forceinline__ void fold_known(SweepLds &S, int nr, int tid) {
-    // 2 x 8 values in flight: the kernels' register budget (a 2 x 16 form took the upper kernel
-    // from 88 to 120 VGPRs, one wave per SIMD fewer: slower, round 6 A/B)
-    constexpr int K = CPK_FOLD_V1 ? 16 : 8;
+    constexpr int K = 16;
     for (int i = tid; i < nr; i += TPB) {
         int e = S.p[i];
         const int e1 = S.ps[i];
         double acc = S.w[i];
-        const int nb = (e1 - e) / K;  // full batches
-        if (!CPK_FOLD_V1 && nb >= 2) {
-            const int last = e1 - K;  // the last full batch's start: a clamped batch stays in the row
-            double A[K], B[K];
-#pragma unroll
-            for (int j = 0; j < K; j++) A[j] = S.v[e + j];
-            int b = 0;
-            for (; b + 2 <= nb; b += 2) {
-                const int eb = e + (b + 1) * K, ea = min(e + (b + 2) * K, last);
-#pragma unroll
-                for (int j = 0; j < K; j++) B[j] = S.v[eb + j];
-#pragma unroll
-                for (int j = 0; j < K; j++) acc -= A[j];
-#pragma unroll
-                for (int j = 0; j < K; j++) A[j] = S.v[ea + j];
-#pragma unroll
-                for (int j = 0; j < K; j++) acc -= B[j];
-            }
-            if (b < nb) {  // an odd last full batch: loaded into A by the loop's last pass
-#pragma unroll
-                for (int j = 0; j < K; j++) acc -= A[j];
-                b++;
-            }
-            e += b * K;
-        }
         for (; e + K <= e1; e += K) {
             double v[K];
 #pragma unroll
@@ -1709,117 +1668,7 @@ __device__ __forceinline__ void levels_colsweep(SweepLds &S, int nr, int lane) {
         if (t < nr) S.w[S.lv[t]] = st.acc[q];
     }
 }
-
-// Column sweep v3 (round 6).  v2's step cost 207-353 cycles against a dependent core of about
-// 25: every take selected the accumulator, the code and the value
-// with v_cndmask pairs, and the next step's compare waited for the LDS reload of the row's next
-// entry (s_waitcnt lgkmcnt before the compare, in the ISA).  Here each row slot keeps its head
-// entry (code c, value v) AND the entry after it (cn, vn) in registers, so a step's compare and
-// its multiply-subtract never wait on LDS: a take shifts cn/vn into c/v and issues the load of
-// the following entry, which the next take needs one step later at the earliest.  The take is
-// an exec-masked region (a divergent branch, skipped when no lane of the slot takes), so a step
-// costs per slot a compare, and for takers one multiply, one subtract, the shift and one load
-// pair.  DRAIN blocks (outside runs behind in-block terms, ~8 % of the steps on the +-64
-// window's first upper round) keep v2's drain trips for the runs.  Same terms, same order:
-// bit-identical to v2 and to the row-order oracle.
-template <int RPL>
-struct ColState3 {
-    double acc[RPL], v[RPL], vn[RPL];
-    int e[RPL], e1[RPL], c[RPL], cn[RPL], pn[RPL];  // pn: the entry (cn, vn) holds
-};
-// the entry after head e (code c): the next one, or (DRAIN: in-block heads carry their run of
-// outside entries) the one after the run; clamped to the block's padding (code R: never taken)
-template <bool DRAIN>
-__device__ __forceinline__ int cs3_next(int e, int c, int ne) {
-    return min(DRAIN ? e + 1 + ((c >> 8) & kCsRunMax) : e + 1, ne);
-}
-// A take shifts (cn, vn) into the head and advances pn; the entry at pn is then (re)loaded
-// unconditionally, outside the taken branch, into the same registers every step -- a load whose
-// target is merged with the old value at the branch join made the compiler copy it there, after
-// an s_waitcnt on the load (seen in the ISA).  The reload is used at the row's next take, one
-// step later at the earliest.
-template <int Q, int RPL, bool DRAIN>
-__device__ __forceinline__ void colsweep3_steps(ColState3<RPL> &st, const SweepLds &S, int nr, int ne) {
-    if constexpr (Q < RPL) {
-        const int jn = min(kWave, nr - Q * kWave);
-        for (int jj = 0; jj < jn; jj++) {
-            const int t = Q * kWave + jj;
-            const double x = lane_bcast(st.acc[Q], jj);  // the row of step t: every term taken
-            int rs[RPL], rk[RPL];  // DRAIN: this step's runs (first entry, length)
-            int km = 0;
-#pragma unroll
-            for (int q = Q; q < RPL; q++) {
-                const bool in = (st.c[q] & kCsStep) == t;  // an in-block term at its step
-                // non-DRAIN: an outside term at the head is taken by any step, against 1.0 (v * 1.0 = v)
-                const bool tk = st.e[q] < st.e1[q] && (DRAIN ? in : (in || (st.c[q] & kCsOut)));
-                // DRAIN: the run behind a taken term (its entries follow it; the layout counts a
-                // run only up to the row's next in-block entry or its end, mark_dataflow)
-                if (DRAIN) rs[q] = st.e[q] + 1, rk[q] = (st.c[q] >> 8) & kCsRunMax;
-#if CPK_COLSWEEP_BRANCH
-                if (tk) {
-                    const double xs = (DRAIN || in) ? x : 1.0;
-                    st.acc[q] = st.acc[q] - st.v[q] * xs;
-                    st.e[q] = st.pn[q], st.c[q] = st.cn[q], st.v[q] = st.vn[q];
-                    st.pn[q] = cs3_next<DRAIN>(st.pn[q], st.cn[q], ne);
-                }
-#else
-                // branch-free (one basic block per step: the slots' operations interleave; an
-                // exec-masked region per slot measured 3.5 % slower on the +-64 window, round 6)
-                {
-                    const double xs = (DRAIN || in) ? x : 1.0;
-                    const double a2 = st.acc[q] - st.v[q] * xs;
-                    const int pn2 = cs3_next<DRAIN>(st.pn[q], st.cn[q], ne);
-                    st.acc[q] = tk ? a2 : st.acc[q];
-                    st.e[q] = tk ? st.pn[q] : st.e[q];
-                    st.c[q] = tk ? st.cn[q] : st.c[q];
-                    st.v[q] = tk ? st.vn[q] : st.v[q];
-                    st.pn[q] = tk ? pn2 : st.pn[q];
-                }
-#endif
-                st.cn[q] = (uint16_t)S.c[st.pn[q]], st.vn[q] = S.v[st.pn[q]];
-                if (DRAIN) rk[q] = tk ? rk[q] : 0, km = max(km, rk[q]);
-            }
-            if (DRAIN && __any(km > 0)) {  // the runs behind this step's in-block terms, in order
-                for (int j0 = 0; __any(j0 < km); j0 += 4) {
-                    double u[RPL][4];
-#pragma unroll
-                    for (int q = Q; q < RPL; q++)
-#pragma unroll
-                        for (int i = 0; i < 4; i++) u[q][i] = S.v[j0 + i < rk[q] ? rs[q] + j0 + i : rs[q]];
-#pragma unroll
-                    for (int q = Q; q < RPL; q++)
-#pragma unroll
-                        for (int i = 0; i < 4; i++) st.acc[q] = j0 + i < rk[q] ? st.acc[q] - u[q][i] : st.acc[q];
-                }
-            }
-        }
-        colsweep3_steps<Q + 1, RPL, DRAIN>(st, S, nr, ne);
-    }
-}
-template <int RPL, bool DRAIN>
-__device__ __forceinline__ void levels_colsweep3(SweepLds &S, int nr, int ne, int lane) {
-    ColState3<RPL> st;
-#pragma unroll
-    for (int q = 0; q < RPL; q++) {
-        const int t = lane + q * kWave;
-        const int k = t < nr ? S.lv[t] : 0;
-        st.e[q] = t < nr ? S.ps[k] : ne, st.e1[q] = t < nr ? S.p[k + 1] : ne;
-        st.acc[q] = S.w[k];
-        st.c[q] = (uint16_t)S.c[st.e[q]], st.v[q] = S.v[st.e[q]];  // e <= e1 <= ne: inside the padded image
-        st.pn[q] = cs3_next<DRAIN>(st.e[q], st.c[q], ne);
-        st.cn[q] = (uint16_t)S.c[st.pn[q]], st.vn[q] = S.v[st.pn[q]];
-    }
-    colsweep3_steps<0, RPL, DRAIN>(st, S, nr, ne);
-#pragma unroll
-    for (int q = 0; q < RPL; q++) {
-        const int t = lane + q * kWave;
-        if (t < nr) S.w[S.lv[t]] = st.acc[q];
-    }
-}
-
-__device__ __forceinline__ void colsweep_dispatch(SweepLds &S, int nr, int ne, int lane, bool drain) {
-#if CPK_COLSWEEP_V2
-    (void)ne;
+__device__ __forceinline__ void colsweep_dispatch(SweepLds &S, int nr, int lane, bool drain) {
     if (drain) {
         if (nr <= kWave) levels_colsweep<1, true>(S, nr, lane);
         else if (nr <= 2 * kWave) levels_colsweep<2, true>(S, nr, lane);
@@ -1829,19 +1678,6 @@ __device__ __forceinline__ void colsweep_dispatch(SweepLds &S, int nr, int ne, i
         else if (nr <= 2 * kWave) levels_colsweep<2, false>(S, nr, lane);
         else levels_colsweep<4, false>(S, nr, lane);
     }
-#else
-    // v3 at up to two rows per lane (its per-row state in registers: the kernels' budget keeps
-    // five waves per SIMD); wider blocks (rare) keep v2
-    if (drain) {
-        if (nr <= kWave) levels_colsweep3<1, true>(S, nr, ne, lane);
-        else if (nr <= 2 * kWave) levels_colsweep3<2, true>(S, nr, ne, lane);
-        else levels_colsweep<4, true>(S, nr, lane);
-    } else {
-        if (nr <= kWave) levels_colsweep3<1, false>(S, nr, ne, lane);
-        else if (nr <= 2 * kWave) levels_colsweep3<2, false>(S, nr, ne, lane);
-        else levels_colsweep<4, false>(S, nr, lane);
-    }
-#endif
 }
 
 // The level phase, out of LDS.  Per level every thread takes whole rows and consumes a row's
@@ -2425,7 +2261,7 @@ __device__ __forceinline__ void upper_block(
     // (a single wave's LDS accesses complete in program order) the chain is LDS latency only;
     // narrow levels give each row a lane group (levels_grouped)
     if (tid < kWave) {
-        if (cs) colsweep_dispatch(S, nr, ne, tid, m.l1 & (BWD ? kMetaCoBwd : kMetaCoFwd));
+        if (cs) colsweep_dispatch(S, nr, tid, m.l1 & (BWD ? kMetaCoBwd : kMetaCoFwd));
         else if (CPK_UPPER_DATAFLOW && (m.l1 & (BWD ? kMetaDfBwd : kMetaDfFwd)))
             levels_dataflow<BWD, CPK_DF_CH(BWD), true, RMAX / kWave>(S, nr, R, ne, tid);
         else if (CPK_UPPER_GROUP(BWD)) levels_grouped<CPK_UPPER_CH(BWD), BWD, true>(S, nl, false, tid);
@@ -2563,7 +2399,7 @@ __device__ __forceinline__ void last_block(
     if (uf.p) fold_known<TPB>(S, nr, tid);
     else fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (csf) colsweep_dispatch(S, nr, nef, tid, m.l1 & kMetaCoFwd);
+        if (csf) colsweep_dispatch(S, nr, tid, m.l1 & kMetaCoFwd);
         else if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfFwd)) levels_dataflow<false, CPK_DF_CH(false), true, RMAX / kWave>(S, nr, R, nef, tid);
         else if (CPK_UPPER_GROUP(false)) levels_grouped<CPK_UPPER_CH(false), false, true>(S, nl, false, tid);
         else sweep_levels<kWave, false, true, CPK_UPPER_CH(false), true, true>(S, nl, false, tid);
@@ -2601,7 +2437,7 @@ __device__ __forceinline__ void last_block(
     if (uf.p) fold_known<TPB>(S, nr, tid);
     else fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
-        if (csb) colsweep_dispatch(S, nr, neb, tid, m.l1 & kMetaCoBwd);
+        if (csb) colsweep_dispatch(S, nr, tid, m.l1 & kMetaCoBwd);
         else if (CPK_UPPER_DATAFLOW && (m.l1 & kMetaDfBwd)) levels_dataflow<true, CPK_DF_CH(true), true, RMAX / kWave>(S, nr, R, neb, tid);
         else if (CPK_UPPER_GROUP(true)) levels_grouped<CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
         else sweep_levels<kWave, true, true, CPK_UPPER_CH(true), true, true>(S, nl, false, tid);
