@@ -243,18 +243,24 @@ def main(argv=None):
         return int(st.niters)
 
     setup_s = time.perf_counter() - t_setup
-    for _ in range(args.warmup):
-        step()
-    if dist:
-        dist.barrier()
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    iters = 0
-    loop_ms = 0.0
-    for _ in range(args.steps):
-        iters += step()
-        loop_ms += st.loop_ms
-    ctx.synchronize()
+    try:
+        for _ in range(args.warmup):
+            step()
+        if dist:
+            dist.barrier()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        iters = 0
+        loop_ms = 0.0
+        for _ in range(args.steps):
+            iters += step()
+            loop_ms += st.loop_ms
+        ctx.synchronize()
+    except cpk.CpkError as e:
+        # a distributed solve's status agreement makes every rank return the same error
+        # (INTEGRATION.md section 5): every rank reports it and exits non-zero, none waits
+        print(f"bench: solve failed on rank {rank}: {e}", file=sys.stderr, flush=True)
+        sys.exit(4)
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
