@@ -1499,56 +1499,6 @@ __device__ __forceinline__ void fold_known(SweepLds &S, int nr, int tid) {
     __syncthreads();
 }
 
-// fold_known through a transposed copy (round 6).  A row's leading terms sit contiguously in the
-// image, one row after another, and fold_known gives each row to one thread: at step j the
-// lanes read entry p[k] + j of their rows, addresses a row length apart -- for the +-64 window's
-// chained separator blocks (~15 rows of ~130-200 leading terms) the rows are nearly equally
-// long, so the lanes hit the same LDS bank and each load serialises (the fold took ~5 K cycles
-// for ~130 terms a row, ~37 cycles a term).  Here the terms are first copied, consecutive
-// threads taking consecutive entries of one row (conflict-free reads), to T[j * nr + k], and
-// each row's thread then reads T's column k: at every step the lanes read consecutive words.
-// Used where the launch has LDS beyond its image (the sweep chain: one workgroup per CU, §7d)
-// and the rows are few enough to share the threads; the same terms in the same order.
-template <int TPB>
-__device__ __forceinline__ void fold_known_t(SweepLds &S, int nr, int tid, double *T, int tcap) {
-    __shared__ int s_maxl;
-    if (T && tcap > 0 && nr > 0 && nr * 4 <= TPB) {
-        if (tid == 0) s_maxl = 0;
-        __syncthreads();
-        int ml = 0;
-        for (int i = tid; i < nr; i += TPB) ml = max(ml, S.ps[i] - S.p[i]);
-        if (ml) atomicMax(&s_maxl, ml);
-        __syncthreads();
-        const int maxl = s_maxl;
-        if (maxl >= 16 && (int64_t)maxl * nr <= tcap) {
-            const int L = TPB / nr, k = tid / L, jj = tid - k * L;
-            if (k < nr) {
-                const int p0 = S.p[k], lk = S.ps[k] - p0;
-#pragma unroll 4
-                for (int j = jj; j < lk; j += L) T[j * nr + k] = S.v[p0 + j];
-            }
-            __syncthreads();
-            for (int i = tid; i < nr; i += TPB) {
-                const int lk = S.ps[i] - S.p[i];
-                double acc = S.w[i];
-                int j = 0;
-                for (; j + 16 <= lk; j += 16) {
-                    double v[16];
-#pragma unroll
-                    for (int u = 0; u < 16; u++) v[u] = T[(j + u) * nr + i];
-#pragma unroll
-                    for (int u = 0; u < 16; u++) acc -= v[u];
-                }
-                for (; j < lk; j++) acc -= T[j * nr + i];
-                S.w[i] = acc;
-            }
-            __syncthreads();
-            return;
-        }
-    }
-    fold_known<TPB>(S, nr, tid);
-}
-
 // the LDS image of an upper-round launch: rows (the 1.0 slot's index) and entries it holds
 struct Img {
     int R, CAP;
@@ -2222,9 +2172,8 @@ __device__ __forceinline__ void upper_block(
     const uint32_t *__restrict__ ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
     double *w, double *out, int sched_in, double *ys, double *xs, const PackArgs &pk, const UFold &uf, int64_t b,
-    const Img &img, const Wait &wait = Wait{}, int tcap = 0) {
+    const Img &img, const Wait &wait = Wait{}) {
     // the LDS image of this launch (Img: its blocks' largest rows / entries, <= the kernel's R / CAP)
-    // tcap: doubles of LDS past the image (the sweep chain's; fold_known_t)
     constexpr int RMAX = RPU * TPB;
     const int R = img.R, CAP = img.CAP;
 #ifdef CPK_PIPE_STAMPS
@@ -2305,7 +2254,7 @@ __device__ __forceinline__ void upper_block(
     }
     __syncthreads();
     CPK_UP_STAMP(0);
-    if (uf.p) fold_known_t<TPB>(S, nr, tid, reinterpret_cast<double *>(smem + sweep_lds_bytes_dev(R, CAP)), tcap);
+    if (uf.p) fold_known<TPB>(S, nr, tid);
     else fold_prefix<TPB, 1>(S, nr, -1, R);
     CPK_UP_STAMP(1);
     // levels on one wave: a level holds a few rows, and without a workgroup barrier per level
@@ -2372,7 +2321,7 @@ __device__ __forceinline__ void last_block(
     const uint32_t *__restrict__ bptr, const int32_t *__restrict__ bcol, const double *__restrict__ bval,
     const double *__restrict__ D, const int32_t *__restrict__ perm, const double *__restrict__ xin, int64_t neg_from,
     int sched_in, double *xs, double *w, double *out, double *ys, const UFold &uf, const Img &img,
-    const Wait &wait = Wait{}, int tcap = 0) {
+    const Wait &wait = Wait{}) {
     constexpr int RMAX = RPU * TPB;
     const int R = img.R, CAP = img.CAP;
     const int r0 = m.r0, r1 = m.r1, nr = r1 - r0, nl = (m.l1 & kMetaL1Mask) - m.l0;
@@ -2447,7 +2396,7 @@ __device__ __forceinline__ void last_block(
         }
     }
     __syncthreads();
-    if (uf.p) fold_known_t<TPB>(S, nr, tid, reinterpret_cast<double *>(smem + sweep_lds_bytes_dev(R, CAP)), tcap);
+    if (uf.p) fold_known<TPB>(S, nr, tid);
     else fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
         if (csf) colsweep_dispatch(S, nr, tid, m.l1 & kMetaCoFwd);
@@ -2485,7 +2434,7 @@ __device__ __forceinline__ void last_block(
         }
     }
     __syncthreads();
-    if (uf.p) fold_known_t<TPB>(S, nr, tid, reinterpret_cast<double *>(smem + sweep_lds_bytes_dev(R, CAP)), tcap);
+    if (uf.p) fold_known<TPB>(S, nr, tid);
     else fold_prefix<TPB, 1>(S, nr, -1, R);
     if (tid < kWave) {
         if (csb) colsweep_dispatch(S, nr, tid, m.l1 & kMetaCoBwd);
@@ -2588,9 +2537,6 @@ constexpr uint32_t kChainSpinCap = CPK_CHAIN_SPIN_CAP;  // polls (2^20: with the
 #ifndef CPK_CHAIN_ACQUIRE
 #define CPK_CHAIN_ACQUIRE 0
 #endif
-#ifndef CPK_CHAIN_FOLD_T
-#define CPK_CHAIN_FOLD_T 1  // chained tasks fold through a transposed copy in the LDS past the image (fold_known_t)
-#endif
 #ifndef CPK_CHAIN_LDS_MIN
 #define CPK_CHAIN_LDS_MIN 83968
 #endif
@@ -2613,7 +2559,6 @@ struct ChainArgs {
     const int32_t *task, *dptr, *didx;
     uint32_t *flag, *ctrl;
     int ntask;
-    int tcap;  // doubles of LDS past the kernel image (fold_known_t's transposed copy)
 };
 __device__ __forceinline__ uint32_t ld_agent32(const uint32_t *p) {
     return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2677,13 +2622,13 @@ __global__ __launch_bounds__(TPB) void sptrsv_chain_kernel(
     };
     if (kind == 0)
         upper_block<TPB, RPU, EPU, false, false, true>(smem, meta[b], lvl_row, fptr, fcol, fval, D, perm, xin, neg_from, w,
-                                                       nullptr, sched_in, nullptr, xs, pk, uf, b, img, wait, ch.tcap);
+                                                       nullptr, sched_in, nullptr, xs, pk, uf, b, img, wait);
     else if (kind == 1)
         last_block<TPB, RPU, EPU, ADD, true>(smem, meta[b], lvl_row, fptr, fcol, fval, bptr, bcol, bval, D, perm, xin,
-                                             neg_from, sched_in, xs, w, out, ys, uf, img, wait, ch.tcap);
+                                             neg_from, sched_in, xs, w, out, ys, uf, img, wait);
     else
         upper_block<TPB, RPU, EPU, true, ADD, true>(smem, meta[b], lvl_row, bptr, bcol, bval, D, perm, nullptr, 0, w, out,
-                                                    0, ys, nullptr, pk, uf, b, img, wait, ch.tcap);
+                                                    0, ys, nullptr, pk, uf, b, img, wait);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w stores done
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2845,8 +2790,7 @@ static void launch_chain_t(Ctx &c, const DFactor &F, int kind, const FwdIn &in, 
     const Img img{RPU * TPB, EPU * TPB};  // narrow rounds: every task resident at the kernel's image
     const BlkMeta *meta = reinterpret_cast<const BlkMeta *>(F.meta.p);
     const size_t ldsb = std::max<size_t>(img_bytes(img), (size_t)CPK_CHAIN_LDS_MIN);
-    const int tcap = CPK_CHAIN_FOLD_T ? (int)((ldsb - img_bytes(img)) / sizeof(double)) : 0;
-    const ChainArgs ch{h.task.p, h.dptr.p, h.didx.p, h.flag.p, h.ctrl.p, (int)h.ntask, tcap};
+    const ChainArgs ch{h.task.p, h.dptr.p, h.didx.p, h.flag.p, h.ctrl.p, (int)h.ntask};
     if (add)
         hipLaunchKernelGGL((sptrsv_chain_kernel<TPB, RPU, EPU, true>), dim3((unsigned)h.ntask), dim3(TPB), ldsb, c.stream,
                            ch, meta, F.lvl_row.p, F.fptr.p, F.fcol.p, F.fval.p, F.bptr.p, F.bcol.p, F.bval.p, F.D.p,

@@ -14,7 +14,7 @@ import cpkrylov_amd as cpk  # noqa: E402
 from cpkrylov_amd import _lib  # noqa: E402
 from cpkrylov_amd.synthetic import saddle_system  # noqa: E402
 
-S = saddle_system(int(os.environ.get("N", "10000000")))
+S = saddle_system(int(os.environ.get("N", "10000000")), window=int(os.environ.get("W", "4")))
 ctx = cpk.Context(device=0)
 A, Cm = cpk.Matrix(S["Q"], ctx), cpk.Matrix(S["C"], ctx)
 M = cpk.opLDL2(S["G"], S["B"], -S["C"], ctx=ctx)
