@@ -1,6 +1,6 @@
 """Per-block cycles of the round-0 sweep kernels at S10 (diagnostic library built with
 -DCPK_PIPE_STAMPS, loaded through CPK_LIB_PATH), against the block's static features (levels,
-rows, entries, Kps entries), and a least-squares cost model per kernel variant: the input of
+rows, entries, Kps entries; env W = B window, default 4), and a least-squares cost model per kernel variant: the input of
 the host-side longest-processing-time assignment of round-0 blocks to workgroups.
 Writes gpurun_out/blk_cycles.npz and prints the fits as JSON."""
 import ctypes as C
@@ -16,7 +16,7 @@ import cpkrylov_amd as cpk  # noqa: E402
 from cpkrylov_amd import _lib  # noqa: E402
 from cpkrylov_amd.synthetic import saddle_system  # noqa: E402
 
-S = saddle_system(int(os.environ.get("N", "10000000")))
+S = saddle_system(int(os.environ.get("N", "10000000")), window=int(os.environ.get("W", "4")))
 H = cpk.analyze(S["G"], S["B"], -S["C"])
 rp, bl, lr, order, perm, L = H["round_ptr"], H["blk_lvl"], H["lvl_row"], H["order"], H["perm"], H["L"]
 nb = int(rp[1] - rp[0])
@@ -41,7 +41,7 @@ buf = np.zeros(4 * KMAX, np.uint64)
 got = C.c_int64(0)
 _lib.check(_lib.lib.cpk_debug_blk_cycles(buf.ctypes.data_as(C.POINTER(C.c_uint64)), buf.size, C.byref(got)))
 cyc = buf.reshape(4, KMAX)[:, bl[:nb]].astype(np.float64)
-np.savez(os.path.join(os.environ.get("OUT", "gpurun_out"), "blk_cycles.npz"), cyc=cyc, rows=rows, nl=nl, fe=fe, be=be,
+np.savez(os.path.join(os.environ.get("OUT", "gpurun_out"), f"blk_cycles_w{os.environ.get('W', '4')}.npz"), cyc=cyc, rows=rows, nl=nl, fe=fe, be=be,
          ke=ke)
 names = ["fwd", "fwd_resid", "bwd", "bwd_add"]
 for v in range(4):
