@@ -1571,15 +1571,20 @@ struct ColState {
 template <int Q, int RPL>
 __device__ __forceinline__ void colsweep_run_load(const ColState<RPL> &st, const SweepLds &S, int j0, double (&u)[4][4]) {
     if constexpr (Q < RPL) {
+        // one base per row and trip, clamped to the run's end (e + k <= e1 <= ne: the four reads
+        // stay inside the padded image), the four loads at immediate offsets (two ds_read2_b64)
+        const double *b = S.v + st.e[Q] + min(j0, st.k[Q]);
 #pragma unroll
-        for (int i = 0; i < 4; i++) u[Q][i] = S.v[j0 + i < st.k[Q] ? st.e[Q] + j0 + i : st.e[Q]];
+        for (int i = 0; i < 4; i++) u[Q][i] = b[i];
     }
 }
 template <int Q, int RPL>
 __device__ __forceinline__ void colsweep_run_sub(ColState<RPL> &st, int j0, const double (&u)[4][4]) {
     if constexpr (Q < RPL) {
+        // a term past the run subtracts +0.0: acc - 0.0 == acc, the sign of a zero acc included
+        const int kk = st.k[Q] - j0;
 #pragma unroll
-        for (int i = 0; i < 4; i++) st.acc[Q] = j0 + i < st.k[Q] ? st.acc[Q] - u[Q][i] : st.acc[Q];
+        for (int i = 0; i < 4; i++) st.acc[Q] = st.acc[Q] - (i < kk ? u[Q][i] : 0.0);
     }
 }
 template <int Q, int RPL>
