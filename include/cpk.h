@@ -141,9 +141,13 @@ int cpk_ctx_create_sim(int device, cpk_simgroup group, int rank, int nranks, cpk
  * no_sched_resid, no_fused_resid, r0_xcd_chunk, tsolve_global, tsolve_sweep,
  * no_piggy, no_halo_merge, no_graph, no_fuse_last, no_tkr, no_minres_fuse, dist_graph, batch,
  * dist1 (a 1-rank communicator runs the distributed kernels; set before building operators),
- * profile_fwd_sched (diagnostic), sweep_set ("0" returns sweep to the per-path default).
+ * profile_fwd_sched (diagnostic), sweep_set ("0" returns sweep to the per-path default),
+ * profile_passes (diagnostic: cpdqgmres runs eagerly with events between its passes, read by
+ * cpk_debug_pass_times), fail_inject ("rank:site[:n]", site setup / batch / chain: a test hook
+ * that makes one rank of a distributed solve fail at that point).
  * Booleans as "0"/"1".  A distributed preconditioner allgathers a hash of its plan and of every
- * option at creation and fails (CPK_ERR_ARGS) on every rank unless all ranks agree. */
+ * option but fail_inject at creation and fails (CPK_ERR_ARGS) on every rank unless all ranks
+ * agree. */
 int cpk_ctx_set_option(cpk_ctx ctx, const char *name, const char *value);
 int cpk_ctx_get_option(cpk_ctx ctx, const char *name, char *buf, size_t cap);
 /* Every engine option of the context as "name=value;name=value;..." (the form cpk_analyze's
