@@ -457,24 +457,28 @@ def cpu_baseline(S, b1, M_gpu, args, hist_gpu, niters_gpu):
         h = st1["residHistory"]
         h0 = h[0]
         dev = float(np.max(np.abs(h - hist_gpu[:len(h)])) / h0) if len(h) == len(hist_gpu) else None
-        # sensitivity band: the OpenMP leg (different dot rounding) and two perturbed rhs
-        band = 0.0
+        # sensitivity band: the OpenMP leg (different dot rounding) and four perturbed rhs; each
+        # sample's own deviation is reported, so the GPU's can be read against their spread
+        samples = []
         if stT["solved"] and len(stT["residHistory"]) == len(h):
-            band = float(np.max(np.abs(stT["residHistory"] - h)) / h0)
+            samples.append(float(np.max(np.abs(stT["residHistory"] - h)) / h0))
         rng = np.random.default_rng(12345)
-        for _ in range(2):
+        for _ in range(4):
             bp = b1 * (1 + 1e-15 * rng.standard_normal(b1.shape[0]))
             _, _, _, _, sp_ = leg(host["threads"], 0, opts_extra={}, rhs=bp)
             hp = sp_["residHistory"]
             L_ = min(len(hp), len(h))
-            band = max(band, float(np.max(np.abs(hp[:L_] - h[:L_])) / h0))
+            samples.append(float(np.max(np.abs(hp[:L_] - h[:L_])) / h0))
+        band = max(samples) if samples else 0.0
         tol = max(1e-8, 10 * band)
         parity = {"niters_gpu": niters_gpu, "niters_oracle": it1, "niters_equal": niters_gpu == it1,
-                  "max_hist_dev_over_h0": dev, "band_over_h0": band, "tolerance_over_h0": tol,
+                  "max_hist_dev_over_h0": dev, "band_over_h0": band, "band_samples_over_h0": samples,
+                  "tolerance_over_h0": tol,
                   "pass": bool(niters_gpu == it1 and dev is not None and dev <= tol),
                   "method": "serial oracle run to convergence = reference; band = max history deviation of "
-                            "the OpenMP leg and of two rhs perturbed by 1e-15 relative; tolerance = "
-                            "max(1e-8, 10 x band) (tests/test_gpu_parity.py)"}
+                            "the OpenMP leg and of four rhs perturbed by 1e-15 relative (each in "
+                            "band_samples_over_h0, the OpenMP leg first); tolerance = max(1e-8, 10 x band) "
+                            "(tests/test_gpu_parity.py)"}
     return cpu, parity
 
 
