@@ -470,9 +470,17 @@ def cpu_baseline(S, b1, M_gpu, args, hist_gpu, niters_gpu):
             L_ = min(len(hp), len(h))
             samples.append(float(np.max(np.abs(hp[:L_] - h[:L_])) / h0))
         band = max(samples) if samples else 0.0
+        # one perturbed rhs on the serial leg (the reference's own order): what the perturbation
+        # alone moves, against the order changes the samples above carry
+        bp = b1 * (1 + 1e-15 * rng.standard_normal(b1.shape[0]))
+        _, _, _, _, sp_ = leg(1, 0, opts_extra={}, rhs=bp)
+        hp = sp_["residHistory"]
+        L_ = min(len(hp), len(h))
+        serial_pert = float(np.max(np.abs(hp[:L_] - h[:L_])) / h0)
         tol = max(1e-8, 10 * band)
         parity = {"niters_gpu": niters_gpu, "niters_oracle": it1, "niters_equal": niters_gpu == it1,
                   "max_hist_dev_over_h0": dev, "band_over_h0": band, "band_samples_over_h0": samples,
+                  "serial_perturbed_over_h0": serial_pert,
                   "tolerance_over_h0": tol,
                   "pass": bool(niters_gpu == it1 and dev is not None and dev <= tol),
                   "method": "serial oracle run to convergence = reference; band = max history deviation of "
